@@ -1,0 +1,560 @@
+// cudasp_scan hot path for MI355X (gfx950): kernels, per-device fixed-base
+// table, scanner objects and the C ABI declared in include/cudasp_abi.h.
+//
+// Kernel pipeline for one batch of n rows (all device-resident):
+//   k_shared_secret   stage A of scan_rows.hpp: reads tweak columns (8 x n u32
+//                     each, column-major), writes t (8 x n u32).
+//   k_match           stage B: reads t, gathers from the 32 MiB fixed-base
+//                     table, compares with the outputs CSR, writes one flag per
+//                     row and (optionally) the compacted row indices via a
+//                     per-wavefront ballot + one atomic per wave.
+// Replaces the reference's ec_pmul + serialize + hash + host round trip +
+// fixed-point + check sequence (src/cudasp_gpu.cu:764-956), which crosses PCIe
+// twice per batch; here nothing leaves the device between the two kernels.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cudasp_abi.h"
+#include "scan_prepare.hpp"
+
+using namespace cudasp;
+
+#define CUDASP_VERSION_STRING "cudasp-mi355x 0.1.0 (gfx950)"
+
+// ----------------------------------------------------------------- errors
+namespace {
+thread_local std::string g_last_error;
+
+int set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return set_error(CUDASP_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                       __FILE__, __LINE__);                                                    \
+  } while (0)
+
+constexpr int BLOCK = 256;
+// Grid cap for the grid-stride kernels; also bounds the per-slot scratch.
+constexpr uint32_t MAX_BLOCKS = 4096;
+}  // namespace
+
+// ----------------------------------------------------------------- kernels
+
+__global__ __launch_bounds__(BLOCK) void k_shared_secret(const uint32_t* __restrict__ tx,
+                                                         const uint32_t* __restrict__ ty, uint32_t n,
+                                                         const int8_t* __restrict__ naf, ScanConsts k,
+                                                         uint32_t* __restrict__ vscr,
+                                                         uint32_t* __restrict__ t_out) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  Scratch sc{vscr, stride, slot};
+  for (uint32_t row = slot; row < n; row += stride) {
+    uint32_t x[8], y[8], t[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      x[j] = tx[(size_t)j * n + row];
+      y[j] = ty[(size_t)j * n + row];
+    }
+    row_shared_secret(t, x, y, naf, k.naf_len, k.mid, sc);
+#pragma unroll
+    for (int j = 0; j < 8; j++) t_out[(size_t)j * n + row] = t[j];
+  }
+}
+
+template <bool VALUES>
+__global__ __launch_bounds__(BLOCK) void k_match(const uint32_t* __restrict__ t_in, uint32_t n,
+                                                 const uint32_t* __restrict__ fb, ScanConsts k,
+                                                 const uint32_t* __restrict__ labels,
+                                                 const int64_t* __restrict__ outputs,
+                                                 const uint32_t* __restrict__ offs,
+                                                 const uint32_t* __restrict__ lens,
+                                                 uint32_t* __restrict__ lscr, uint8_t* __restrict__ flags,
+                                                 uint32_t* __restrict__ match_rows,
+                                                 uint32_t* __restrict__ match_count,
+                                                 int64_t* __restrict__ values) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  Scratch sc{lscr, stride, slot};
+  // The whole block walks the rows together so that ballots see full waves.
+  for (uint32_t row0 = blockIdx.x * blockDim.x; row0 < n; row0 += stride) {
+    const uint32_t row = row0 + threadIdx.x;
+    const bool valid = row < n;
+    bool hit = false;
+    if (valid) {
+      uint32_t t[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) t[j] = t_in[(size_t)j * n + row];
+      uint32_t off = VALUES ? 0u : offs[row];
+      uint32_t len = VALUES ? 0u : lens[row];
+      hit = row_match(t, fb, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
+      if (!VALUES) flags[row] = hit ? 1 : 0;
+    }
+    if (!VALUES && match_rows != nullptr) {
+      const uint64_t m = __ballot(hit);
+      if (m) {
+        const uint32_t lane = threadIdx.x & 63u;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(match_count, (uint32_t)__popcll(m));
+        base = __shfl(base, 0);
+        if (hit) match_rows[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = row;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_fb_build(const uint32_t* __restrict__ bases,
+                                                    uint32_t* __restrict__ table) {
+  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (uint32_t)(FB_WINDOWS * FB_ENTRIES)) return;
+  const uint32_t window = idx / FB_ENTRIES, j = idx % FB_ENTRIES;
+  ge Q;
+  ge_from_words(Q, bases + window * 16);
+  uint32_t out[16];
+  fb_build_entry(out, Q, j);
+  uint4* dst = reinterpret_cast<uint4*>(table + (size_t)idx * FB_WORDS);
+#pragma unroll
+  for (int q = 0; q < 4; q++) dst[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rows_to_cols(const uint8_t* __restrict__ rows, uint32_t n,
+                                                        uint32_t* __restrict__ x, uint32_t* __restrict__ y) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < n; row += stride) {
+    const uint4* src = reinterpret_cast<const uint4*>(rows + (size_t)row * 64);
+    uint32_t w[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      uint4 v = src[q];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      x[(size_t)j * n + row] = w[j];
+      y[(size_t)j * n + row] = w[8 + j];
+    }
+  }
+}
+
+// ------------------------------------------------------------- host helpers
+namespace {
+
+// ------------------------------------------------ per-device fixed-base table
+struct DeviceTable {
+  uint32_t* table = nullptr;
+};
+std::mutex g_table_mutex;
+std::map<int, DeviceTable> g_tables;
+
+int ensure_device_table(int device, const uint32_t** out) {
+  std::lock_guard<std::mutex> lock(g_table_mutex);
+  auto it = g_tables.find(device);
+  if (it != g_tables.end()) {
+    *out = it->second.table;
+    return CUDASP_OK;
+  }
+  std::vector<uint32_t> bases = fb_window_bases();
+  uint32_t* d_bases = nullptr;
+  uint32_t* d_table = nullptr;
+  HIP_TRY(hipMalloc(&d_bases, bases.size() * 4));
+  HIP_TRY(hipMalloc(&d_table, (size_t)FB_WINDOWS * FB_ENTRIES * FB_WORDS * 4));
+  HIP_TRY(hipMemcpy(d_bases, bases.data(), bases.size() * 4, hipMemcpyHostToDevice));
+  const uint32_t total = FB_WINDOWS * FB_ENTRIES;
+  hipLaunchKernelGGL(k_fb_build, dim3((total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, 0, d_bases, d_table);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipFree(d_bases));
+  g_tables[device].table = d_table;
+  *out = d_table;
+  return CUDASP_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ scanner
+struct cudasp_scanner {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  ScanConsts consts{};
+  const uint32_t* d_fb = nullptr;
+  int8_t* d_naf = nullptr;
+  uint32_t* d_labels = nullptr;
+  uint32_t label_count = 0;
+  uint32_t capacity = 0;
+  uint32_t* d_t = nullptr;         // 8 x capacity
+  uint32_t* d_vscratch = nullptr;  // VB_SCRATCH_WORDS x slots
+  uint32_t* d_lscratch = nullptr;  // 10 L x slots
+  uint32_t slots = 0;
+  // host-path staging
+  uint8_t* d_rows = nullptr;   // capacity x 64
+  uint32_t* d_tx = nullptr;    // 8 x capacity
+  uint32_t* d_ty = nullptr;
+  uint8_t* d_flags = nullptr;  // capacity
+  uint32_t* d_offs = nullptr;
+  uint32_t* d_lens = nullptr;
+  int64_t* d_outputs = nullptr;
+  size_t outputs_cap = 0;
+};
+
+namespace {
+
+uint32_t grid_for(uint32_t n) {
+  uint32_t blocks = (n + BLOCK - 1) / BLOCK;
+  if (blocks > MAX_BLOCKS) blocks = MAX_BLOCKS;
+  if (blocks == 0) blocks = 1;
+  return blocks;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+void free_scanner(cudasp_scanner* s) {
+  if (!s) return;
+  DeviceGuard g(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  void* ptrs[] = {s->d_naf, s->d_labels, s->d_t, s->d_vscratch, s->d_lscratch, s->d_rows,
+                  s->d_tx,  s->d_ty,     s->d_flags, s->d_offs, s->d_lens,    s->d_outputs};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+int launch_pipeline(cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, const int64_t* outputs,
+                    const uint32_t* offs, const uint32_t* lens, uint32_t n, uint8_t* flags, uint32_t* match_rows,
+                    uint32_t* match_count, int64_t* values, uint32_t* t_out, hipStream_t st) {
+  if (n == 0) return CUDASP_OK;
+  if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
+  uint32_t blocks = grid_for(n);
+  if (blocks * BLOCK > s->slots) blocks = s->slots / BLOCK;
+  uint32_t* t = t_out ? t_out : s->d_t;
+  hipLaunchKernelGGL(k_shared_secret, dim3(blocks), dim3(BLOCK), 0, st, tx, ty, n, s->d_naf, s->consts,
+                     s->d_vscratch, t);
+  HIP_TRY(hipGetLastError());
+  if (values) {
+    hipLaunchKernelGGL(k_match<true>, dim3(blocks), dim3(BLOCK), 0, st, t, n, s->d_fb, s->consts, s->d_labels,
+                       nullptr, nullptr, nullptr, s->d_lscratch, nullptr, nullptr, nullptr, values);
+  } else {
+    hipLaunchKernelGGL(k_match<false>, dim3(blocks), dim3(BLOCK), 0, st, t, n, s->d_fb, s->consts, s->d_labels,
+                       outputs, offs, lens, s->d_lscratch, flags, match_rows, match_count, nullptr);
+  }
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cudasp_last_error(void) { return g_last_error.c_str(); }
+
+const char* cudasp_version(void) { return CUDASP_VERSION_STRING; }
+
+int cudasp_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const uint8_t spend_public_key[64],
+                          const uint8_t* label_keys, uint32_t label_count, uint32_t max_rows,
+                          cudasp_scanner** out) {
+  g_last_error.clear();
+  if (!out || !scan_private_key || !spend_public_key || (label_count > 0 && !label_keys))
+    return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  int ndev = cudasp_device_count();
+  if (ndev <= 0) return set_error(CUDASP_ERR_NO_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= ndev) return set_error(CUDASP_ERR_INVALID_ARG, "device %d out of range (%d devices)", device, ndev);
+  if (max_rows == 0) max_rows = 1;
+
+  // --- host-side constants -------------------------------------------------
+  cudasp_scanner* s = new cudasp_scanner();
+  std::vector<int8_t> naf;
+  std::vector<uint32_t> labels;
+  std::string err;
+  int prc = prepare_scan(scan_private_key, spend_public_key, label_keys, label_count, s->consts, naf, labels, err);
+  if (prc != CUDASP_OK) {
+    delete s;
+    return set_error(prc, "%s", err.c_str());
+  }
+  s->device = device;
+  s->capacity = max_rows;
+  s->label_count = label_count;
+
+  // --- device state --------------------------------------------------------
+  DeviceGuard g(device);
+  int rc = ensure_device_table(device, &s->d_fb);
+  if (rc != CUDASP_OK) {
+    delete s;
+    return rc;
+  }
+  s->slots = grid_for(max_rows) * BLOCK;
+#define ALLOC(ptr, bytes)                                                                          \
+  do {                                                                                             \
+    hipError_t e_ = hipMalloc(&(ptr), (bytes) ? (bytes) : 4);                                      \
+    if (e_ != hipSuccess) {                                                                        \
+      free_scanner(s);                                                                             \
+      return set_error(CUDASP_ERR_HIP, "hipMalloc(%zu) failed: %s", (size_t)(bytes), hipGetErrorString(e_)); \
+    }                                                                                              \
+  } while (0)
+  ALLOC(s->d_naf, naf.size());
+  ALLOC(s->d_labels, labels.size() * 4);
+  ALLOC(s->d_t, (size_t)8 * max_rows * 4);
+  ALLOC(s->d_vscratch, (size_t)VB_SCRATCH_WORDS * s->slots * 4);
+  ALLOC(s->d_lscratch, (size_t)10 * label_count * s->slots * 4);
+#undef ALLOC
+  hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    free_scanner(s);
+    return set_error(CUDASP_ERR_HIP, "hipStreamCreate failed: %s", hipGetErrorString(e));
+  }
+  e = hipMemcpy(s->d_naf, naf.data(), naf.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(s->d_labels, labels.data(), labels.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    free_scanner(s);
+    return set_error(CUDASP_ERR_HIP, "hipMemcpy failed: %s", hipGetErrorString(e));
+  }
+  *out = s;
+  return CUDASP_OK;
+}
+
+void cudasp_scanner_destroy(cudasp_scanner* s) { free_scanner(s); }
+
+int cudasp_scanner_sync(cudasp_scanner* s) {
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  DeviceGuard g(s->device);
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  return CUDASP_OK;
+}
+
+int cudasp_scan_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint32_t* d_tweak_y,
+                       const int64_t* d_outputs, const uint32_t* d_output_offsets,
+                       const uint32_t* d_output_lengths, uint32_t n, uint8_t* d_match_flags,
+                       uint32_t* d_match_rows, uint32_t* d_match_count, void* stream) {
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  if (n == 0) return CUDASP_OK;
+  if (!d_tweak_x || !d_tweak_y || !d_output_offsets || !d_output_lengths || !d_match_flags)
+    return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
+  DeviceGuard g(s->device);
+  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  return launch_pipeline(s, d_tweak_x, d_tweak_y, d_outputs, d_output_offsets, d_output_lengths, n, d_match_flags,
+                         (d_match_rows && d_match_count) ? d_match_rows : nullptr,
+                         (d_match_rows && d_match_count) ? d_match_count : nullptr, nullptr, nullptr, st);
+}
+
+int cudasp_row_values_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint32_t* d_tweak_y, uint32_t n,
+                             uint32_t* d_t, int64_t* d_values, void* stream) {
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  if (n == 0) return CUDASP_OK;
+  if (!d_tweak_x || !d_tweak_y || !d_values) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
+  DeviceGuard g(s->device);
+  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  return launch_pipeline(s, d_tweak_x, d_tweak_y, nullptr, nullptr, nullptr, n, nullptr, nullptr, nullptr, d_values,
+                         d_t, st);
+}
+
+int cudasp_tweaks_to_columns(const uint8_t* d_tweak_rows, uint32_t n, uint32_t* d_tweak_x, uint32_t* d_tweak_y,
+                             void* stream) {
+  if (n == 0) return CUDASP_OK;
+  if (!d_tweak_rows || !d_tweak_x || !d_tweak_y) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
+  hipLaunchKernelGGL(k_rows_to_cols, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, d_tweak_rows, n,
+                     d_tweak_x, d_tweak_y);
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+int cudasp_scan_host(cudasp_scanner* s, const uint8_t* h_tweak_keys, const int64_t* h_outputs, size_t outputs_size,
+                     const uint32_t* h_output_offsets, const uint32_t* h_output_lengths, uint32_t n,
+                     uint8_t* h_match_flags) {
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  if (n == 0) return CUDASP_OK;
+  if (!h_tweak_keys || !h_output_offsets || !h_output_lengths || !h_match_flags || (outputs_size && !h_outputs))
+    return set_error(CUDASP_ERR_INVALID_ARG, "null host buffer");
+  if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
+  for (uint32_t i = 0; i < n; i++)
+    if ((size_t)h_output_offsets[i] + h_output_lengths[i] > outputs_size)
+      return set_error(CUDASP_ERR_INVALID_ARG, "row %u: outputs range [%u, +%u) exceeds outputs_size %zu", i,
+                       h_output_offsets[i], h_output_lengths[i], outputs_size);
+  DeviceGuard g(s->device);
+  if (!s->d_rows) {
+    HIP_TRY(hipMalloc(&s->d_rows, (size_t)64 * s->capacity));
+    HIP_TRY(hipMalloc(&s->d_tx, (size_t)32 * s->capacity));
+    HIP_TRY(hipMalloc(&s->d_ty, (size_t)32 * s->capacity));
+    HIP_TRY(hipMalloc(&s->d_flags, (size_t)s->capacity));
+    HIP_TRY(hipMalloc(&s->d_offs, (size_t)4 * s->capacity));
+    HIP_TRY(hipMalloc(&s->d_lens, (size_t)4 * s->capacity));
+  }
+  if (outputs_size > s->outputs_cap) {
+    if (s->d_outputs) HIP_TRY(hipFree(s->d_outputs));
+    s->d_outputs = nullptr;
+    HIP_TRY(hipMalloc(&s->d_outputs, outputs_size * 8));
+    s->outputs_cap = outputs_size;
+  }
+  hipStream_t st = s->stream;
+  HIP_TRY(hipMemcpyAsync(s->d_rows, h_tweak_keys, (size_t)64 * n, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(s->d_offs, h_output_offsets, (size_t)4 * n, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(s->d_lens, h_output_lengths, (size_t)4 * n, hipMemcpyHostToDevice, st));
+  if (outputs_size) HIP_TRY(hipMemcpyAsync(s->d_outputs, h_outputs, outputs_size * 8, hipMemcpyHostToDevice, st));
+  int rc = cudasp_tweaks_to_columns(s->d_rows, n, s->d_tx, s->d_ty, st);
+  if (rc != CUDASP_OK) return rc;
+  rc = launch_pipeline(s, s->d_tx, s->d_ty, s->d_outputs, s->d_offs, s->d_lens, n, s->d_flags, nullptr, nullptr,
+                       nullptr, nullptr, st);
+  if (rc != CUDASP_OK) return rc;
+  HIP_TRY(hipMemcpyAsync(h_match_flags, s->d_flags, n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return CUDASP_OK;
+}
+
+// ------------------------------------------------ reference three-phase ABI
+struct LegacyBatch {
+  cudasp_scanner* scanner = nullptr;
+  int64_t* d_outputs = nullptr;
+  uint32_t* d_offs = nullptr;
+  uint32_t* d_lens = nullptr;
+  uint32_t* d_tx = nullptr;
+  uint32_t* d_ty = nullptr;
+  uint8_t* d_flags = nullptr;
+  uint32_t count = 0;
+};
+
+static void words_to_bytes(uint8_t* out, const uint32_t* w, int nwords) {
+  for (int i = 0; i < nwords; i++) {
+    out[4 * i] = (uint8_t)w[i];
+    out[4 * i + 1] = (uint8_t)(w[i] >> 8);
+    out[4 * i + 2] = (uint8_t)(w[i] >> 16);
+    out[4 * i + 3] = (uint8_t)(w[i] >> 24);
+  }
+}
+
+static void free_legacy(LegacyBatch* b) {
+  if (!b) return;
+  if (b->scanner) {
+    DeviceGuard g(b->scanner->device);
+    (void)hipStreamSynchronize(b->scanner->stream);
+    void* ptrs[] = {b->d_outputs, b->d_offs, b->d_lens, b->d_tx, b->d_ty, b->d_flags};
+    for (void* p : ptrs)
+      if (p) (void)hipFree(p);
+    free_scanner(b->scanner);
+  }
+  delete b;
+}
+
+void* LaunchBatchScan(uint32_t** managed_points_x, uint32_t** managed_points_y, const uint32_t* h_scalar,
+                      const uint32_t* h_spend_pubkey_x, const uint32_t* h_spend_pubkey_y,
+                      const uint32_t* h_label_keys_x, const uint32_t* h_label_keys_y, uint32_t label_count,
+                      const int64_t* h_outputs, const uint32_t* h_output_offsets,
+                      const uint32_t* h_output_lengths, uint8_t** managed_match_flags, uint32_t count,
+                      size_t outputs_size) {
+  if (!managed_points_x || !managed_points_y || !managed_match_flags || !h_scalar || !h_spend_pubkey_x ||
+      !h_spend_pubkey_y || !h_output_offsets || !h_output_lengths || count == 0) {
+    set_error(CUDASP_ERR_INVALID_ARG, "LaunchBatchScan: invalid argument");
+    return nullptr;
+  }
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) {
+    set_error(CUDASP_ERR_HIP, "hipGetDevice failed");
+    return nullptr;
+  }
+  uint8_t scan[32], spend[64];
+  words_to_bytes(scan, h_scalar, 8);
+  words_to_bytes(spend, h_spend_pubkey_x, 8);
+  words_to_bytes(spend + 32, h_spend_pubkey_y, 8);
+  std::vector<uint8_t> labels(64 * (size_t)label_count);
+  for (uint32_t j = 0; j < label_count; j++) {
+    words_to_bytes(&labels[64 * j], h_label_keys_x + 8 * j, 8);
+    words_to_bytes(&labels[64 * j + 32], h_label_keys_y + 8 * j, 8);
+  }
+  LegacyBatch* b = new LegacyBatch();
+  b->count = count;
+  if (cudasp_scanner_create(device, scan, spend, labels.data(), label_count, count, &b->scanner) != CUDASP_OK) {
+    delete b;
+    return nullptr;
+  }
+  hipStream_t st = b->scanner->stream;
+  bool ok = hipMallocManaged((void**)managed_points_x, (size_t)32 * count) == hipSuccess &&
+            hipMallocManaged((void**)managed_points_y, (size_t)32 * count) == hipSuccess &&
+            hipMallocManaged((void**)managed_match_flags, count) == hipSuccess &&
+            hipMalloc(&b->d_outputs, (outputs_size ? outputs_size : 1) * 8) == hipSuccess &&
+            hipMalloc(&b->d_offs, (size_t)4 * count) == hipSuccess &&
+            hipMalloc(&b->d_lens, (size_t)4 * count) == hipSuccess &&
+            hipMalloc(&b->d_tx, (size_t)32 * count) == hipSuccess &&
+            hipMalloc(&b->d_ty, (size_t)32 * count) == hipSuccess &&
+            hipMalloc(&b->d_flags, count) == hipSuccess;
+  if (ok) {
+    memset(*managed_match_flags, 0, count);
+    ok = (outputs_size == 0 ||
+          hipMemcpyAsync(b->d_outputs, h_outputs, outputs_size * 8, hipMemcpyHostToDevice, st) == hipSuccess) &&
+         hipMemcpyAsync(b->d_offs, h_output_offsets, (size_t)4 * count, hipMemcpyHostToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(b->d_lens, h_output_lengths, (size_t)4 * count, hipMemcpyHostToDevice, st) == hipSuccess &&
+         hipStreamSynchronize(st) == hipSuccess;
+  }
+  if (!ok) {
+    set_error(CUDASP_ERR_HIP, "LaunchBatchScan: allocation or copy failed");
+    free_legacy(b);
+    return nullptr;
+  }
+  return b;
+}
+
+int RunBatchScanKernels(void* state_handle, uint32_t* managed_points_x, uint32_t* managed_points_y,
+                        const uint32_t* /*h_scalar*/, const uint32_t* /*h_spend_pubkey_x*/,
+                        const uint32_t* /*h_spend_pubkey_y*/, const uint32_t* /*h_label_keys_x*/,
+                        const uint32_t* /*h_label_keys_y*/, uint32_t /*label_count*/, uint8_t* managed_match_flags,
+                        uint32_t count) {
+  // Like the reference, the keys were bound in LaunchBatchScan; the repeated
+  // host key arguments are accepted and ignored (src/cudasp_gpu.cu:677-682).
+  LegacyBatch* b = static_cast<LegacyBatch*>(state_handle);
+  if (!b || !b->scanner || !managed_points_x || !managed_points_y || !managed_match_flags || count != b->count) {
+    set_error(CUDASP_ERR_INVALID_ARG, "RunBatchScanKernels: invalid state or arguments");
+    return -1;
+  }
+  DeviceGuard g(b->scanner->device);
+  hipStream_t st = b->scanner->stream;
+  if (hipMemcpyAsync(b->d_tx, managed_points_x, (size_t)32 * count, hipMemcpyDefault, st) != hipSuccess ||
+      hipMemcpyAsync(b->d_ty, managed_points_y, (size_t)32 * count, hipMemcpyDefault, st) != hipSuccess) {
+    set_error(CUDASP_ERR_HIP, "RunBatchScanKernels: point copy failed");
+    return -1;
+  }
+  if (launch_pipeline(b->scanner, b->d_tx, b->d_ty, b->d_outputs, b->d_offs, b->d_lens, count, b->d_flags, nullptr,
+                      nullptr, nullptr, nullptr, st) != CUDASP_OK)
+    return -1;
+  if (hipMemcpyAsync(managed_match_flags, b->d_flags, count, hipMemcpyDefault, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    set_error(CUDASP_ERR_HIP, "RunBatchScanKernels: kernel or flag copy failed");
+    return -1;
+  }
+  return 0;
+}
+
+void FreeBatchScanState(void* state_handle) { free_legacy(static_cast<LegacyBatch*>(state_handle)); }
+
+void FreeBatchScanManaged(void* ptr) {
+  if (ptr) (void)hipFree(ptr);
+}
+
+}  // extern "C"

@@ -1,0 +1,7 @@
+"""cudasp_amd -- MI355X-native cudasp_scan (BIP-352 silent-payment scanning).
+
+The compute path is the HIP library ``libcudasp_amd.so`` (gfx950 kernels behind
+the C ABI in ``include/cudasp_abi.h``); this package is its Python face.
+"""
+from ._native import CudaspError, load as load_native  # noqa: F401
+from .scanner import Scanner  # noqa: F401

@@ -1,0 +1,75 @@
+"""ctypes binding of the in-tree HIP library ``libcudasp_amd.so``.
+
+The library is the product: every compute call goes to the gfx950 kernels
+through the C ABI declared in ``include/cudasp_abi.h``.  There is no CPU
+fallback; if the library is missing or no device is visible, calls raise.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libcudasp_amd.so")
+
+CUDASP_OK = 0
+CUDASP_ERR_INVALID_ARG = -2
+CUDASP_ERR_HIP = -3
+CUDASP_ERR_NO_DEVICE = -4
+CUDASP_ERR_CAPACITY = -5
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_I32 = ctypes.c_int
+
+# name -> (restype, argtypes); mirrors include/cudasp_abi.h
+SIGNATURES = {
+    "cudasp_last_error": (ctypes.c_char_p, []),
+    "cudasp_version": (ctypes.c_char_p, []),
+    "cudasp_device_count": (_I32, []),
+    "cudasp_scanner_create": (_I32, [_I32, _P, _P, _P, _U32, _U32, ctypes.POINTER(_P)]),
+    "cudasp_scanner_destroy": (None, [_P]),
+    "cudasp_scan_device": (_I32, [_P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P]),
+    "cudasp_scan_host": (_I32, [_P, _P, _P, ctypes.c_size_t, _P, _P, _U32, _P]),
+    "cudasp_row_values_device": (_I32, [_P, _P, _P, _U32, _P, _P, _P]),
+    "cudasp_scanner_sync": (_I32, [_P]),
+    "cudasp_tweaks_to_columns": (_I32, [_P, _U32, _P, _P, _P]),
+    "LaunchBatchScan": (_P, [_P, _P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _U32, ctypes.c_size_t]),
+    "RunBatchScanKernels": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _U32]),
+    "FreeBatchScanState": (None, [_P]),
+    "FreeBatchScanManaged": (None, [_P]),
+}
+
+
+class CudaspError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__("cudasp error %d: %s" % (code, message))
+        self.code = code
+
+
+_lib = None
+
+
+def load(path=None):
+    """Load (once) and return the native library; raises if it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise CudaspError(CUDASP_ERR_NO_DEVICE,
+                          "HIP library %s not built (run `make -C duckdb-cudasp-extension_amd` "
+                          "or __graft_entry__.build())" % p)
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != CUDASP_OK:
+        msg = load().cudasp_last_error()
+        raise CudaspError(rc, msg.decode() if msg else "")
+    return rc

@@ -1,0 +1,105 @@
+"""Scanner: one query's keys bound on one MI355X device.
+
+Thin Python face of ``cudasp_scanner_*`` (include/cudasp_abi.h).  Device
+buffers are torch tensors (PyTorch is only the allocator / stream provider
+here); host buffers are numpy arrays.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+
+
+def _ptr(t):
+    """Raw pointer of a torch tensor or numpy array (None -> NULL)."""
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data
+    return t.data_ptr()
+
+
+def _as_bytes(b, n, what):
+    if isinstance(b, (bytes, bytearray)):
+        if len(b) != n:
+            raise ValueError("%s must be exactly %d bytes, got %d bytes" % (what, n, len(b)))
+        return bytes(b)
+    raise TypeError("%s must be bytes" % what)
+
+
+class Scanner:
+    """Bind scan key, spend key and label keys on `device` for batches of at
+    most `max_rows` rows (CudaspScanBindData + LaunchBatchScan of the
+    reference, src/cudasp_extension.cu:87-104, src/cudasp_gpu.cu:445-669)."""
+
+    def __init__(self, scan_private_key, spend_public_key, label_keys=(), max_rows=300000, device=0):
+        lib = _native.load()
+        scan = _as_bytes(scan_private_key, 32, "scan_private_key")
+        spend = _as_bytes(spend_public_key, 64, "spend_public_key")
+        labels = [_as_bytes(l, 64, "label key") for l in label_keys]
+        self.label_count = len(labels)
+        self.max_rows = int(max_rows)
+        self.device = int(device)
+        lab = b"".join(labels) if labels else None
+        h = ctypes.c_void_p()
+        _native.check(lib.cudasp_scanner_create(self.device, scan, spend, lab, self.label_count,
+                                                self.max_rows, ctypes.byref(h)))
+        self._h = h
+        self._lib = lib
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.cudasp_scanner_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ----------------------------------------------------------- device path
+    def scan_device(self, tweak_x, tweak_y, outputs, offsets, lengths, flags, match_rows=None,
+                    match_count=None, stream=None):
+        """Asynchronous scan of device-resident columns (torch tensors)."""
+        n = int(flags.numel())
+        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        _native.check(self._lib.cudasp_scan_device(
+            self._h, _ptr(tweak_x), _ptr(tweak_y), _ptr(outputs), _ptr(offsets), _ptr(lengths), n,
+            _ptr(flags), _ptr(match_rows), _ptr(match_count), st))
+
+    def row_values_device(self, tweak_x, tweak_y, t_out, values, stream=None):
+        n = int(tweak_x.numel() // 8)
+        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        _native.check(self._lib.cudasp_row_values_device(
+            self._h, _ptr(tweak_x), _ptr(tweak_y), n, _ptr(t_out), _ptr(values), st))
+
+    def sync(self):
+        _native.check(self._lib.cudasp_scanner_sync(self._h))
+
+    # ------------------------------------------------------------- host path
+    def scan_host(self, tweak_keys, outputs, offsets, lengths):
+        """Synchronous scan from host memory.  tweak_keys: uint8 [n, 64];
+        outputs: int64 CSR values; offsets/lengths: uint32 [n].  Returns a
+        uint8 [n] array of match flags."""
+        tk = np.ascontiguousarray(tweak_keys, dtype=np.uint8).reshape(-1, 64)
+        n = tk.shape[0]
+        outs = np.ascontiguousarray(outputs, dtype=np.int64)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint32)
+        lens = np.ascontiguousarray(lengths, dtype=np.uint32)
+        if offs.shape[0] != n or lens.shape[0] != n:
+            raise ValueError("offsets/lengths must have one entry per row")
+        flags = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return flags
+        _native.check(self._lib.cudasp_scan_host(
+            self._h, _ptr(tk), _ptr(outs) if outs.size else None, outs.size, _ptr(offs), _ptr(lens), n,
+            _ptr(flags)))
+        return flags

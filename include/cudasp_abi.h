@@ -1,0 +1,127 @@
+/*
+ * cudasp_abi.h -- C ABI of the MI355X (gfx950) cudasp_scan hot path.
+ *
+ * Two layers, both plain C (pointers and sizes only, no HIP or torch types):
+ *
+ * 1. The reference's own three-phase batch ABI, same names, argument order and
+ *    meaning, so the reference host (src/cudasp_extension.cu:21-52, which
+ *    forward-declares these) links against this library unchanged:
+ *      LaunchBatchScan      replaces src/cudasp_gpu.cu:445-669
+ *      RunBatchScanKernels  replaces src/cudasp_gpu.cu:673-966
+ *      FreeBatchScanState   replaces src/cudasp_gpu.cu:969-1023
+ *    plus FreeBatchScanManaged, the replacement for the host's cudaFree of the
+ *    three managed buffers (src/cudasp_extension.cu:395-397).
+ *
+ * 2. The scanner API the rebuilt host uses: one scanner per (query, device),
+ *    created once with the query's keys (the bind-time data of
+ *    CudaspScanBindData, src/cudasp_extension.cu:87-104), then any number of
+ *    batches, either device-resident and asynchronous on a caller stream, or
+ *    from host memory (synchronous, the ProcessBatch contract of
+ *    src/cudasp_extension.cu:226-410).
+ *
+ * Byte conventions are the reference's (src/cudasp_extension.cu:59-85):
+ * scan key 32 bytes little-endian; spend, label and tweak keys 64 bytes =
+ * x (32 B LE) || y (32 B LE).  Limb arrays are u32, limb 0 least significant;
+ * device tweak columns are column-major: limb j of row i at [j * n + i].
+ *
+ * A row matches when int64(upper 64 bits of (t*G + B).x), or of
+ * (t*G + B + L_j).x for some label j, is in the row's outputs list, with
+ * t = SHA256(SHA256("BIP0352/SharedSecret")^2 || ser(d*T) || 00000000)
+ * (src/cudasp_gpu.cu:74-178, :236-354).
+ *
+ * Errors: functions return CUDASP_OK (0) or a negative code; the message of
+ * the last failure on the calling thread is available from cudasp_last_error().
+ */
+#ifndef CUDASP_ABI_H
+#define CUDASP_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CUDASP_OK 0
+#define CUDASP_ERR_INVALID_ARG (-2)
+#define CUDASP_ERR_HIP (-3)
+#define CUDASP_ERR_NO_DEVICE (-4)
+#define CUDASP_ERR_CAPACITY (-5)
+
+/* Thread-local message of the last failure ("" if none). */
+const char* cudasp_last_error(void);
+/* Library version string. */
+const char* cudasp_version(void);
+/* Number of visible HIP devices (0 if none). */
+int cudasp_device_count(void);
+
+/* ---------------------------------------------------------------- scanner */
+typedef struct cudasp_scanner cudasp_scanner;
+
+/* Create a scanner on `device` for one query's keys.  label_keys holds
+ * label_count 64-byte keys back to back (may be NULL when label_count is 0).
+ * max_rows bounds the rows of any later batch.  The first scanner on a device
+ * also builds that device's fixed-base table (32 MiB, kept for the process).
+ * Fails with CUDASP_ERR_INVALID_ARG for a scan key that is 0 mod n. */
+int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const uint8_t spend_public_key[64],
+                          const uint8_t* label_keys, uint32_t label_count, uint32_t max_rows,
+                          cudasp_scanner** out);
+void cudasp_scanner_destroy(cudasp_scanner* s);
+
+/* Device-resident batch, asynchronous on `stream` (a hipStream_t; NULL = the
+ * scanner's own stream).  Inputs: tweak x and y columns (8 x n each,
+ * column-major), the outputs CSR (values, per-row u32 offset and length).
+ * Outputs: d_match_flags[n] (0/1, required); if d_match_rows and
+ * d_match_count are both non-NULL, *d_match_count (which the caller zeroes)
+ * receives the number of matches and d_match_rows their row indices, in no
+ * particular order. */
+int cudasp_scan_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint32_t* d_tweak_y,
+                       const int64_t* d_outputs, const uint32_t* d_output_offsets,
+                       const uint32_t* d_output_lengths, uint32_t n, uint8_t* d_match_flags,
+                       uint32_t* d_match_rows, uint32_t* d_match_count, void* stream);
+
+/* Host batch, synchronous: tweak keys as n 64-byte blobs back to back, the
+ * outputs CSR in host memory; writes h_match_flags[n]. */
+int cudasp_scan_host(cudasp_scanner* s, const uint8_t* h_tweak_keys, const int64_t* h_outputs,
+                     size_t outputs_size, const uint32_t* h_output_offsets, const uint32_t* h_output_lengths,
+                     uint32_t n, uint8_t* h_match_flags);
+
+/* Diagnostic stage outputs for parity tests, asynchronous on `stream`:
+ * d_t (8 x n column-major) receives the shared-secret hash scalar t;
+ * d_values ((1 + label_count) x n column-major) the int64 compare values of
+ * the base output and of each label (INT64_MIN for a label sum at infinity). */
+int cudasp_row_values_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint32_t* d_tweak_y,
+                             uint32_t n, uint32_t* d_t, int64_t* d_values, void* stream);
+
+/* Wait for the scanner's own stream. */
+int cudasp_scanner_sync(cudasp_scanner* s);
+
+/* Transpose n row-major 64-byte tweak blobs (device memory) into x and y
+ * columns (8 x n each), asynchronous on `stream`. */
+int cudasp_tweaks_to_columns(const uint8_t* d_tweak_rows, uint32_t n, uint32_t* d_tweak_x, uint32_t* d_tweak_y,
+                             void* stream);
+
+/* -------------------------------------------- reference three-phase ABI */
+void* LaunchBatchScan(uint32_t** managed_points_x, uint32_t** managed_points_y, const uint32_t* h_scalar,
+                      const uint32_t* h_spend_pubkey_x, const uint32_t* h_spend_pubkey_y,
+                      const uint32_t* h_label_keys_x, const uint32_t* h_label_keys_y, uint32_t label_count,
+                      const int64_t* h_outputs, const uint32_t* h_output_offsets,
+                      const uint32_t* h_output_lengths, uint8_t** managed_match_flags, uint32_t count,
+                      size_t outputs_size);
+
+int RunBatchScanKernels(void* state_handle, uint32_t* managed_points_x, uint32_t* managed_points_y,
+                        const uint32_t* h_scalar, const uint32_t* h_spend_pubkey_x,
+                        const uint32_t* h_spend_pubkey_y, const uint32_t* h_label_keys_x,
+                        const uint32_t* h_label_keys_y, uint32_t label_count, uint8_t* managed_match_flags,
+                        uint32_t count);
+
+void FreeBatchScanState(void* state_handle);
+
+/* Frees one of the managed buffers LaunchBatchScan allocated. */
+void FreeBatchScanManaged(void* ptr);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CUDASP_ABI_H */

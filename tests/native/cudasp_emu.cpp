@@ -1,0 +1,235 @@
+// CPU emulation harness for the cudasp kernel math (test infrastructure only).
+//
+// Compiles the exact __host__ __device__ row functions of
+// duckdb-cudasp-extension_amd/csrc/scan_rows.hpp and the host preparation of
+// scan_prepare.hpp for the CPU, with every field-element magnitude
+// precondition checked (CUDASP_FE_CHECK), so the kernel arithmetic can be
+// verified against the golden fixtures in this GPU-less container.  It is never
+// part of the product path: the product is libcudasp_amd.so, which only runs
+// on a gfx950 device.
+#define CUDASP_FE_CHECK 1
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../duckdb-cudasp-extension_amd/csrc/scan_prepare.hpp"
+
+namespace cudasp {
+void fe_check_fail(const char* what, int limb, uint32_t v) {
+  fprintf(stderr, "cudasp_emu: magnitude check failed in %s: limb %d = 0x%08x\n", what, limb, v);
+  abort();
+}
+}  // namespace cudasp
+
+using namespace cudasp;
+
+namespace {
+
+void fe_from_bytes(fe& r, const uint8_t b[32]) {
+  uint32_t w[8];
+  for (int i = 0; i < 8; i++)
+    w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+           ((uint32_t)b[4 * i + 3] << 24);
+  fe_from_u32x8(r, w);
+}
+
+void fe_to_bytes(uint8_t b[32], const fe& a) {
+  fe t = a;
+  fe_normalize(t);
+  uint32_t w[8];
+  fe_to_u32x8(w, t);
+  for (int i = 0; i < 8; i++) {
+    b[4 * i] = (uint8_t)w[i];
+    b[4 * i + 1] = (uint8_t)(w[i] >> 8);
+    b[4 * i + 2] = (uint8_t)(w[i] >> 16);
+    b[4 * i + 3] = (uint8_t)(w[i] >> 24);
+  }
+}
+
+void words_from_row(uint32_t x[8], uint32_t y[8], const uint8_t* row) {
+  for (int i = 0; i < 8; i++) {
+    x[i] = (uint32_t)row[4 * i] | ((uint32_t)row[4 * i + 1] << 8) | ((uint32_t)row[4 * i + 2] << 16) |
+           ((uint32_t)row[4 * i + 3] << 24);
+    const uint8_t* r = row + 32;
+    y[i] = (uint32_t)r[4 * i] | ((uint32_t)r[4 * i + 1] << 8) | ((uint32_t)r[4 * i + 2] << 16) |
+           ((uint32_t)r[4 * i + 3] << 24);
+  }
+}
+
+// Lazily filled copy of the device fixed-base table.
+struct LazyTable {
+  std::vector<uint32_t> table;
+  std::vector<uint8_t> filled;
+  std::vector<uint32_t> bases;
+  LazyTable() : table((size_t)FB_WINDOWS * FB_ENTRIES * FB_WORDS), filled((size_t)FB_WINDOWS * FB_ENTRIES), bases(fb_window_bases()) {}
+  void ensure(int window, uint32_t j) {
+    size_t idx = (size_t)window * FB_ENTRIES + j;
+    if (filled[idx]) return;
+    ge Q;
+    ge_from_words(Q, &bases[window * 16]);
+    fb_build_entry(&table[idx * FB_WORDS], Q, j);
+    filled[idx] = 1;
+  }
+  // Same recoding as row_match: t made odd, b_i = bits [16i+1, 16i+16].
+  void ensure_for(const uint32_t t_in[8]) {
+    uint32_t t[9];
+    for (int i = 0; i < 8; i++) t[i] = t_in[i];
+    t[8] = 0;
+    t[0] |= 1u;
+    for (int i = 0; i < FB_WINDOWS; i++) {
+      uint32_t bits = (t[0] >> 1) & 0xFFFFu;
+      for (int q = 0; q < 8; q++) t[q] = (t[q] >> 16) | (t[q + 1] << 16);
+      t[8] >>= 16;
+      bool neg = (bits & 0x8000u) == 0;
+      ensure(i, (bits ^ (neg ? 0x7FFFu : 0u)) & 0x7FFFu);
+    }
+  }
+};
+
+LazyTable& lazy_table() {
+  static LazyTable t;
+  return t;
+}
+
+}  // namespace
+
+extern "C" {
+
+int emu_fe_mul(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
+  fe x, y, r;
+  fe_from_bytes(x, a);
+  fe_from_bytes(y, b);
+  fe_mul(r, x, y);
+  fe_to_bytes(out, r);
+  return 0;
+}
+
+int emu_fe_sqr(const uint8_t a[32], uint8_t out[32]) {
+  fe x, r;
+  fe_from_bytes(x, a);
+  fe_sqr(r, x);
+  fe_to_bytes(out, r);
+  return 0;
+}
+
+int emu_fe_inv(const uint8_t a[32], uint8_t out[32]) {
+  fe x, r;
+  fe_from_bytes(x, a);
+  fe_inv(r, x);
+  fe_to_bytes(out, r);
+  return 0;
+}
+
+int emu_fe_normalize(const uint8_t a[32], uint8_t out[32]) {
+  fe x;
+  fe_from_bytes(x, a);
+  fe_to_bytes(out, x);
+  return 0;
+}
+
+int emu_glv_split(const uint8_t k[32], uint8_t k1[32], int* neg1, uint8_t k2[32], int* neg2) {
+  host::Big<8> d = host::big_zero<8>();
+  for (int i = 0; i < 32; i++) d.w[i / 4] |= (uint32_t)k[i] << (8 * (i % 4));
+  host::SignedHalf a, b;
+  host::glv_split(d, a, b);
+  for (int i = 0; i < 32; i++) {
+    k1[i] = (uint8_t)(a.mag.w[i / 4] >> (8 * (i % 4)));
+    k2[i] = (uint8_t)(b.mag.w[i / 4] >> (8 * (i % 4)));
+  }
+  *neg1 = a.neg;
+  *neg2 = b.neg;
+  return 0;
+}
+
+int emu_wnaf(const uint8_t k[32], int w, int8_t* digits, int max_digits) {
+  host::Big<8> d = host::big_zero<8>();
+  for (int i = 0; i < 32; i++) d.w[i / 4] |= (uint32_t)k[i] << (8 * (i % 4));
+  return host::wnaf(digits, max_digits, d, w);
+}
+
+int emu_midstate(uint32_t mid[8]) {
+  bip352_midstate(mid);
+  return 0;
+}
+
+int emu_fb_entry(uint32_t window, uint32_t j, uint32_t out[16]) {
+  std::vector<uint32_t> bases = fb_window_bases();
+  ge Q;
+  ge_from_words(Q, &bases[window * 16]);
+  fb_build_entry(out, Q, j);
+  return 0;
+}
+
+// Stage A for n rows: t as 8 LE u32 words per row.
+int emu_shared_secret(const uint8_t scan[32], const uint8_t* tweaks, uint32_t n, uint32_t* t_out) {
+  static const uint8_t dummy_spend[64] = {0};
+  ScanConsts k;
+  std::vector<int8_t> naf;
+  std::vector<uint32_t> labels;
+  std::string err;
+  // Spend key only feeds stage B; use G's encoding-free path: prepare_scan
+  // needs a point, so pass the generator-derived b later.  Here only the
+  // scan-key dependent constants matter.
+  (void)dummy_spend;
+  host::Big<8> d = host::big_zero<8>();
+  for (int i = 0; i < 32; i++) d.w[i / 4] |= (uint32_t)scan[i] << (8 * (i % 4));
+  d = host::scalar_reduce(d);
+  if (host::big_is_zero(d)) return CUDASP_ERR_INVALID_ARG;
+  host::SignedHalf k1, k2;
+  host::glv_split(d, k1, k2);
+  naf.assign(2 * NAF_MAX, 0);
+  int len1 = host::wnaf(naf.data(), NAF_MAX, k1.mag, 5);
+  int len2 = host::wnaf(naf.data() + NAF_MAX, NAF_MAX, k2.mag, 5);
+  for (int i = 0; i < NAF_MAX; i++) {
+    if (k1.neg) naf[i] = (int8_t)-naf[i];
+    if (k2.neg) naf[NAF_MAX + i] = (int8_t)-naf[NAF_MAX + i];
+  }
+  uint32_t mid[8];
+  bip352_midstate(mid);
+  uint32_t naf_len = (uint32_t)(len1 > len2 ? len1 : len2);
+  std::vector<uint32_t> scratch(VB_SCRATCH_WORDS);
+  Scratch sc{scratch.data(), 1, 0};
+  for (uint32_t r = 0; r < n; r++) {
+    uint32_t x[8], y[8];
+    words_from_row(x, y, tweaks + 64 * (size_t)r);
+    row_shared_secret(t_out + 8 * (size_t)r, x, y, naf.data(), naf_len, mid, sc);
+  }
+  return 0;
+}
+
+// Full pipeline values for n rows: values[r * (1 + L) + j] (j = 0 base, 1.. labels);
+// t_out (optional) 8 words per row; flags (optional) with the outputs CSR.
+int emu_row_values(const uint8_t scan[32], const uint8_t spend[64], const uint8_t* labels_bytes, uint32_t L,
+                   const uint8_t* tweaks, uint32_t n, int64_t* values, uint32_t* t_out, const int64_t* outputs,
+                   const uint32_t* offs, const uint32_t* lens, uint8_t* flags) {
+  ScanConsts k;
+  std::vector<int8_t> naf;
+  std::vector<uint32_t> labels;
+  std::string err;
+  int rc = prepare_scan(scan, spend, labels_bytes, L, k, naf, labels, err);
+  if (rc != CUDASP_OK) {
+    fprintf(stderr, "cudasp_emu: prepare_scan: %s\n", err.c_str());
+    return rc;
+  }
+  std::vector<uint32_t> vscr(VB_SCRATCH_WORDS);
+  std::vector<uint32_t> lscr(10 * (size_t)(L ? L : 1));
+  Scratch sa{vscr.data(), 1, 0}, sb{lscr.data(), 1, 0};
+  LazyTable& tab = lazy_table();
+  std::vector<int64_t> vals(1 + L);
+  for (uint32_t r = 0; r < n; r++) {
+    uint32_t x[8], y[8], t[8];
+    words_from_row(x, y, tweaks + 64 * (size_t)r);
+    row_shared_secret(t, x, y, naf.data(), k.naf_len, k.mid, sa);
+    if (t_out)
+      for (int j = 0; j < 8; j++) t_out[8 * (size_t)r + j] = t[j];
+    tab.ensure_for(t);
+    uint32_t off = offs ? offs[r] : 0, len = lens ? lens[r] : 0;
+    bool hit = row_match(t, tab.table.data(), k, labels.data(), outputs, off, len, sb, vals.data(), 1);
+    if (values)
+      for (uint32_t j = 0; j <= L; j++) values[(size_t)r * (1 + L) + j] = vals[j];
+    if (flags) flags[r] = hit ? 1 : 0;
+  }
+  return 0;
+}
+
+}  // extern "C"

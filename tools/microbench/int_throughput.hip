@@ -1,0 +1,116 @@
+// Microbenchmark: per-instruction VALU throughput on gfx950 for the integer
+// primitives a 256-bit field multiply can be built from. Each lane runs 8
+// independent chains so the measurement is issue-throughput, not latency.
+// Output: one line per op with lane-ops/s and lane-ops per CU per cycle at the
+// measured clock (2.4 GHz nominal).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+
+#define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+template <int OP>
+__global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t seed) {
+  uint32_t a[8], b[8];
+  uint64_t acc[8];
+  double f[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a[i] = seed * (threadIdx.x + 3 * i + 1) + blockIdx.x;
+    b[i] = a[i] ^ 0x9e3779b9u;
+    acc[i] = (uint64_t)a[i] * 7u + b[i];
+    f[i] = (double)a[i] * 1e-9;
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if constexpr (OP == 0) {  // v_mad_u64_u32 with carry-out
+          uint64_t c;
+          asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[k]), "=s"(c) : "v"(a[k]), "v"(b[k]));
+        } else if constexpr (OP == 1) {
+          asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 2) {
+          asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 3) {
+          asm volatile("v_add_co_u32 %0, vcc, %0, %1\n\tv_addc_co_u32 %1, vcc, %1, %0, vcc"
+                       : "+v"(a[k]), "+v"(b[k]) : : "vcc");
+        } else if constexpr (OP == 4) {
+          asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 5) {
+          asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(f[k]) : "v"(f[(k + 1) & 7]));
+        } else if constexpr (OP == 6) {
+          asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a[k]) : "v"(b[k]), "v"(b[(k+1)&7]));
+        } else if constexpr (OP == 7) {
+          asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 8) {  // 3-input add
+          asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(b[k]), "v"(b[(k+1)&7]));
+        } else if constexpr (OP == 9) {  // carry-in add into 3rd word from sgpr mask
+          uint64_t c = 0;
+          asm volatile("v_addc_co_u32_e64 %0, %1, %0, 0, %1" : "+v"(a[k]), "+s"(c));
+        } else if constexpr (OP == 10) {  // v_lshl_add / alignbit
+          asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 11) {  // 64-bit add via v_lshl_add_u64 (gfx940+)
+          asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(acc[k]) : "v"(acc[(k+1)&7]));
+        }
+      }
+    }
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s ^= a[i] ^ b[i] ^ (uint32_t)acc[i] ^ (uint32_t)(acc[i] >> 32) ^ (uint32_t)(uint64_t)f[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <int OP>
+static void run(const char* name, int instrs_per_op, int blocks, uint32_t* d) {
+  int iters = 2000;
+  hipEvent_t e0, e1;
+  CHK(hipEventCreate(&e0));
+  CHK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(bench<OP>, dim3(blocks), dim3(256), 0, 0, d, 10, 1u);
+  CHK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; rep++) {
+    CHK(hipEventRecord(e0));
+    hipLaunchKernelGGL(bench<OP>, dim3(blocks), dim3(256), 0, 0, d, iters, 1u + rep);
+    CHK(hipEventRecord(e1));
+    CHK(hipEventSynchronize(e1));
+    float ms;
+    CHK(hipEventElapsedTime(&ms, e0, e1));
+    if (ms < best) best = ms;
+  }
+  double lane_ops = (double)blocks * 256 * iters * 16 * 8 * instrs_per_op;
+  double rate = lane_ops / (best * 1e-3);
+  // lanes-per-CU-per-cycle at 2.4 GHz (full-rate VALU = 128)
+  double per_cu_cyc = rate / (256.0 * 2.4e9);
+  printf("%-28s %8.3f ms  %10.3f Tlane-op/s  %7.2f lane-op/CU/cyc@2.4GHz\n", name, best, rate * 1e-12, per_cu_cyc);
+  CHK(hipEventDestroy(e0));
+  CHK(hipEventDestroy(e1));
+}
+
+int main() {
+  hipDeviceProp_t p;
+  CHK(hipGetDeviceProperties(&p, 0));
+  printf("device %s  CUs %d  clock %d kHz\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
+  int blocks = p.multiProcessorCount * 8;
+  uint32_t* d;
+  CHK(hipMalloc(&d, (size_t)blocks * 256 * 4));
+  run<4>("v_add_u32", 1, blocks, d);
+  run<8>("v_add3_u32", 1, blocks, d);
+  run<10>("v_alignbit_b32", 1, blocks, d);
+  run<3>("v_add_co+v_addc_co (2 ins)", 2, blocks, d);
+  run<9>("v_addc_co_u32_e64 sgpr cin", 1, blocks, d);
+  run<11>("v_lshl_add_u64", 1, blocks, d);
+  run<0>("v_mad_u64_u32", 1, blocks, d);
+  run<1>("v_mul_lo_u32", 1, blocks, d);
+  run<2>("v_mul_hi_u32", 1, blocks, d);
+  run<6>("v_mad_u32_u24", 1, blocks, d);
+  run<7>("v_mul_hi_u32_u24", 1, blocks, d);
+  run<5>("v_fma_f64", 1, blocks, d);
+  CHK(hipFree(d));
+  return 0;
+}
