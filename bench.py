@@ -1,0 +1,333 @@
+#!/usr/bin/env python3
+"""bench.py -- tx/s through cudasp_scan on a 32.7M-row synthetic tweak table.
+
+Contract (see DESIGN.md "Measurement"):
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  N > 1 is launched by the driver as one process per GPU via
+  torch.distributed.run; ranks read RANK / LOCAL_RANK / WORLD_SIZE.
+
+Workload (BASELINE.json metric "tx/sec through cudasp_scan on 32M-row tweak
+table", configs[3] shape): every rank holds its own 32.7M-row synthetic table
+resident in HBM (weak scaling: per-GPU work is fixed as N grows) laid out as the
+reference's batches of batch_size = 300000 rows, tweak limbs column-major per
+batch.  A step is one pass of the hot path over the rank's whole table: every
+batch goes through cudasp_scan_device (stage A: d*T + tagged hash; stage B:
+t*G + B, labels, compare, flag + ballot compaction), batches round-robin over
+`--streams` HIP streams (the reference's per-thread streams,
+src/cudasp_gpu.cu:505).  Inputs are resident before the timed region; the
+PCIe-inclusive host path is measured separately.
+
+Synthetic data: T_i = (s0 + g) G with s0 = SHA256("cudasp-synth-v1")
+mod n and g the global row index; 2 splitmix64 outputs per row (seed
+0xC0DA5EED); every 1000th row gets its true compare value planted, so the
+expected match count is known exactly and checked after the run.
+
+Only the cpu_baseline leg touches oracle/ (the C restatement, timed on a
+bounded sample on this box's host cores, and checked against the GPU flags).
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "duckdb-cudasp-extension_amd"))
+
+from cudasp_amd import Scanner, _native  # noqa: E402
+
+METRIC = "tx/sec through cudasp_scan on 32M-row tweak table at 1/2/4/8 MI355X"
+# Keys of the BIP-352 test vector as the reference's SQL test passes them
+# (test/sql/cudasp.test:54): scan key LE, spend key LE x || y.
+SCAN_KEY = bytes.fromhex("2c1f0cb94db3946522cc1487256535dd33a1f911946baff817a72880064e690f")
+SPEND_KEY = bytes.fromhex(
+    "36cf8fcd4d4890ab6c1083aeb5b50c260c20acda7839120e3575836f6d85c95c"
+    "e0d705e31ff9fdcce67a8f3598871c6dfbe6bcde8a51cb7b48b0f95be0ea94de")
+# Label key of test/sql/cudasp.test:104.
+TEST_LABEL = bytes.fromhex(
+    "cd63f9212a2deebde8a71e9ea23f6f958c47c41d2ed74b9617fe6fb554d1524e"
+    "292fabddbdcbb643eafc328875c46d75a1d697b2b31c42d38aa93f85eab34bc1")
+N_ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+P_FIELD = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEFFFFFC2F
+GX = 0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798
+GY = 0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8
+OUTPUT_SEED = 0xC0DA5EED
+PLANT_EVERY = 1000
+# Algorithmic HBM bytes per row: 64 tweak + 8 offset/length
+# + 8 per output + 1 flag.
+def bytes_per_row(k):
+    return 73 + 8 * k
+
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, spec
+VALU_MAD_PEAK = 37.1e12    # measured v_mad_u64_u32 lane-ops/s (profiles/r01_microbench_int.txt)
+
+
+def _ec_add(p, q):
+    if p is None:
+        return q
+    if q is None:
+        return p
+    if p[0] == q[0]:
+        if (p[1] + q[1]) % P_FIELD == 0:
+            return None
+        lam = 3 * p[0] * p[0] * pow(2 * p[1], -1, P_FIELD) % P_FIELD
+    else:
+        lam = (q[1] - p[1]) * pow(q[0] - p[0], -1, P_FIELD) % P_FIELD
+    x = (lam * lam - p[0] - q[0]) % P_FIELD
+    return (x, (lam * (p[0] - x) - p[1]) % P_FIELD)
+
+
+def _ec_mul(k, p):
+    r = None
+    while k:
+        if k & 1:
+            r = _ec_add(r, p)
+        p = _ec_add(p, p)
+        k >>= 1
+    return r
+
+
+def label_keys(count):
+    """Label keys: the SQL test's label, then L_j = (j+1) c G."""
+    out = []
+    if count >= 1:
+        out.append(TEST_LABEL)
+    c = int.from_bytes(hashlib.sha256(b"cudasp-label-v1").digest(), "big") % N_ORDER
+    j = 1
+    while len(out) < count:
+        pt = _ec_mul((j + 1) * c % N_ORDER, (GX, GY))
+        out.append(pt[0].to_bytes(32, "little") + pt[1].to_bytes(32, "little"))
+        j += 1
+    return out
+
+
+def synth_s0():
+    s0 = int.from_bytes(hashlib.sha256(b"cudasp-synth-v1").digest(), "big") % N_ORDER
+    return s0.to_bytes(32, "little")
+
+
+class Table:
+    """One rank's resident synthetic table, batch-major."""
+
+    def __init__(self, lib, device, rows, batch, k, labels, first_global, dev_stream):
+        self.rows, self.batch, self.k = rows, batch, k
+        self.nb = (rows + batch - 1) // batch
+        self.sizes = [min(batch, rows - b * batch) for b in range(self.nb)]
+        dev = torch.device("cuda", device)
+        self.tx = torch.empty((self.nb, 8, batch), dtype=torch.int32, device=dev)
+        self.ty = torch.empty((self.nb, 8, batch), dtype=torch.int32, device=dev)
+        self.outs = torch.empty((self.nb, batch * k), dtype=torch.int64, device=dev)
+        self.offs = torch.empty((self.nb, batch), dtype=torch.int32, device=dev)
+        self.lens = torch.empty((self.nb, batch), dtype=torch.int32, device=dev)
+        self.flags = torch.zeros((self.nb, batch), dtype=torch.uint8, device=dev)
+        self.match_rows = torch.zeros((self.nb, batch), dtype=torch.int32, device=dev)
+        self.match_count = torch.zeros((self.nb,), dtype=torch.int32, device=dev)
+        s0 = synth_s0()
+        st = ctypes.c_void_p(dev_stream.cuda_stream)
+        for b in range(self.nb):
+            m = self.sizes[b]
+            g0 = first_global + b * batch
+            _native.check(lib.cudasp_synth_tweak_columns(device, s0, g0, m, self.tx[b].data_ptr(),
+                                                         self.ty[b].data_ptr(), st))
+            _native.check(lib.cudasp_synth_outputs(OUTPUT_SEED, g0, m, k, self.outs[b].data_ptr(),
+                                                   self.offs[b].data_ptr(), self.lens[b].data_ptr(), st))
+        torch.cuda.synchronize(dev)
+        # Plant true values (computed by the product's own stage outputs; the
+        # test suite checks those against the oracle): base value every 1000th
+        # global row, label-0 value on the row after it when labels exist.
+        self.expected = 0
+        per_batch = 2 * ((batch + PLANT_EVERY - 1) // PLANT_EVERY) + 2
+        planter = Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=per_batch, device=device)
+        for b in range(self.nb):
+            m = self.sizes[b]
+            g0 = first_global + b * batch
+            base_idx = [i for i in range((-g0) % PLANT_EVERY, m, PLANT_EVERY)]
+            lab_idx = [i for i in range((1 - g0) % PLANT_EVERY, m, PLANT_EVERY)] if labels else []
+            idx = base_idx + lab_idx
+            if not idx:
+                continue
+            it = torch.tensor(idx, dtype=torch.int64, device=dev)
+            gx = self.cols(self.tx, b).index_select(1, it).contiguous()
+            gy = self.cols(self.ty, b).index_select(1, it).contiguous()
+            t = torch.empty((8, len(idx)), dtype=torch.int32, device=dev)
+            vals = torch.empty((1 + len(labels), len(idx)), dtype=torch.int64, device=dev)
+            planter.row_values_device(gx, gy, t, vals)
+            planter.sync()
+            nbase = len(base_idx)
+            pos = it * k  # slot 0 of each planted row's outputs list
+            self.outs[b].index_copy_(0, pos[:nbase], vals[0, :nbase])
+            if lab_idx:
+                self.outs[b].index_copy_(0, pos[nbase:], vals[1, nbase:])
+            self.expected += len(idx)
+        planter.close()
+        torch.cuda.synchronize(dev)
+
+
+def _cols(self, arr, b):
+    """Batch b of a column array as its (8, m) column-major view (limb j of row
+    i at j*m + i, the layout the kernels read)."""
+    m = self.sizes[b]
+    return arr[b].view(-1)[: 8 * m].view(8, m)
+
+
+Table.cols = _cols
+
+
+def run_step(tab, scanners, streams, events=None):
+    tab.match_count.zero_()
+    for b in range(tab.nb):
+        s = b % len(scanners)
+        st = streams[s]
+        with torch.cuda.stream(st):
+            m = tab.sizes[b]
+            if events is not None:
+                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                e0.record(st)
+                scanners[s].stage_shared_secret(tab.tx[b], tab.ty[b], m, st)
+                e1.record(st)
+                scanners[s].stage_match(tab.outs[b], tab.offs[b], tab.lens[b], m, tab.flags[b],
+                                        tab.match_rows[b], tab.match_count[b:b + 1], st)
+                e2.record(st)
+                events.append((e0, e1, e2))
+            else:
+                scanners[s].scan_device(tab.tx[b], tab.ty[b], tab.outs[b], tab.offs[b], tab.lens[b],
+                                        tab.flags[b][:m], tab.match_rows[b], tab.match_count[b:b + 1], stream=st)
+
+
+def cpu_baseline(tab, labels, sample_rows, threads):
+    sys.path.insert(0, ROOT)
+    from oracle import oracle  # the C restatement: baseline + checker only
+    m = min(sample_rows, tab.sizes[0])
+    x = tab.cols(tab.tx, 0)[:, :m].cpu().numpy().view(np.uint32)
+    y = tab.cols(tab.ty, 0)[:, :m].cpu().numpy().view(np.uint32)
+    tweaks = np.ascontiguousarray(np.concatenate([x.T, y.T], axis=1).astype("<u4")).view(np.uint8).reshape(m, 64)
+    outs = tab.outs[0][: m * tab.k].cpu().numpy()
+    offs = tab.offs[0][:m].cpu().numpy().view(np.uint32)
+    lens = tab.lens[0][:m].cpu().numpy().view(np.uint32)
+    t0 = time.perf_counter()
+    flags, _ = oracle.scan(SCAN_KEY, SPEND_KEY, labels, tweaks, outs, offs, lens, threads=threads)
+    dt = time.perf_counter() - t0
+    gpu_flags = tab.flags[0][:m].cpu().numpy()
+    return dict(value=m / dt, unit="tx/s", cores=threads, kind="port",
+                sample="first %d rows of the rank-0 table (batch 0), %d labels, %d outputs/row, "
+                       "oracle/cudasp_oracle.c with %d pthreads" % (m, len(labels), tab.k, threads),
+                seconds=round(dt, 3), flags_match_gpu=bool(np.array_equal(flags, gpu_flags)),
+                sample_matches=int(flags.sum()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rows", type=int, default=32_700_000, help="rows per rank")
+    ap.add_argument("--batch-size", type=int, default=300_000)
+    ap.add_argument("--labels", type=int, default=0)
+    ap.add_argument("--outputs-per-row", type=int, default=2)
+    ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--cpu-rows", type=int, default=300000)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_k_shared_secret.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = local if world > 1 else 0
+    torch.cuda.set_device(device)
+    lib = _native.load()
+
+    labels = label_keys(args.labels)
+    gen_stream = torch.cuda.Stream(device)
+    t_setup = time.perf_counter()
+    tab = Table(lib, device, args.rows, args.batch_size, args.outputs_per_row, labels,
+                first_global=rank * args.rows, dev_stream=gen_stream)
+    streams = [torch.cuda.Stream(device) for _ in range(args.streams)]
+    scanners = [Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=args.batch_size, device=device)
+                for _ in range(args.streams)]
+    setup_s = time.perf_counter() - t_setup
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        run_step(tab, scanners, streams)
+    torch.cuda.synchronize(device)
+
+    times = []
+    for _ in range(args.steps):
+        barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        run_step(tab, scanners, streams)
+        torch.cuda.synchronize(device)
+        barrier()
+        times.append(time.perf_counter() - t0)
+    step_s = float(np.mean(times))
+    total_s = float(np.sum(times))
+    if world > 1:
+        tt = torch.tensor([total_s], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        total_s = float(tt.item())
+    found = int(tab.match_count.sum().item())
+    flagged = int(tab.flags.sum().item())
+
+    # Per-launch kernel durations (HIP events on the launching stream), one
+    # extra pass with each batch split into its two stage launches.
+    events = []
+    run_step(tab, scanners, streams, events=events)
+    torch.cuda.synchronize(device)
+    ka = [e0.elapsed_time(e1) for e0, e1, _ in events]
+    kb = [e1.elapsed_time(e2) for _, e1, e2 in events]
+    ka_ms, kb_ms = float(np.mean(ka)), float(np.mean(kb))
+    rows_per_launch = float(np.mean(tab.sizes))
+    algo_bytes = bytes_per_row(args.outputs_per_row) * rows_per_launch
+    achieved_gbs = algo_bytes / (ka_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc_summary):
+        with open(args.pmc_summary) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    rows_total = args.rows * world * args.steps
+    value = rows_total / total_s
+    result = dict(
+        metric=METRIC, value=value, unit="tx/s", n_gpus=world, steps=args.steps, warmup=args.warmup,
+        ms_per_step=total_s / args.steps * 1e3, higher_is_better=True, scaling="weak", vs_baseline=None,
+        dtype="u32", data="synthetic",
+        config=dict(workload="32.7M-row synthetic tweak table per rank, %d labels, %d outputs/row, "
+                             "batch_size %d, device-resident (BASELINE.json configs[3] shape; each rank "
+                             "scans its own table)" % (args.labels, args.outputs_per_row, args.batch_size),
+                    rows_per_rank=args.rows, batch_size=args.batch_size, labels=args.labels,
+                    outputs_per_row=args.outputs_per_row, streams=args.streams, parallelism="dp%d" % world),
+        roofline=dict(bound="hbm", achieved=achieved_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
+                      frac=achieved_gbs / HBM_PEAK_GBS, traffic=traffic,
+                      kernel="k_shared_secret", kernel_ms=ka_ms, match_kernel_ms=kb_ms,
+                      algorithmic_bytes_per_launch=algo_bytes, rows_per_launch=rows_per_launch,
+                      note="integer-VALU-bound path; see alu_roofline"),
+        matches=dict(found=found, flagged=flagged, expected_planted_rank0=tab.expected),
+        setup_s=round(setup_s, 2),
+    )
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(tab, labels, args.cpu_rows, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    for s in scanners:
+        s.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

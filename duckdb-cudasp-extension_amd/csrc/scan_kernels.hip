@@ -152,6 +152,92 @@ __global__ __launch_bounds__(BLOCK) void k_rows_to_cols(const uint8_t* __restric
   }
 }
 
+
+// ------------------------------------------------------ synthetic tables
+// Deterministic benchmark/test inputs: tweak T_i = (s0 + i) G
+// and splitmix64 outputs.  Generation only; never part of a scan.
+struct SynthConsts {
+  uint32_t s0[8];  // < n
+  uint32_t c_odd[16];
+  uint32_t c_even[16];
+};
+
+__device__ __forceinline__ void add_index_mod_n(uint32_t s[8], const uint32_t s0[8], uint64_t idx) {
+  const uint32_t nn[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
+                          0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t add = i == 0 ? (idx & 0xFFFFFFFFu) : (i == 1 ? (idx >> 32) : 0);
+    c += (uint64_t)s0[i] + add;
+    s[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  // s >= n ?  (s < 2^256 + n, so compare including the carry word)
+  bool ge = c != 0;
+  if (!ge) {
+    ge = true;
+    for (int i = 7; i >= 0; i--) {
+      if (s[i] != nn[i]) {
+        ge = s[i] > nn[i];
+        break;
+      }
+    }
+  }
+  if (ge) {
+    int64_t b = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      b += (int64_t)s[i] - nn[i];
+      s[i] = (uint32_t)b;
+      b >>= 32;
+    }
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_synth_tweaks(SynthConsts c, uint64_t first, uint32_t n,
+                                                        const uint32_t* __restrict__ fb, uint32_t* __restrict__ x,
+                                                        uint32_t* __restrict__ y) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < n; row += stride) {
+    uint32_t s[8];
+    add_index_mod_n(s, c.s0, first + row);
+    gej R;
+    fixed_base_mul(R, s, fb, c.c_odd, c.c_even);
+    fe zi;
+    fe_inv(zi, R.z);
+    ge A;
+    gej_to_ge_zinv(A, R, zi);
+    uint32_t wx[8], wy[8];
+    fe_to_u32x8(wx, A.x);
+    fe_to_u32x8(wy, A.y);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      x[(size_t)j * n + row] = wx[j];
+      y[(size_t)j * n + row] = wy[j];
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_synth_outputs(uint64_t seed, uint64_t first, uint32_t n, uint32_t k,
+                                                         int64_t* __restrict__ outs, uint32_t* __restrict__ offs,
+                                                         uint32_t* __restrict__ lens) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < n; row += stride) {
+    uint64_t g = first + row;
+    offs[row] = row * k;
+    lens[row] = k;
+    for (uint32_t j = 0; j < k; j++) outs[(size_t)row * k + j] = (int64_t)splitmix64(seed ^ (g * k + j));
+  }
+}
+
 // ------------------------------------------------------------- host helpers
 namespace {
 
@@ -427,6 +513,74 @@ int cudasp_scan_host(cudasp_scanner* s, const uint8_t* h_tweak_keys, const int64
   if (rc != CUDASP_OK) return rc;
   HIP_TRY(hipMemcpyAsync(h_match_flags, s->d_flags, n, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  return CUDASP_OK;
+}
+
+int cudasp_stage_shared_secret_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint32_t* d_tweak_y,
+                                      uint32_t n, uint32_t* d_t, void* stream) {
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  if (n == 0) return CUDASP_OK;
+  if (!d_tweak_x || !d_tweak_y || !d_t) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
+  if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
+  DeviceGuard g(s->device);
+  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  uint32_t blocks = grid_for(n);
+  if (blocks * BLOCK > s->slots) blocks = s->slots / BLOCK;
+  hipLaunchKernelGGL(k_shared_secret, dim3(blocks), dim3(BLOCK), 0, st, d_tweak_x, d_tweak_y, n, s->d_naf,
+                     s->consts, s->d_vscratch, d_t);
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+int cudasp_stage_match_device(cudasp_scanner* s, const uint32_t* d_t, const int64_t* d_outputs,
+                              const uint32_t* d_output_offsets, const uint32_t* d_output_lengths, uint32_t n,
+                              uint8_t* d_match_flags, uint32_t* d_match_rows, uint32_t* d_match_count, void* stream) {
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  if (n == 0) return CUDASP_OK;
+  if (!d_t || !d_output_offsets || !d_output_lengths || !d_match_flags)
+    return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
+  if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
+  DeviceGuard g(s->device);
+  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  uint32_t blocks = grid_for(n);
+  if (blocks * BLOCK > s->slots) blocks = s->slots / BLOCK;
+  bool compact = d_match_rows && d_match_count;
+  hipLaunchKernelGGL(k_match<false>, dim3(blocks), dim3(BLOCK), 0, st, d_t, n, s->d_fb, s->consts, s->d_labels,
+                     d_outputs, d_output_offsets, d_output_lengths, s->d_lscratch, d_match_flags,
+                     compact ? d_match_rows : nullptr, compact ? d_match_count : nullptr, nullptr);
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+int cudasp_synth_tweak_columns(int device, const uint8_t s0_le[32], uint64_t first_index, uint32_t n,
+                               uint32_t* d_x, uint32_t* d_y, void* stream) {
+  if (n == 0) return CUDASP_OK;
+  if (!s0_le || !d_x || !d_y) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  DeviceGuard g(device);
+  const uint32_t* fb = nullptr;
+  int rc = ensure_device_table(device, &fb);
+  if (rc != CUDASP_OK) return rc;
+  SynthConsts c;
+  host::Big<8> s0 = host::big_zero<8>();
+  for (int i = 0; i < 32; i++) s0.w[i / 4] |= (uint32_t)s0_le[i] << (8 * (i % 4));
+  s0 = host::scalar_reduce(s0);
+  for (int i = 0; i < 8; i++) c.s0[i] = s0.w[i];
+  const GenPowers& gp = gen_powers();
+  hp_words(c.c_odd, gp.q[FB_WINDOWS]);
+  hp_words(c.c_even, hp_add(gp.q[FB_WINDOWS], hp_neg(gp.q[0])));
+  hipLaunchKernelGGL(k_synth_tweaks, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, c, first_index, n, fb,
+                     d_x, d_y);
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+int cudasp_synth_outputs(uint64_t seed, uint64_t first_index, uint32_t n, uint32_t k, int64_t* d_outputs,
+                         uint32_t* d_offsets, uint32_t* d_lengths, void* stream) {
+  if (n == 0) return CUDASP_OK;
+  if (!d_outputs || !d_offsets || !d_lengths) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
+  hipLaunchKernelGGL(k_synth_outputs, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, seed, first_index, n,
+                     k, d_outputs, d_offsets, d_lengths);
+  HIP_TRY(hipGetLastError());
   return CUDASP_OK;
 }
 

@@ -220,14 +220,13 @@ CUDASP_HD void fb_entry(ge& P, const uint32_t* table, int window, uint32_t bits1
   if (neg) ge_neg(P, P);
 }
 
-// Stage B.  Returns whether the row matches; if values != nullptr, writes the
-// base value and one value per label (values[j * vstride]).
-CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k,
-                         const uint32_t* labels, const int64_t* outputs, uint32_t off, uint32_t len,
-                         const Scratch& sc, int64_t* values, uint32_t vstride) {
+// P = t*G (Jacobian) from the fixed-base table.  t: 8 LE words, any 256-bit
+// value (not reduced mod n, like the reference, src/cudasp_gpu.cu:862-877;
+// n*G = O makes that irrelevant).  c_odd / c_even: 2^256 G and 2^256 G - G.
+CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb_table, const uint32_t* c_odd,
+                              const uint32_t* c_even) {
   // t even -> use t+1 and add -G at the end (odd-digit recoding needs an odd
-  // scalar).  t is not reduced mod n, like the reference
-  // (src/cudasp_gpu.cu:862-877); n*G = O makes that irrelevant.
+  // scalar).
   uint32_t t[9];
 #pragma unroll
   for (int i = 0; i < 8; i++) t[i] = t_in[i];
@@ -239,7 +238,6 @@ CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const
   // The window loop is not unrolled (16 mixed additions would blow the
   // instruction cache), so t is consumed by shifting instead of indexing a
   // register array with the loop counter (that would spill to scratch).
-  gej R;
 #pragma unroll 1
   for (int i = 0; i < FB_WINDOWS; i++) {
     uint32_t bits = (t[0] >> 1) & 0xFFFFu;
@@ -255,8 +253,17 @@ CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const
     }
   }
   ge C;
-  ge_from_words(C, even ? k.c_even : k.c_odd);
-  gej_add_ge(R, R, C);  // P0 = t*G (Jacobian)
+  ge_from_words(C, even ? c_even : c_odd);
+  gej_add_ge(R, R, C);
+}
+
+// Stage B.  Returns whether the row matches; if values != nullptr, writes the
+// base value and one value per label (values[j * vstride]).
+CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k,
+                         const uint32_t* labels, const int64_t* outputs, uint32_t off, uint32_t len,
+                         const Scratch& sc, int64_t* values, uint32_t vstride) {
+  gej R;
+  fixed_base_mul(R, t_in, fb_table, k.c_odd, k.c_even);  // P0 = t*G
   // B is added on its own (not folded into c_*), so F = P0 + B is the same
   // single chord addition as the reference's even for a spend key that is not
   // on the curve.

@@ -81,6 +81,29 @@ class Scanner:
         _native.check(self._lib.cudasp_row_values_device(
             self._h, _ptr(tweak_x), _ptr(tweak_y), n, _ptr(t_out), _ptr(values), st))
 
+    def stage_shared_secret(self, tweak_x, tweak_y, n, stream=None, t_out=None):
+        """Launch only stage A (d*T, serialize, tagged hash) for n rows; t goes to
+        t_out or to a scanner-held buffer used by the next stage_match."""
+        if t_out is None:
+            import torch
+            if getattr(self, "_t", None) is None:
+                self._t = torch.empty((8 * self.max_rows,), dtype=torch.int32,
+                                      device=torch.device("cuda", self.device))
+            t_out = self._t
+        self._t_last = t_out
+        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        _native.check(self._lib.cudasp_stage_shared_secret_device(
+            self._h, _ptr(tweak_x), _ptr(tweak_y), int(n), _ptr(t_out), st))
+
+    def stage_match(self, outputs, offsets, lengths, n, flags, match_rows=None, match_count=None, stream=None,
+                    t_in=None):
+        """Launch only stage B on the t of the previous stage_shared_secret."""
+        t_in = self._t_last if t_in is None else t_in
+        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        _native.check(self._lib.cudasp_stage_match_device(
+            self._h, _ptr(t_in), _ptr(outputs), _ptr(offsets), _ptr(lengths), int(n), _ptr(flags),
+            _ptr(match_rows), _ptr(match_count), st))
+
     def sync(self):
         _native.check(self._lib.cudasp_scanner_sync(self._h))
 

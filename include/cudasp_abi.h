@@ -101,6 +101,23 @@ int cudasp_scanner_sync(cudasp_scanner* s);
 int cudasp_tweaks_to_columns(const uint8_t* d_tweak_rows, uint32_t n, uint32_t* d_tweak_x, uint32_t* d_tweak_y,
                              void* stream);
 
+/* Stage-level launches (the two kernels of cudasp_scan_device, separately;
+ * used to time each kernel).  Asynchronous on `stream`. */
+int cudasp_stage_shared_secret_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint32_t* d_tweak_y,
+                                      uint32_t n, uint32_t* d_t, void* stream);
+int cudasp_stage_match_device(cudasp_scanner* s, const uint32_t* d_t, const int64_t* d_outputs,
+                              const uint32_t* d_output_offsets, const uint32_t* d_output_lengths, uint32_t n,
+                              uint8_t* d_match_flags, uint32_t* d_match_rows, uint32_t* d_match_count, void* stream);
+
+/* Synthetic benchmark tables, generated on `device`:
+ * tweak rows T_i = (s0 + first_index + i) G as x/y columns (8 x n each), and
+ * k splitmix64 outputs per row: outputs[i*k + j] = splitmix64(seed ^ ((first_index + i)*k + j)),
+ * offsets[i] = i*k, lengths[i] = k. */
+int cudasp_synth_tweak_columns(int device, const uint8_t s0_le[32], uint64_t first_index, uint32_t n,
+                               uint32_t* d_x, uint32_t* d_y, void* stream);
+int cudasp_synth_outputs(uint64_t seed, uint64_t first_index, uint32_t n, uint32_t k, int64_t* d_outputs,
+                         uint32_t* d_offsets, uint32_t* d_lengths, void* stream);
+
 /* -------------------------------------------- reference three-phase ABI */
 void* LaunchBatchScan(uint32_t** managed_points_x, uint32_t** managed_points_y, const uint32_t* h_scalar,
                       const uint32_t* h_spend_pubkey_x, const uint32_t* h_spend_pubkey_y,
