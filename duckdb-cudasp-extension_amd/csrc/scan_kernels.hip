@@ -358,6 +358,10 @@ extern "C" {
 
 const char* cudasp_last_error(void) { return g_last_error.c_str(); }
 
+// Used by the table-function host (csrc/host) to report through the same
+// thread-local message; not part of the public header.
+void cudasp_internal_set_error(const char* msg) { g_last_error = msg ? msg : ""; }
+
 const char* cudasp_version(void) { return CUDASP_VERSION_STRING; }
 
 int cudasp_device_count(void) {

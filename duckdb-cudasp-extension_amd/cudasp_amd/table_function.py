@@ -1,0 +1,238 @@
+"""cudasp_scan(...) -- the reference's SQL table function, driven from Python.
+
+This is a thin ctypes driver of the C++ table-function host
+(csrc/host/cudasp_host.cpp, ABI include/cudasp_host.h) playing the role of
+DuckDB's executor: it binds the arguments (same validation and messages as
+CudaspScanBind, src/cudasp_extension.cu:420-509), feeds the input table to one
+local state per "executor thread" in DuckDB-sized chunks of <= 2048 rows
+(CudaspScanFunction :534-552), then finalizes every thread; the last one emits
+the matches (CudaspScanFinalFunction :554-624).
+
+    rows = [(txid: bytes, height: int, tweak_key: bytes(64), outputs: [int|None] | None), ...]
+    cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size=...)
+      -> [(txid, height, tweak_key), ...]   (order unspecified, like the reference)
+"""
+import ctypes
+import threading
+
+from . import _native
+
+VECTOR_SIZE = 2048
+TF_HAVE_MORE_OUTPUT = 1
+
+
+class InvalidInputException(ValueError):
+    """Raised with the reference's InvalidInputException messages."""
+
+
+class _BlobArg(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("size", ctypes.c_uint64), ("is_blob", ctypes.c_int)]
+
+
+class _Chunk(ctypes.Structure):
+    _fields_ = [
+        ("count", ctypes.c_uint32),
+        ("txid_data", ctypes.POINTER(ctypes.c_void_p)),
+        ("txid_size", ctypes.POINTER(ctypes.c_uint32)),
+        ("txid_valid", ctypes.POINTER(ctypes.c_uint8)),
+        ("height", ctypes.POINTER(ctypes.c_int32)),
+        ("height_valid", ctypes.POINTER(ctypes.c_uint8)),
+        ("tweak_data", ctypes.POINTER(ctypes.c_void_p)),
+        ("tweak_size", ctypes.POINTER(ctypes.c_uint32)),
+        ("tweak_valid", ctypes.POINTER(ctypes.c_uint8)),
+        ("list_offset", ctypes.POINTER(ctypes.c_uint64)),
+        ("list_length", ctypes.POINTER(ctypes.c_uint64)),
+        ("list_valid", ctypes.POINTER(ctypes.c_uint8)),
+        ("child_values", ctypes.POINTER(ctypes.c_int64)),
+        ("child_valid", ctypes.POINTER(ctypes.c_uint8)),
+    ]
+
+
+class _Output(ctypes.Structure):
+    _fields_ = [
+        ("count", ctypes.c_uint32),
+        ("txid_data", ctypes.c_void_p * VECTOR_SIZE),
+        ("txid_size", ctypes.c_uint32 * VECTOR_SIZE),
+        ("height", ctypes.c_int32 * VECTOR_SIZE),
+        ("tweak_data", ctypes.c_void_p * VECTOR_SIZE),
+        ("tweak_size", ctypes.c_uint32 * VECTOR_SIZE),
+    ]
+
+
+_P = ctypes.c_void_p
+_HOST_SIGNATURES = {
+    "cudasp_tf_bind": (ctypes.c_int, [ctypes.c_uint32, _BlobArg, _BlobArg, ctypes.c_int, ctypes.POINTER(_BlobArg),
+                                      ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                      ctypes.POINTER(_P), ctypes.c_char_p, ctypes.c_size_t]),
+    "cudasp_tf_bind_free": (None, [_P]),
+    "cudasp_tf_bind_batch_size": (ctypes.c_uint64, [_P]),
+    "cudasp_tf_init": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
+    "cudasp_tf_global_free": (None, [_P]),
+    "cudasp_tf_num_gpus": (ctypes.c_int, [_P]),
+    "cudasp_tf_local_init": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
+    "cudasp_tf_local_free": (None, [_P]),
+    "cudasp_tf_local_gpu": (ctypes.c_int, [_P]),
+    "cudasp_tf_function": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Chunk)]),
+    "cudasp_tf_final": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Output)]),
+}
+
+_host = None
+
+
+def _lib():
+    global _host
+    if _host is None:
+        lib = _native.load()
+        for name, (res, args) in _HOST_SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _host = lib
+    return _host
+
+
+def _blob(value):
+    """(keep-alive, _BlobArg) for a Python value; bytes-like = BLOB."""
+    if isinstance(value, (bytes, bytearray, memoryview)):
+        buf = ctypes.create_string_buffer(bytes(value), max(1, len(value)))
+        return buf, _BlobArg(ctypes.cast(buf, ctypes.c_void_p), len(value), 1)
+    return None, _BlobArg(None, 0, 0)
+
+
+class BoundScan:
+    """Bind data of one cudasp_scan call (CudaspScanBindData)."""
+
+    def __init__(self, scan_private_key, spend_public_key, label_keys, batch_size=None, arg_count=4):
+        lib = _lib()
+        keep = []
+        k1, a1 = _blob(scan_private_key)
+        k2, a2 = _blob(spend_public_key)
+        keep += [k1, k2]
+        is_list = isinstance(label_keys, (list, tuple))
+        labels = list(label_keys) if is_list else []
+        arr = (_BlobArg * max(1, len(labels)))()
+        for i, l in enumerate(labels):
+            k, arr[i] = _blob(l)
+            keep.append(k)
+        has_bs = batch_size is not None
+        bs_int = isinstance(batch_size, int) and not isinstance(batch_size, bool)
+        err = ctypes.create_string_buffer(512)
+        h = _P()
+        rc = lib.cudasp_tf_bind(arg_count, a1, a2, 1 if is_list else 0, arr, len(labels), 1 if has_bs else 0,
+                                1 if bs_int else 0, int(batch_size) if bs_int else 0, ctypes.byref(h), err, 512)
+        if rc != 0:
+            raise InvalidInputException(err.value.decode())
+        self._h = h
+        self.batch_size = lib.cudasp_tf_bind_batch_size(h)
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib().cudasp_tf_bind_free(self._h)
+            self._h = None
+
+
+def _make_chunk(rows):
+    """Build a DuckDB-like unified chunk from Python rows; returns (keep, chunk)."""
+    n = len(rows)
+    keep = []
+    txid_ptrs = (ctypes.c_void_p * n)()
+    txid_size = (ctypes.c_uint32 * n)()
+    txid_valid = (ctypes.c_uint8 * n)()
+    height = (ctypes.c_int32 * n)()
+    height_valid = (ctypes.c_uint8 * n)()
+    tweak_ptrs = (ctypes.c_void_p * n)()
+    tweak_size = (ctypes.c_uint32 * n)()
+    tweak_valid = (ctypes.c_uint8 * n)()
+    list_offset = (ctypes.c_uint64 * n)()
+    list_length = (ctypes.c_uint64 * n)()
+    list_valid = (ctypes.c_uint8 * n)()
+    child = []
+    child_ok = []
+    for i, (txid, h, tweak, outs) in enumerate(rows):
+        if txid is not None:
+            b = ctypes.create_string_buffer(bytes(txid), max(1, len(txid)))
+            keep.append(b)
+            txid_ptrs[i] = ctypes.cast(b, ctypes.c_void_p)
+            txid_size[i] = len(txid)
+            txid_valid[i] = 1
+        if h is not None:
+            height[i] = h
+            height_valid[i] = 1
+        if tweak is not None:
+            b = ctypes.create_string_buffer(bytes(tweak), max(1, len(tweak)))
+            keep.append(b)
+            tweak_ptrs[i] = ctypes.cast(b, ctypes.c_void_p)
+            tweak_size[i] = len(tweak)
+            tweak_valid[i] = 1
+        list_offset[i] = len(child)
+        if outs is not None:
+            list_valid[i] = 1
+            list_length[i] = len(outs)
+            for o in outs:
+                child.append(0 if o is None else o)
+                child_ok.append(0 if o is None else 1)
+    cv = (ctypes.c_int64 * max(1, len(child)))(*child)
+    cvalid = (ctypes.c_uint8 * max(1, len(child_ok)))(*child_ok)
+    keep += [txid_ptrs, txid_size, txid_valid, height, height_valid, tweak_ptrs, tweak_size, tweak_valid,
+             list_offset, list_length, list_valid, cv, cvalid]
+    c = _Chunk(n, txid_ptrs, txid_size, txid_valid, height, height_valid, tweak_ptrs, tweak_size, tweak_valid,
+               list_offset, list_length, list_valid, cv, cvalid)
+    return keep, c
+
+
+def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size=None, threads=1,
+                chunk_rows=VECTOR_SIZE):
+    """Run the table function over `rows` with `threads` executor threads.
+    Chunks are dealt round-robin to the threads, as DuckDB's parallel scan
+    would hand out morsels; each thread gets its own local state (and GPU,
+    round-robin, CudaspScanLocalInit :523-529)."""
+    lib = _lib()
+    bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size)
+    g = _P()
+    _native.check(lib.cudasp_tf_init(bound._h, ctypes.byref(g)))
+    locals_ = []
+    try:
+        for _ in range(threads):
+            l = _P()
+            _native.check(lib.cudasp_tf_local_init(g, ctypes.byref(l)))
+            locals_.append(l)
+        chunks = [rows[i:i + chunk_rows] for i in range(0, len(rows), chunk_rows)]
+        errors = []
+        results = []
+        res_lock = threading.Lock()
+
+        def worker(t):
+            try:
+                for ci in range(t, len(chunks), threads):
+                    keep, c = _make_chunk(chunks[ci])
+                    rc = lib.cudasp_tf_function(bound._h, g, locals_[t], ctypes.byref(c))
+                    if rc < 0:
+                        _native.check(rc)
+                out = _Output()
+                while True:
+                    rc = lib.cudasp_tf_final(bound._h, g, locals_[t], ctypes.byref(out))
+                    if rc < 0:
+                        _native.check(rc)
+                    got = []
+                    for i in range(out.count):
+                        got.append((ctypes.string_at(out.txid_data[i], out.txid_size[i]), out.height[i],
+                                    ctypes.string_at(out.tweak_data[i], out.tweak_size[i])))
+                    with res_lock:
+                        results.extend(got)
+                    if rc != TF_HAVE_MORE_OUTPUT:
+                        break
+            except Exception as e:  # surfaced after join
+                errors.append(e)
+
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        if errors:
+            raise errors[0]
+        return results
+    finally:
+        for l in locals_:
+            lib.cudasp_tf_local_free(l)
+        lib.cudasp_tf_global_free(g)

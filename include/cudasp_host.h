@@ -1,0 +1,122 @@
+/*
+ * cudasp_host.h -- C ABI of the rebuilt cudasp_scan table-function host.
+ *
+ * This is the DuckDB-independent core of the reference's host plumbing
+ * (src/cudasp_extension.cu:87-659): bind-time validation, per-thread row
+ * accumulation, batch trigger, round-robin GPU assignment, batch processing
+ * through the kernel ABI of cudasp_abi.h, the mutex-guarded global match list
+ * and the single-thread emit in chunks of at most 2048 rows.  A DuckDB
+ * extension (duckdb_ext/cudasp_extension.cpp) maps DuckDB's TableFunction
+ * callbacks 1:1 onto these calls; the tests drive the same calls directly.
+ *
+ *   reference                        this ABI
+ *   CudaspScanBind        :420-509   cudasp_tf_bind
+ *   CudaspScanInit        :511-514   cudasp_tf_init
+ *   CudaspScanLocalInit   :516-532   cudasp_tf_local_init
+ *   CudaspScanFunction    :534-552   cudasp_tf_function
+ *   CudaspScanFinalFunction :554-624 cudasp_tf_final
+ *
+ * Every function is thread-safe in the way DuckDB calls the reference's: one
+ * local state per executor thread, shared bind data and global state.
+ * Failure messages of cudasp_tf_function / cudasp_tf_final are available from
+ * cudasp_last_error() (cudasp_abi.h) on the calling thread.
+ */
+#ifndef CUDASP_HOST_H
+#define CUDASP_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CUDASP_TF_NEED_MORE_INPUT 0 /* OperatorResultType::NEED_MORE_INPUT */
+#define CUDASP_TF_FINISHED 0        /* OperatorFinalizeResultType::FINISHED */
+#define CUDASP_TF_HAVE_MORE_OUTPUT 1 /* OperatorFinalizeResultType::HAVE_MORE_OUTPUT */
+#define CUDASP_TF_VECTOR_SIZE 2048  /* STANDARD_VECTOR_SIZE */
+#define CUDASP_TF_DEFAULT_BATCH 300000
+
+typedef struct cudasp_tf_bind_data cudasp_tf_bind_data;
+typedef struct cudasp_tf_global cudasp_tf_global;
+typedef struct cudasp_tf_local cudasp_tf_local;
+
+/* One bind-time argument as DuckDB hands it over: is_blob = the value's
+ * logical type is BLOB. */
+typedef struct {
+  const uint8_t* data;
+  uint64_t size;
+  int is_blob;
+} cudasp_tf_blob_arg;
+
+/* Bind.  arg_count = number of positional arguments (4 expected);
+ * label_keys_is_list = the 4th argument is a LIST; has_batch_size /
+ * batch_size_is_integer / batch_size as for the named parameter.  On failure
+ * returns a negative code and writes the reference's InvalidInputException
+ * message (NUL-terminated, truncated to err_cap) into err. */
+int cudasp_tf_bind(uint32_t arg_count, cudasp_tf_blob_arg scan_private_key, cudasp_tf_blob_arg spend_public_key,
+                   int label_keys_is_list, const cudasp_tf_blob_arg* label_keys, uint32_t label_count,
+                   int has_batch_size, int batch_size_is_integer, int64_t batch_size, cudasp_tf_bind_data** out,
+                   char* err, size_t err_cap);
+void cudasp_tf_bind_free(cudasp_tf_bind_data* b);
+uint64_t cudasp_tf_bind_batch_size(const cudasp_tf_bind_data* b);
+
+/* Global state (one per query): detects the devices. */
+int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out);
+void cudasp_tf_global_free(cudasp_tf_global* g);
+int cudasp_tf_num_gpus(const cudasp_tf_global* g);
+
+/* Local state (one per executor thread): round-robin GPU. */
+int cudasp_tf_local_init(cudasp_tf_global* g, cudasp_tf_local** out);
+void cudasp_tf_local_free(cudasp_tf_local* l);
+int cudasp_tf_local_gpu(const cudasp_tf_local* l);
+
+/* One input chunk (<= 2048 rows) of the input table, columns by position:
+ * 0 txid BLOB, 1 height INTEGER, 2 tweak_key BLOB, 3 outputs BIGINT[]
+ * (src/cudasp_extension.cu:159-163), in DuckDB's unified form.  Validity
+ * arrays may be NULL (= all valid).  outputs: per-row list entries
+ * (offset/length into child_values), list validity, child validity. */
+typedef struct {
+  uint32_t count;
+  const uint8_t* const* txid_data;
+  const uint32_t* txid_size;
+  const uint8_t* txid_valid;
+  const int32_t* height;
+  const uint8_t* height_valid;
+  const uint8_t* const* tweak_data;
+  const uint32_t* tweak_size;
+  const uint8_t* tweak_valid;
+  const uint64_t* list_offset;
+  const uint64_t* list_length;
+  const uint8_t* list_valid;
+  const int64_t* child_values;
+  const uint8_t* child_valid;
+} cudasp_tf_chunk;
+
+/* in_out_function: accumulate, run a batch once batch_size rows are held.
+ * Returns CUDASP_TF_NEED_MORE_INPUT or a negative error code (message via
+ * cudasp_last_error()). */
+int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
+                       const cudasp_tf_chunk* chunk);
+
+/* One output chunk: up to 2048 matching rows (txid, height, tweak_key).  The
+ * pointers stay valid until the global state is freed. */
+typedef struct {
+  uint32_t count;
+  const uint8_t* txid_data[CUDASP_TF_VECTOR_SIZE];
+  uint32_t txid_size[CUDASP_TF_VECTOR_SIZE];
+  int32_t height[CUDASP_TF_VECTOR_SIZE];
+  const uint8_t* tweak_data[CUDASP_TF_VECTOR_SIZE];
+  uint32_t tweak_size[CUDASP_TF_VECTOR_SIZE];
+} cudasp_tf_output;
+
+/* in_out_function_final: flush this thread's rows; the last thread to finish
+ * emits all matches.  Returns CUDASP_TF_FINISHED (0) or
+ * CUDASP_TF_HAVE_MORE_OUTPUT (1), or a negative error code. */
+int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l, cudasp_tf_output* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CUDASP_HOST_H */

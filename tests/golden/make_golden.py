@@ -153,6 +153,7 @@ def parse_sql_test(path):
             labels = [blob(b).hex() for b in blobs[2:]]
             bs = re.search(r"batch_size := (\d+)", sql)
             queries.append(dict(line=text[:text.index(sql)].count("\n") + 1,
+                                test_data_rows_visible=len(tables["test_data"]),
                                 select="count" if "COUNT(*)" in sql else "height",
                                 table=table.group(1),
                                 where_height=int(table.group(2)) if table.group(2) else None,
@@ -168,7 +169,8 @@ def main():
     cache = {}
     for q in queries:
         if q["table"] == "test_data":
-            rows = [r for r in tables["test_data"] if q["where_height"] in (None, r["height"])]
+            visible = tables["test_data"][:q["test_data_rows_visible"]]
+            rows = [r for r in visible if q["where_height"] in (None, r["height"])]
             mult = 1
         else:
             rows = [tables[q["table"]]["row"]]
@@ -192,7 +194,7 @@ def main():
     kats = []
     seen = set()
     for q in queries:
-        for r in tables["test_data"]:
+        for r in tables["test_data"][:q["test_data_rows_visible"]]:
             if q["table"] != "test_data" or q["where_height"] not in (None, r["height"]):
                 continue
             key = (q["scan_key"], q["spend_key"], tuple(q["label_keys"]), r["tweak"])
@@ -234,7 +236,7 @@ def main():
         elif kind == 5 and outs:
             outs[0] = None  # NULL list element is dropped
             outs.append(st["v"])
-        rows.append(dict(txid=os.urandom(0).hex() + "%064x" % i, height=800000 + i, tweak=tweak.hex(),
+        rows.append(dict(txid="%064x" % i, height=800000 + i, tweak=tweak.hex(),
                          outputs=outs, v=st["v"], label_values=st["label_values"],
                          t="%064x" % st["t"], F_x="%064x" % st["F"][0],
                          match_all_labels=row_matches(st, outs),

@@ -1,0 +1,135 @@
+"""GPU: synthetic-table generation and full-batch properties.
+
+* generated tweak rows equal the oracle's (s0 + i) G (sampled indices);
+* per-row compare values on a few thousand synthetic rows with labels equal
+  the oracle's, bit for bit;
+* at the benchmark's batch size (300000 rows): every planted value is found,
+  results are deterministic, split-invariant (one batch vs two halves vs the
+  host path) and label-order invariant."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+SCAN = bytes.fromhex("2c1f0cb94db3946522cc1487256535dd33a1f911946baff817a72880064e690f")
+SPEND = bytes.fromhex("36cf8fcd4d4890ab6c1083aeb5b50c260c20acda7839120e3575836f6d85c95ce0d705e31ff9fdcce67a8f3598871c6dfbe6bcde8a51cb7b48b0f95be0ea94de")
+LABEL = bytes.fromhex("cd63f9212a2deebde8a71e9ea23f6f958c47c41d2ed74b9617fe6fb554d1524e292fabddbdcbb643eafc328875c46d75a1d697b2b31c42d38aa93f85eab34bc1")
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def s0():
+    return (int.from_bytes(hashlib.sha256(b"cudasp-synth-v1").digest(), "big") % N).to_bytes(32, "little")
+
+
+def synth(torch, first, n):
+    from cudasp_amd import _native
+    lib = _native.load()
+    x = torch.empty((8, n), dtype=torch.int32, device="cuda")
+    y = torch.empty((8, n), dtype=torch.int32, device="cuda")
+    outs = torch.empty((2 * n,), dtype=torch.int64, device="cuda")
+    offs = torch.empty((n,), dtype=torch.int32, device="cuda")
+    lens = torch.empty((n,), dtype=torch.int32, device="cuda")
+    _native.check(lib.cudasp_synth_tweak_columns(0, s0(), first, n, x.data_ptr(), y.data_ptr(), None))
+    _native.check(lib.cudasp_synth_outputs(0xC0DA5EED, first, n, 2, outs.data_ptr(), offs.data_ptr(),
+                                           lens.data_ptr(), None))
+    torch.cuda.synchronize()
+    return x, y, outs, offs, lens
+
+
+def rows_of(x, y):
+    xs = x.cpu().numpy().view(np.uint32)
+    ys = y.cpu().numpy().view(np.uint32)
+    return np.ascontiguousarray(np.concatenate([xs.T, ys.T], axis=1).astype("<u4")).view(np.uint8).reshape(-1, 64)
+
+
+def test_synth_tweaks_match_oracle(torch):
+    from oracle import oracle
+    first = 10**9
+    x, y, _, _, _ = synth(torch, first, 4096)
+    rows = rows_of(x, y)
+    for i in (0, 1, 2, 1000, 4095):
+        assert rows[i].tobytes() == oracle.synth_tweak(s0(), first + i)
+
+
+def test_values_match_oracle_with_labels(torch):
+    from cudasp_amd import Scanner
+    from oracle import oracle
+    n = 3000
+    x, y, outs, offs, lens = synth(torch, 777, n)
+    labels = [LABEL, SPEND]
+    with Scanner(SCAN, SPEND, labels, max_rows=n) as s:
+        t = torch.empty((8, n), dtype=torch.int32, device="cuda")
+        v = torch.empty((3, n), dtype=torch.int64, device="cuda")
+        s.row_values_device(x, y, t, v)
+        s.sync()
+    _, ov = oracle.scan(SCAN, SPEND, labels, rows_of(x, y), threads=16, want_values=True)
+    assert (v.cpu().numpy().T == ov).all()
+
+
+def _plant(torch, x, y, outs, labels, every=1000):
+    from cudasp_amd import Scanner
+    n = x.shape[1]
+    idx = torch.arange(0, n, every, device="cuda")
+    with Scanner(SCAN, SPEND, labels, max_rows=len(idx)) as s:
+        t = torch.empty((8, len(idx)), dtype=torch.int32, device="cuda")
+        v = torch.empty((1 + len(labels), len(idx)), dtype=torch.int64, device="cuda")
+        s.row_values_device(x.index_select(1, idx).contiguous(), y.index_select(1, idx).contiguous(), t, v)
+        s.sync()
+    outs.index_copy_(0, idx * 2, v[-1])  # plant the last label's (or base) value
+    return idx
+
+
+def test_full_batch_properties(torch):
+    from cudasp_amd import Scanner
+    n = 300000
+    x, y, outs, offs, lens = synth(torch, 0, n)
+    labels = [LABEL, SPEND]
+    planted = _plant(torch, x, y, outs, labels)
+    flags = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    rows = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    with Scanner(SCAN, SPEND, labels, max_rows=n) as s:
+        s.scan_device(x, y, outs, offs, lens, flags, rows, cnt)
+        s.sync()
+        f1 = flags.cpu().numpy().copy()
+        c = int(cnt.item())
+        assert set(np.nonzero(f1)[0].tolist()) == set(planted.cpu().tolist())
+        assert sorted(rows[:c].cpu().tolist()) == planted.cpu().tolist()
+        # deterministic
+        flags.zero_()
+        s.scan_device(x, y, outs, offs, lens, flags)
+        s.sync()
+        assert (flags.cpu().numpy() == f1).all()
+        # split invariance: two halves as separate batches
+        h = n // 2
+        parts = []
+        for a, b in ((0, h), (h, n)):
+            xs, ys = x[:, a:b].contiguous(), y[:, a:b].contiguous()
+            o = outs[2 * a:2 * b].contiguous()
+            of = (offs[a:b] - 2 * a).contiguous()
+            fl = torch.zeros(b - a, dtype=torch.uint8, device="cuda")
+            s.scan_device(xs, ys, o, of, lens[a:b].contiguous(), fl)
+            s.sync()
+            parts.append(fl.cpu().numpy())
+        assert (np.concatenate(parts) == f1).all()
+        # host path on the same rows
+        hf = s.scan_host(rows_of(x, y), outs.cpu().numpy(), offs.cpu().numpy().view(np.uint32),
+                         lens.cpu().numpy().view(np.uint32))
+        assert (hf == f1).all()
+    # label order does not change the flags
+    with Scanner(SCAN, SPEND, labels[::-1], max_rows=n) as s2:
+        flags.zero_()
+        s2.scan_device(x, y, outs, offs, lens, flags)
+        s2.sync()
+        assert (flags.cpu().numpy() == f1).all()

@@ -1,0 +1,187 @@
+"""CPU: the kernel math of duckdb-cudasp-extension_amd/csrc/*.hpp, compiled for
+the host with every field-magnitude precondition checked (tests/native), against
+Python integers, the golden fixtures and the C oracle.  This is how the HIP
+arithmetic is verified in the GPU-less build container; the GPU parity tests
+(-m gpu) then check the device build of the same code."""
+import ctypes
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import golden_io
+from oracle import oracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+P = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEFFFFFC2F
+N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+GX = 0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798
+GY = 0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8
+LAMBDA = 0x5363ad4cc05c30e0a5261c028812645a122e22ea20816678df02967c1b23bd72
+
+
+@pytest.fixture(scope="module")
+def emu():
+    path = os.path.join(HERE, "native", "libcudasp_emu.so")
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])
+    lib = ctypes.CDLL(path)
+    V = ctypes.c_void_p
+    lib.emu_row_values.argtypes = [V, V, V, ctypes.c_uint32, V, ctypes.c_uint32, V, V, V, V, V, V]
+    lib.emu_fb_entry.argtypes = [ctypes.c_uint32, ctypes.c_uint32, V]
+    lib.emu_wnaf.argtypes = [V, ctypes.c_int, V, ctypes.c_int]
+    return lib
+
+
+def _add(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    if a[0] == b[0]:
+        if (a[1] + b[1]) % P == 0:
+            return None
+        lam = 3 * a[0] * a[0] * pow(2 * a[1], -1, P) % P
+    else:
+        lam = (b[1] - a[1]) * pow(b[0] - a[0], -1, P) % P
+    x = (lam * lam - a[0] - b[0]) % P
+    return (x, (lam * (a[0] - x) - a[1]) % P)
+
+
+def _mul(k, p=(GX, GY)):
+    r = None
+    while k:
+        if k & 1:
+            r = _add(r, p)
+        p = _add(p, p)
+        k >>= 1
+    return r
+
+
+def _le(pt):
+    return pt[0].to_bytes(32, "little") + pt[1].to_bytes(32, "little")
+
+
+def test_field_ops(emu):
+    rng = random.Random(11)
+    out = ctypes.create_string_buffer(32)
+    edge = [0, 1, P - 1, P, P + 1, 2**256 - 1, 2**255, 2**32 + 977]
+    vals = edge + [rng.getrandbits(256) for _ in range(600)]
+    for a in vals:
+        b = rng.choice(vals)
+        emu.emu_fe_mul(a.to_bytes(32, "little"), b.to_bytes(32, "little"), out)
+        assert int.from_bytes(out.raw, "little") == a * b % P
+        emu.emu_fe_sqr(a.to_bytes(32, "little"), out)
+        assert int.from_bytes(out.raw, "little") == a * a % P
+        emu.emu_fe_normalize(a.to_bytes(32, "little"), out)
+        assert int.from_bytes(out.raw, "little") == a % P
+    for a in vals[:80]:
+        if a % P == 0:
+            continue
+        emu.emu_fe_inv(a.to_bytes(32, "little"), out)
+        assert int.from_bytes(out.raw, "little") == pow(a, -1, P)
+
+
+def test_glv_split(emu):
+    rng = random.Random(5)
+    k1b, k2b = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+    n1, n2 = ctypes.c_int(), ctypes.c_int()
+    for k in [1, 2, N - 1, N // 2, LAMBDA] + [rng.randrange(1, N) for _ in range(300)]:
+        emu.emu_glv_split(k.to_bytes(32, "little"), k1b, ctypes.byref(n1), k2b, ctypes.byref(n2))
+        k1 = int.from_bytes(k1b.raw, "little") * (-1 if n1.value else 1)
+        k2 = int.from_bytes(k2b.raw, "little") * (-1 if n2.value else 1)
+        assert (k1 + k2 * LAMBDA - k) % N == 0
+        assert abs(k1) < 2**129 and abs(k2) < 2**129
+
+
+def test_wnaf(emu):
+    rng = random.Random(9)
+    d = (ctypes.c_int8 * 300)()
+    for k in [0, 1, 15, 16, 31, 2**129 - 1] + [rng.getrandbits(130) for _ in range(200)]:
+        ln = emu.emu_wnaf(k.to_bytes(32, "little"), 5, d, 300)
+        digits = list(d)
+        assert sum(x << i for i, x in enumerate(digits)) == k
+        nz = [i for i, x in enumerate(digits) if x]
+        assert all(digits[i] % 2 and -16 < digits[i] < 16 for i in nz)
+        assert all(b - a >= 5 for a, b in zip(nz, nz[1:]))
+        assert ln == (nz[-1] + 1 if nz else 0)
+
+
+def test_fixed_base_entries(emu):
+    rng = random.Random(13)
+    out = (ctypes.c_uint32 * 16)()
+    for w, j in [(0, 0), (0, 32767), (15, 0), (15, 32767)] + [(rng.randrange(16), rng.randrange(32768)) for _ in range(6)]:
+        emu.emu_fb_entry(w, j, out)
+        x = sum(out[i] << (32 * i) for i in range(8))
+        y = sum(out[8 + i] << (32 * i) for i in range(8))
+        assert (x, y) == _mul((2 * j + 1) << (16 * w))
+
+
+def _values(emu, scan, spend, labels, tweaks, outs=None, offs=None, lens=None):
+    n = len(tweaks) // 64
+    L = len(labels)
+    vals = (ctypes.c_int64 * (n * (1 + L)))()
+    t = (ctypes.c_uint32 * (8 * n))()
+    flags = (ctypes.c_uint8 * n)()
+    p = lambda a: None if a is None else a.ctypes.data
+    rc = emu.emu_row_values(scan, spend, b"".join(labels) if labels else None, L, tweaks, n, vals, t,
+                            p(outs) if outs is not None and outs.size else None, p(offs), p(lens),
+                            flags if outs is not None else None)
+    assert rc == 0
+    v = np.frombuffer(vals, dtype=np.int64).reshape(n, 1 + L)
+    tt = np.frombuffer(t, dtype=np.uint32).reshape(n, 8)
+    return v, tt, np.frombuffer(flags, dtype=np.uint8)
+
+
+def test_stage_kats(emu):
+    for k in golden_io.load("stage_kats.json"):
+        labels = [bytes.fromhex(l) for l in k["label_keys"]]
+        v, t, _ = _values(emu, bytes.fromhex(k["scan_key"]), bytes.fromhex(k["spend_key"]), labels,
+                          bytes.fromhex(k["tweak"]))
+        assert sum(int(t[0, j]) << (32 * j) for j in range(8)) == int(k["t"], 16)
+        assert list(v[0]) == [k["v"]] + k["label_values"]
+
+
+def test_random_rows_and_flags(emu):
+    rr = golden_io.load("random_rows.json")
+    rows = rr["rows"]
+    tw = golden_io.tweak_array([r["tweak"] for r in rows])
+    outs, offs, lens = golden_io.csr([r["outputs"] for r in rows])
+    labels = [bytes.fromhex(l) for l in rr["label_keys"]]
+    v, t, f = _values(emu, bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), labels, tw.tobytes(),
+                      outs, offs, lens)
+    assert list(v[:, 0]) == [r["v"] for r in rows]
+    assert [list(x) for x in v[:, 1:]] == [r["label_values"] for r in rows]
+    assert [bool(x) for x in f] == [r["match_all_labels"] for r in rows]
+
+
+def test_against_oracle_random_keys(emu):
+    """Random scan keys (including ones whose GLV halves are negative) and 2 labels."""
+    rng = random.Random(21)
+    for _ in range(3):
+        scan = rng.randrange(1, N).to_bytes(32, "little")
+        spend = _le(_mul(rng.randrange(1, N)))
+        labels = [_le(_mul(rng.randrange(1, N))) for _ in range(2)]
+        tw = b"".join(_le(_mul(rng.randrange(1, N))) for _ in range(6))
+        v, _, _ = _values(emu, scan, spend, labels, tw)
+        _, ov = oracle.scan(scan, spend, labels, np.frombuffer(tw, dtype=np.uint8).reshape(-1, 64), want_values=True)
+        assert (v == ov).all()
+
+
+def test_exceptional_labels(emu):
+    """Label == F doubles, label == -F is infinity (reference Python oracle
+    semantics, scripts/compute_bip352_expected.py:42-46)."""
+    k = [k for k in golden_io.load("stage_kats.json") if k["height"] == 200][0]
+    F = (int(k["F_x"], 16), int(k["F_y"], 16))
+    labels = [_le(F), _le((F[0], (-F[1]) % P))]
+    v, _, _ = _values(emu, bytes.fromhex(k["scan_key"]), bytes.fromhex(k["spend_key"]), labels,
+                      bytes.fromhex(k["tweak"]))
+    two_f = _add(F, F)
+    up = lambda x: (x >> 192) - (1 << 64) if (x >> 192) >= 1 << 63 else (x >> 192)
+    assert v[0, 1] == up(two_f[0])
+    assert v[0, 2] == oracle.LABEL_INFINITY
+    _, ov = oracle.scan(bytes.fromhex(k["scan_key"]), bytes.fromhex(k["spend_key"]), labels,
+                        golden_io.tweak_array([k["tweak"]]), want_values=True)
+    assert list(ov[0]) == list(v[0])
