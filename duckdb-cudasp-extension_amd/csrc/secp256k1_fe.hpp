@@ -274,8 +274,10 @@ CUDASP_HD void fe_sqr_n(fe& r, const fe& a, int n) {
 }
 
 // a^(p-2) via the addition chain 223 ones | 0 | 22 ones | 0000 1 0 11 0 1
+// (kept as a cross-check for tests; the kernels use fe_inv = safegcd,
+// secp256k1_inv.hpp)
 // (p-2 = 0xFF..FE FFFFFC2D): 255 squarings + 15 multiplications.
-CUDASP_HD void fe_inv(fe& r, const fe& a) {
+CUDASP_HD void fe_inv_fermat(fe& r, const fe& a) {
   fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
   fe_sqr(x2, a);
   fe_mul(x2, x2, a);

@@ -11,6 +11,11 @@
 // explicitly (scan_kernels.hip, label_batch).
 #pragma once
 #include "secp256k1_fe.hpp"
+#include "secp256k1_inv.hpp"
+
+namespace cudasp {
+CUDASP_HD void fe_inv(fe& r, const fe& a) { fe_inv_safegcd(r, a); }
+}  // namespace cudasp
 
 namespace cudasp {
 

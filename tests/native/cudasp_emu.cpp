@@ -120,6 +120,14 @@ int emu_fe_inv(const uint8_t a[32], uint8_t out[32]) {
   return 0;
 }
 
+int emu_fe_inv_fermat(const uint8_t a[32], uint8_t out[32]) {
+  fe x, r;
+  fe_from_bytes(x, a);
+  fe_inv_fermat(r, x);
+  fe_to_bytes(out, r);
+  return 0;
+}
+
 int emu_fe_normalize(const uint8_t a[32], uint8_t out[32]) {
   fe x;
   fe_from_bytes(x, a);

@@ -77,10 +77,16 @@ def test_field_ops(emu):
         assert int.from_bytes(out.raw, "little") == a * a % P
         emu.emu_fe_normalize(a.to_bytes(32, "little"), out)
         assert int.from_bytes(out.raw, "little") == a % P
-    for a in vals[:80]:
+    inv_vals = vals[:40] + [P - 2, 2, 3, 2**255, 2**256 - 2**32 - 978, P + 5] + [rng.randrange(1, P) for _ in range(3000)]
+    for a in inv_vals:
         if a % P == 0:
             continue
-        emu.emu_fe_inv(a.to_bytes(32, "little"), out)
+        emu.emu_fe_inv(a.to_bytes(32, "little"), out)  # safegcd (the kernels' inversion)
+        assert int.from_bytes(out.raw, "little") == pow(a, -1, P), hex(a)
+    for a in inv_vals[:60]:
+        if a % P == 0:
+            continue
+        emu.emu_fe_inv_fermat(a.to_bytes(32, "little"), out)
         assert int.from_bytes(out.raw, "little") == pow(a, -1, P)
 
 
