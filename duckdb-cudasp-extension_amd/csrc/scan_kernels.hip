@@ -51,13 +51,21 @@ int set_error(int code, const char* fmt, ...) {
   } while (0)
 
 constexpr int BLOCK = 256;
+// Minimum waves per SIMD requested for the two hot kernels (register budget:
+// 2 -> 256 VGPRs, 3 -> 168, 4 -> 128).  Tuned on MI355X; see DESIGN.md.
+#ifndef CUDASP_WAVES_A
+#define CUDASP_WAVES_A 2
+#endif
+#ifndef CUDASP_WAVES_B
+#define CUDASP_WAVES_B 2
+#endif
 // Grid cap for the grid-stride kernels; also bounds the per-slot scratch.
 constexpr uint32_t MAX_BLOCKS = 4096;
 }  // namespace
 
 // ----------------------------------------------------------------- kernels
 
-__global__ __launch_bounds__(BLOCK) void k_shared_secret(const uint32_t* __restrict__ tx,
+__global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const uint32_t* __restrict__ tx,
                                                          const uint32_t* __restrict__ ty, uint32_t n,
                                                          const int8_t* __restrict__ naf, ScanConsts k,
                                                          uint32_t* __restrict__ vscr,
@@ -79,7 +87,7 @@ __global__ __launch_bounds__(BLOCK) void k_shared_secret(const uint32_t* __restr
 }
 
 template <bool VALUES>
-__global__ __launch_bounds__(BLOCK) void k_match(const uint32_t* __restrict__ t_in, uint32_t n,
+__global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t* __restrict__ t_in, uint32_t n,
                                                  const uint32_t* __restrict__ fb, ScanConsts k,
                                                  const uint32_t* __restrict__ labels,
                                                  const int64_t* __restrict__ outputs,

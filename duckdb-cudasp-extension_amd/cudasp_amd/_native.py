@@ -57,7 +57,7 @@ def load(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("CUDASP_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise CudaspError(CUDASP_ERR_NO_DEVICE,
                           "HIP library %s not built (run `make -C duckdb-cudasp-extension_amd` "
