@@ -12,11 +12,18 @@
 //     (src/cudasp_gpu.cu:705-761);
 //   * each thread keeps one scanner (keys bound once, device buffers reused)
 //     instead of allocating and freeing per batch (src/cudasp_gpu.cu:487-666);
+//   * rows are accumulated straight into pinned host buffers and batches run
+//     asynchronously, double-buffered: while the GPU scans batch b (H2D,
+//     transpose, both kernels, D2H of the flags, all on the thread's stream),
+//     the DuckDB thread accumulates batch b+1; the reference blocks the thread
+//     for the whole GPU round trip (README.md:140 "serial table scan overhead");
 //   * a failed batch is reported (cudasp_tf_function/final return an error)
 //     instead of being dropped silently (:325, :378);
 //   * a tweak_key BLOB that is not 64 bytes is an error instead of an
 //     out-of-bounds read (:333, ConvertTweakKeyToU32 always reads 64 bytes).
 #include "../../../include/cudasp_host.h"
+
+#include <hip/hip_runtime.h>
 
 #include <atomic>
 #include <cstdarg>
@@ -66,32 +73,46 @@ struct cudasp_tf_global {
   std::atomic<int> next_gpu_assignment{0};
 };
 
-struct cudasp_tf_local {
-  bool finalized = false;
-  bool is_output_thread = false;
-  int assigned_gpu = -1;
-  // accumulated rows, flat
+// One accumulation/launch buffer set of a thread (double-buffered).
+struct HostSlot {
+  // row data for the kernels, pinned for asynchronous H2D
+  uint8_t* h_tweaks = nullptr;  // cap_rows x 64
+  uint32_t* h_offs = nullptr;
+  uint32_t* h_lens = nullptr;
+  uint8_t* h_flags = nullptr;
+  int64_t* h_outputs = nullptr;
+  size_t outputs_cap = 0;
+  size_t n_outputs = 0;
+  // row data for the emit (pageable)
   std::vector<uint8_t> txid_bytes;
   std::vector<uint64_t> txid_offset;
   std::vector<uint32_t> txid_size;
   std::vector<int32_t> heights;
-  std::vector<uint8_t> tweaks;  // n x 64
-  std::vector<int64_t> outputs;
-  std::vector<uint32_t> output_offset;
-  std::vector<uint32_t> output_length;
-  std::vector<uint8_t> flags;
+  uint32_t rows = 0;
+  // device side
+  uint8_t* d_rows = nullptr;
+  uint32_t* d_tx = nullptr;
+  uint32_t* d_ty = nullptr;
+  uint32_t* d_offs = nullptr;
+  uint32_t* d_lens = nullptr;
+  uint8_t* d_flags = nullptr;
+  int64_t* d_outputs = nullptr;
+  size_t d_outputs_cap = 0;
+  hipEvent_t done = nullptr;
+  bool in_flight = false;
+  uint32_t launched_rows = 0;
+};
+
+struct cudasp_tf_local {
+  bool finalized = false;
+  bool is_output_thread = false;
+  int assigned_gpu = -1;
+  uint32_t cap_rows = 0;
+  HostSlot slots[2];
+  int cur = 0;
   cudasp_scanner* scanner = nullptr;
-  uint32_t rows() const { return (uint32_t)heights.size(); }
-  void clear() {
-    txid_bytes.clear();
-    txid_offset.clear();
-    txid_size.clear();
-    heights.clear();
-    tweaks.clear();
-    outputs.clear();
-    output_offset.clear();
-    output_length.clear();
-  }
+  hipStream_t stream = nullptr;
+  uint32_t rows() const { return slots[cur].rows; }
 };
 
 namespace {
@@ -109,65 +130,185 @@ int host_fail(int code, const char* fmt, ...) {
 
 inline bool valid(const uint8_t* v, uint32_t i) { return v == nullptr || v[i] != 0; }
 
-// AccumulateInput (src/cudasp_extension.cu:154-224).
-int accumulate(cudasp_tf_local& l, const cudasp_tf_chunk& c) {
+#define HOST_HIP(expr)                                                                          \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) return host_fail(CUDASP_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceSet {
+  int prev = -1;
+  explicit DeviceSet(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceSet() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int ensure_outputs_cap(HostSlot& s, size_t need) {
+  if (need <= s.outputs_cap) return CUDASP_OK;
+  size_t cap = s.outputs_cap ? s.outputs_cap : 4096;
+  while (cap < need) cap *= 2;
+  int64_t* p = nullptr;
+  HOST_HIP(hipHostMalloc((void**)&p, cap * sizeof(int64_t), hipHostMallocDefault));
+  if (s.n_outputs) memcpy(p, s.h_outputs, s.n_outputs * sizeof(int64_t));
+  if (s.h_outputs) (void)hipHostFree(s.h_outputs);
+  s.h_outputs = p;
+  s.outputs_cap = cap;
+  return CUDASP_OK;
+}
+
+// Per-thread GPU state, created on the first row: scanner, stream, pinned and
+// device buffers for both slots (cap_rows = batch_size - 1 + one chunk).
+int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
+  if (l.scanner) return CUDASP_OK;
+  DeviceSet dg(l.assigned_gpu);
+  l.cap_rows = (uint32_t)(b.batch_size + CUDASP_TF_VECTOR_SIZE);
+  int rc = cudasp_scanner_create(l.assigned_gpu, (const uint8_t*)b.scan_private_key_data.data(),
+                                 (const uint8_t*)b.spend_public_key_data.data(),
+                                 (const uint8_t*)b.label_keys_flat.data(), (uint32_t)b.label_keys_data.size(),
+                                 l.cap_rows, &l.scanner);
+  if (rc != CUDASP_OK)
+    return host_fail(rc, "Failed to create scanner on GPU %d: %s", l.assigned_gpu, cudasp_last_error());
+  HOST_HIP(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
+  for (HostSlot& s : l.slots) {
+    size_t n = l.cap_rows;
+    HOST_HIP(hipHostMalloc((void**)&s.h_tweaks, n * 64, hipHostMallocDefault));
+    HOST_HIP(hipHostMalloc((void**)&s.h_offs, n * 4, hipHostMallocDefault));
+    HOST_HIP(hipHostMalloc((void**)&s.h_lens, n * 4, hipHostMallocDefault));
+    HOST_HIP(hipHostMalloc((void**)&s.h_flags, n, hipHostMallocDefault));
+    HOST_HIP(hipMalloc((void**)&s.d_rows, n * 64));
+    HOST_HIP(hipMalloc((void**)&s.d_tx, n * 32));
+    HOST_HIP(hipMalloc((void**)&s.d_ty, n * 32));
+    HOST_HIP(hipMalloc((void**)&s.d_offs, n * 4));
+    HOST_HIP(hipMalloc((void**)&s.d_lens, n * 4));
+    HOST_HIP(hipMalloc((void**)&s.d_flags, n));
+    HOST_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    rc = ensure_outputs_cap(s, (size_t)n * 2);
+    if (rc != CUDASP_OK) return rc;
+  }
+  return CUDASP_OK;
+}
+
+void free_local_gpu(cudasp_tf_local& l) {
+  if (!l.scanner && !l.stream) return;
+  DeviceSet dg(l.assigned_gpu);
+  if (l.stream) (void)hipStreamSynchronize(l.stream);
+  for (HostSlot& s : l.slots) {
+    void* host[] = {s.h_tweaks, s.h_offs, s.h_lens, s.h_flags, s.h_outputs};
+    for (void* p : host)
+      if (p) (void)hipHostFree(p);
+    void* dev[] = {s.d_rows, s.d_tx, s.d_ty, s.d_offs, s.d_lens, s.d_flags, s.d_outputs};
+    for (void* p : dev)
+      if (p) (void)hipFree(p);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
+  if (l.stream) (void)hipStreamDestroy(l.stream);
+  if (l.scanner) cudasp_scanner_destroy(l.scanner);
+  l.scanner = nullptr;
+  l.stream = nullptr;
+}
+
+// AccumulateInput (src/cudasp_extension.cu:154-224), into the current slot.
+int accumulate(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const cudasp_tf_chunk& c) {
+  int rc = ensure_local_gpu(b, l);
+  if (rc != CUDASP_OK) return rc;
+  HostSlot& s = l.slots[l.cur];
   for (uint32_t i = 0; i < c.count; i++) {
     // Only rows with valid txid, height and tweak_key (:195-197).
     if (!(valid(c.txid_valid, i) && valid(c.height_valid, i) && valid(c.tweak_valid, i))) continue;
     if (c.tweak_size[i] != TWEAK_KEY_SIZE)
       return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", c.tweak_size[i]);
-    l.txid_offset.push_back(l.txid_bytes.size());
-    l.txid_size.push_back(c.txid_size[i]);
-    l.txid_bytes.insert(l.txid_bytes.end(), c.txid_data[i], c.txid_data[i] + c.txid_size[i]);
-    l.heights.push_back(c.height[i]);
-    l.tweaks.insert(l.tweaks.end(), c.tweak_data[i], c.tweak_data[i] + TWEAK_KEY_SIZE);
+    uint32_t r = s.rows;
+    s.txid_offset.push_back(s.txid_bytes.size());
+    s.txid_size.push_back(c.txid_size[i]);
+    s.txid_bytes.insert(s.txid_bytes.end(), c.txid_data[i], c.txid_data[i] + c.txid_size[i]);
+    s.heights.push_back(c.height[i]);
+    memcpy(s.h_tweaks + (size_t)r * TWEAK_KEY_SIZE, c.tweak_data[i], TWEAK_KEY_SIZE);
     // Outputs: NULL list -> length 0; NULL elements dropped (:206-221).
-    l.output_offset.push_back((uint32_t)l.outputs.size());
+    s.h_offs[r] = (uint32_t)s.n_outputs;
     uint32_t len = 0;
     if (valid(c.list_valid, i)) {
+      rc = ensure_outputs_cap(s, s.n_outputs + c.list_length[i]);
+      if (rc != CUDASP_OK) return rc;
       for (uint64_t k = 0; k < c.list_length[i]; k++) {
         uint64_t ci = c.list_offset[i] + k;
         if (valid(c.child_valid, (uint32_t)ci)) {
-          l.outputs.push_back(c.child_values[ci]);
+          s.h_outputs[s.n_outputs++] = c.child_values[ci];
           len++;
         }
       }
     }
-    l.output_length.push_back(len);
+    s.h_lens[r] = len;
+    s.rows = r + 1;
   }
   return CUDASP_OK;
 }
 
-// ProcessBatch (src/cudasp_extension.cu:226-410).
-int process_batch(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l) {
-  uint32_t n = l.rows();
-  if (n == 0) return CUDASP_OK;
-  if (!l.scanner) {
-    // One scanner per thread on its assigned GPU; capacity covers the largest
-    // batch the >= trigger can produce (batch_size - 1 + one 2048-row chunk).
-    uint64_t cap = b.batch_size + CUDASP_TF_VECTOR_SIZE;
-    int rc = cudasp_scanner_create(l.assigned_gpu, (const uint8_t*)b.scan_private_key_data.data(),
-                                   (const uint8_t*)b.spend_public_key_data.data(),
-                                   (const uint8_t*)b.label_keys_flat.data(), (uint32_t)b.label_keys_data.size(),
-                                   (uint32_t)cap, &l.scanner);
-    if (rc != CUDASP_OK)
-      return host_fail(rc, "Failed to create scanner on GPU %d: %s", l.assigned_gpu, cudasp_last_error());
+// Collect a finished batch's matches into the global list (ProcessBatch
+// :378-392) and reset the slot.
+int harvest(cudasp_tf_global& g, cudasp_tf_local& l, HostSlot& s) {
+  if (!s.in_flight) return CUDASP_OK;
+  {
+    DeviceSet dg(l.assigned_gpu);
+    HOST_HIP(hipEventSynchronize(s.done));
   }
-  l.flags.resize(n);
-  int rc = cudasp_scan_host(l.scanner, l.tweaks.data(), l.outputs.data(), l.outputs.size(), l.output_offset.data(),
-                            l.output_length.data(), n, l.flags.data());
-  if (rc != CUDASP_OK) return host_fail(rc, "cudasp_scan batch of %u rows failed: %s", n, cudasp_last_error());
+  s.in_flight = false;
+  uint32_t n = s.launched_rows;
   {
     std::lock_guard<std::mutex> lock(g.output_lock);
     for (uint32_t i = 0; i < n; i++) {
-      if (!l.flags[i]) continue;
-      g.output_txids.emplace_back((const char*)l.txid_bytes.data() + l.txid_offset[i], l.txid_size[i]);
-      g.output_heights.push_back(l.heights[i]);
-      g.output_tweak_keys.emplace_back((const char*)l.tweaks.data() + (size_t)i * TWEAK_KEY_SIZE, TWEAK_KEY_SIZE);
+      if (!s.h_flags[i]) continue;
+      g.output_txids.emplace_back((const char*)s.txid_bytes.data() + s.txid_offset[i], s.txid_size[i]);
+      g.output_heights.push_back(s.heights[i]);
+      g.output_tweak_keys.emplace_back((const char*)s.h_tweaks + (size_t)i * TWEAK_KEY_SIZE, TWEAK_KEY_SIZE);
     }
   }
-  l.clear();
+  s.txid_bytes.clear();
+  s.txid_offset.clear();
+  s.txid_size.clear();
+  s.heights.clear();
+  s.rows = 0;
+  s.n_outputs = 0;
   return CUDASP_OK;
+}
+
+// ProcessBatch (src/cudasp_extension.cu:226-410), asynchronous: enqueue the
+// current slot on the thread's stream and switch to the other slot, first
+// harvesting it if its previous batch is still outstanding.
+int launch_batch(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l) {
+  (void)b;
+  HostSlot& s = l.slots[l.cur];
+  uint32_t n = s.rows;
+  if (n > 0) {
+    DeviceSet dg(l.assigned_gpu);
+    hipStream_t st = l.stream;
+    if (s.n_outputs > s.d_outputs_cap) {
+      if (s.d_outputs) HOST_HIP(hipFree(s.d_outputs));
+      s.d_outputs = nullptr;
+      size_t cap = s.outputs_cap;
+      HOST_HIP(hipMalloc((void**)&s.d_outputs, cap * sizeof(int64_t)));
+      s.d_outputs_cap = cap;
+    }
+    HOST_HIP(hipMemcpyAsync(s.d_rows, s.h_tweaks, (size_t)n * 64, hipMemcpyHostToDevice, st));
+    HOST_HIP(hipMemcpyAsync(s.d_offs, s.h_offs, (size_t)n * 4, hipMemcpyHostToDevice, st));
+    HOST_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, st));
+    if (s.n_outputs)
+      HOST_HIP(hipMemcpyAsync(s.d_outputs, s.h_outputs, s.n_outputs * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    int rc = cudasp_tweaks_to_columns(s.d_rows, n, s.d_tx, s.d_ty, st);
+    if (rc == CUDASP_OK)
+      rc = cudasp_scan_device(l.scanner, s.d_tx, s.d_ty, s.d_outputs, s.d_offs, s.d_lens, n, s.d_flags, nullptr,
+                              nullptr, st);
+    if (rc != CUDASP_OK) return host_fail(rc, "cudasp_scan batch of %u rows failed: %s", n, cudasp_last_error());
+    HOST_HIP(hipMemcpyAsync(s.h_flags, s.d_flags, n, hipMemcpyDeviceToHost, st));
+    HOST_HIP(hipEventRecord(s.done, st));
+    s.in_flight = true;
+    s.launched_rows = n;
+  }
+  l.cur ^= 1;
+  return harvest(g, l, l.slots[l.cur]);
 }
 
 }  // namespace
@@ -275,7 +416,7 @@ int cudasp_tf_local_init(cudasp_tf_global* g, cudasp_tf_local** out) {
 
 void cudasp_tf_local_free(cudasp_tf_local* l) {
   if (!l) return;
-  if (l->scanner) cudasp_scanner_destroy(l->scanner);
+  free_local_gpu(*l);
   delete l;
 }
 
@@ -285,11 +426,11 @@ int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp
                        const cudasp_tf_chunk* chunk) {
   if (!b || !g || !l || !chunk) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
   if (chunk->count > 0) {
-    int rc = accumulate(*l, *chunk);
+    int rc = accumulate(*b, *l, *chunk);
     if (rc != CUDASP_OK) return rc;
     // ShouldProcessBatch: accumulated >= batch_size (:416-418).
     if (l->rows() >= b->batch_size) {
-      rc = process_batch(*b, *g, *l);
+      rc = launch_batch(*b, *g, *l);
       if (rc != CUDASP_OK) return rc;
     }
   }
@@ -299,8 +440,12 @@ int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp
 int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l, cudasp_tf_output* out) {
   if (!b || !g || !l || !out) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
   out->count = 0;
-  if (!l->finalized && l->rows() > 0) {
-    int rc = process_batch(*b, *g, *l);
+  if (!l->finalized) {
+    // Flush this thread's last rows and wait for both slots.
+    int rc = CUDASP_OK;
+    if (l->rows() > 0) rc = launch_batch(*b, *g, *l);
+    for (HostSlot& s : l->slots)
+      if (rc == CUDASP_OK) rc = harvest(*g, *l, s);
     if (rc != CUDASP_OK) return rc;
   }
   if (!l->finalized) {
