@@ -181,6 +181,31 @@ CUDASP_HD bool fe_equal_norm(const fe& a, const fe& b) {
   return z == 0;
 }
 
+// Small constants as opaque scalar registers on the device, so that the
+// compiler keeps "x * 0x400" as one v_mad_u64_u32 instead of rewriting it as a
+// 64-bit shift + add (two VOP3 instructions).
+CUDASP_HD uint32_t opaque_const(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("s_mov_b32 %0, %1" : "=s"(r) : "i"(v));
+  return r;
+#else
+  return v;
+#endif
+}
+
+// Field multiply/square code shapes (A/B-tested on MI355X, stage A of 300k rows,
+// tools/stage_timing.py):
+//   0  19 parallel column sums + 26-bit carry chain over the high half, fold,
+//      carry chain over the low half                              3.00 ms
+//   1  like 0, but each high column folds through its two 32-bit halves
+//      (no high-half carry chain)                                 2.85 ms  <- default
+//   2  explicit serial mad chains in inline asm: fewest VALU (184/148 per
+//      mul/sqr) but the compiler pads every asm result with s_nop  2.94 ms
+#ifndef CUDASP_FE_VARIANT
+#define CUDASP_FE_VARIANT 1
+#endif
+#if CUDASP_FE_VARIANT == 0
 // Reduction shared by mul and sqr.  c[0..18] are the product columns
 // (each < 2^62).  Folding uses 2^260 = R0 + R1*2^26 (mod p) for the high part
 // and 2^256 = F0 + F1*2^26 for the final top bits.
@@ -267,6 +292,204 @@ CUDASP_HD void fe_sqr(fe& r, const fe& a) {
   }
   fe_reduce_columns(r, c);
 }
+
+#elif CUDASP_FE_VARIANT == 1
+CUDASP_HD void fe_reduce_columns(fe& r, const uint64_t c[19]) {
+  const uint32_t r0 = opaque_const(R0), r1 = opaque_const(R1);
+  const uint32_t r0s = opaque_const(R0 << 6), r1s = opaque_const(R1 << 6);
+  uint64_t t[11];
+#pragma unroll
+  for (int k = 0; k < 10; k++) t[k] = c[k];
+  t[10] = 0;
+#pragma unroll
+  for (int m = 0; m < 9; m++) {
+    uint32_t lo = (uint32_t)c[10 + m], hi = (uint32_t)(c[10 + m] >> 32);
+    t[m] += (uint64_t)lo * r0;
+    t[m + 1] += (uint64_t)lo * r1 + (uint64_t)hi * r0s;
+    t[m + 2] += (uint64_t)hi * r1s;
+  }
+  {
+    uint32_t lo = (uint32_t)t[10], hi = (uint32_t)(t[10] >> 32);
+    t[0] += (uint64_t)lo * r0;
+    t[1] += (uint64_t)lo * r1 + (uint64_t)hi * r0s;
+    t[2] += (uint64_t)hi * r1s;
+  }
+  uint32_t o[10];
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    o[k] = (uint32_t)t[k] & M26;
+    t[k + 1] += t[k] >> 26;
+  }
+  o[9] = (uint32_t)t[9] & M22;
+  uint64_t u = t[9] >> 22;
+  uint32_t ulo = (uint32_t)u, uhi = (uint32_t)(u >> 32);
+  const uint32_t f0 = opaque_const(F0), f1 = opaque_const(F1);
+  const uint32_t f0s = opaque_const(F0 << 6), f1s = opaque_const(F1 << 6);
+  uint64_t s0 = (uint64_t)o[0] + (uint64_t)ulo * f0;
+  uint64_t s1 = (uint64_t)o[1] + (uint64_t)ulo * f1 + (uint64_t)uhi * f0s + (s0 >> 26);
+  uint64_t s2 = (uint64_t)o[2] + (uint64_t)uhi * f1s + (s1 >> 26);
+  r.n[0] = (uint32_t)s0 & M26;
+  r.n[1] = (uint32_t)s1 & M26;
+  r.n[2] = (uint32_t)s2;
+#pragma unroll
+  for (int k = 3; k < 10; k++) r.n[k] = o[k];
+}
+
+CUDASP_HD void fe_mul(fe& r, const fe& a, const fe& b) {
+  FE_CHECK(a, 8, "mul a");
+  FE_CHECK(b, 8, "mul b");
+  uint64_t c[19];
+#pragma unroll
+  for (int k = 0; k < 19; k++) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      int j = k - i;
+      if (j >= 0 && j < 10) s += (uint64_t)a.n[i] * b.n[j];
+    }
+    c[k] = s;
+  }
+  fe_reduce_columns(r, c);
+}
+
+CUDASP_HD void fe_sqr(fe& r, const fe& a) {
+  FE_CHECK(a, 8, "sqr");
+  uint32_t a2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) a2[i] = a.n[i] * 2;
+  uint64_t c[19];
+#pragma unroll
+  for (int k = 0; k < 19; k++) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      int j = k - i;
+      if (j > i && j < 10) s += (uint64_t)a2[i] * a.n[j];
+      else if (j == i) s += (uint64_t)a.n[i] * a.n[i];
+    }
+    c[k] = s;
+  }
+  fe_reduce_columns(r, c);
+}
+
+#else
+// acc + a*b as one v_mad_u64_u32 (accumulator tied in place).  Written as asm
+// so the compiler keeps the carry-free accumulation chains exactly as laid out
+// below instead of re-associating them into parallel partial sums that it then
+// has to add with extra 64-bit adds and register-pair moves.
+CUDASP_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t acc) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t r, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "v"(b), "0"(acc));
+  (void)cc;
+  return r;
+#else
+  return (uint64_t)a * b + acc;
+#endif
+}
+
+// Same with b in a scalar register (the fold constants).
+CUDASP_HD uint64_t mad64s(uint32_t a, uint32_t b_uniform, uint64_t acc) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t r, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "s"(b_uniform), "0"(acc));
+  (void)cc;
+  return r;
+#else
+  return (uint64_t)a * b_uniform + acc;
+#endif
+}
+
+// Product columns: column k = sum_{i+j=k} a_i b_j, each a single mad chain.
+// High columns 10..18 are independent chains; the low columns form one carry
+// chain (below) that starts each column from the previous column's carry.
+//
+// Reduction: a high column c_{10+m} (weight 2^(260 + 26m)) is folded through
+// its two 32-bit halves, which cost nothing to extract:
+//   lo * 2^(260+26m) = lo*R0 @m + lo*R1 @m+1              (2^260 = R0 + R1 2^26)
+//   hi * 2^(292+26m) = hi*(R0<<6) @m+1 + hi*(R1<<6) @m+2
+// then the low column k is accumulated on top of the carry of column k-1,
+// split at 26 bits, and the bits above 2^256 fold with 2^256 = F0 + F1 2^26.
+// Bounds (inputs of magnitude <= 8): columns < 2^61.4, folded terms < 2^51.
+template <bool SQR>
+CUDASP_HD void fe_mul_impl(fe& r, const fe& a, const fe& b) {
+  uint32_t a2[10];
+  if (SQR) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) a2[i] = a.n[i] << 1;
+  }
+  // column term generator
+  auto column = [&](int k, uint64_t acc) -> uint64_t {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      int j = k - i;
+      if (j < 0 || j >= 10) continue;
+      if (SQR) {
+        if (j > i) acc = mad64(a2[i], a.n[j], acc);
+        else if (j == i) acc = mad64(a.n[i], a.n[i], acc);
+      } else {
+        acc = mad64(a.n[i], b.n[j], acc);
+      }
+    }
+    return acc;
+  };
+  uint64_t h[9];
+#pragma unroll
+  for (int m = 0; m < 9; m++) h[m] = column(10 + m, 0);
+  const uint32_t r0 = opaque_const(R0), r1 = opaque_const(R1);
+  const uint32_t r0s = opaque_const(R0 << 6), r1s = opaque_const(R1 << 6);
+  // second-order overflow: column 18's hi*(R1<<6) lands at weight 2^260 again.
+  uint64_t top = mad64s((uint32_t)(h[8] >> 32), r1s, 0);  // weight 2^260, < 2^47
+  uint32_t top_lo = (uint32_t)top, top_hi = (uint32_t)(top >> 32);
+  uint32_t o[10];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    if (k < 9) acc = mad64s((uint32_t)h[k], r0, acc);
+    if (k >= 1 && k - 1 < 9) {
+      acc = mad64s((uint32_t)h[k - 1], r1, acc);
+      acc = mad64s((uint32_t)(h[k - 1] >> 32), r0s, acc);
+    }
+    if (k >= 2 && k - 2 < 8) acc = mad64s((uint32_t)(h[k - 2] >> 32), r1s, acc);
+    if (k == 0) acc = mad64s(top_lo, r0, acc);
+    if (k == 1) {
+      acc = mad64s(top_lo, r1, acc);
+      acc = mad64s(top_hi, r0s, acc);
+    }
+    if (k == 2) acc = mad64s(top_hi, r1s, acc);
+    acc = column(k, acc);
+    if (k < 9) {
+      o[k] = (uint32_t)acc & M26;
+      acc >>= 26;
+    }
+  }
+  o[9] = (uint32_t)acc & M22;
+  uint64_t u = acc >> 22;  // bits >= 2^256, < 2^41
+  uint32_t ulo = (uint32_t)u, uhi = (uint32_t)(u >> 32);
+  const uint32_t f0 = opaque_const(F0), f1 = opaque_const(F1);
+  const uint32_t f0s = opaque_const(F0 << 6), f1s = opaque_const(F1 << 6);
+  uint64_t s0 = mad64s(ulo, f0, o[0]);
+  uint64_t s1 = mad64s(uhi, f0s, mad64s(ulo, f1, (uint64_t)o[1] + (s0 >> 26)));
+  uint64_t s2 = mad64s(uhi, f1s, (uint64_t)o[2] + (s1 >> 26));
+  r.n[0] = (uint32_t)s0 & M26;
+  r.n[1] = (uint32_t)s1 & M26;
+  r.n[2] = (uint32_t)s2;  // < 2^26 + 2^21
+#pragma unroll
+  for (int k = 3; k < 10; k++) r.n[k] = o[k];
+}
+
+CUDASP_HD void fe_mul(fe& r, const fe& a, const fe& b) {
+  FE_CHECK(a, 8, "mul a");
+  FE_CHECK(b, 8, "mul b");
+  fe_mul_impl<false>(r, a, b);
+}
+
+CUDASP_HD void fe_sqr(fe& r, const fe& a) {
+  FE_CHECK(a, 8, "sqr");
+  fe_mul_impl<true>(r, a, a);
+}
+
+#endif
 
 CUDASP_HD void fe_sqr_n(fe& r, const fe& a, int n) {
   fe_sqr(r, a);
