@@ -66,7 +66,14 @@ def bytes_per_row(k):
 
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, spec
-VALU_MAD_PEAK = 37.1e12    # measured v_mad_u64_u32 lane-ops/s (profiles/r01_microbench_int.txt)
+# VALU issue peaks (wave-instructions/s per GPU):
+#   nominal: 4 SIMD32 per CU, a wave64 VALU op every 2 cycles -> 2 per CU-cycle,
+#            x 256 CUs x 2.4 GHz;
+#   measured for VOP3 ops (v_mad_u64_u32, v_add3, v_lshl_add_u64: 37.1e12
+#            lane-ops/s, profiles/r01_microbench_int.txt) -- half the nominal
+#            rate; the scan kernels are ~80% VOP3.
+VALU_WAVE_INSTR_PEAK = 2 * 256 * 2.4e9
+VOP3_WAVE_INSTR_MEASURED = 37.1e12 / 64
 
 
 def _ec_add(p, q):
@@ -116,14 +123,16 @@ def synth_s0():
 class Table:
     """One rank's resident synthetic table, batch-major."""
 
-    def __init__(self, lib, device, rows, batch, k, labels, first_global, dev_stream):
-        self.rows, self.batch, self.k = rows, batch, k
+    def __init__(self, lib, device, rows, batch, k, labels, first_global, dev_stream, kmax=0):
+        """k: fixed outputs per row; kmax > 0: variable lengths uniform in [1, kmax]."""
+        self.rows, self.batch, self.k, self.kmax = rows, batch, k, kmax
+        cap = kmax if kmax else k
         self.nb = (rows + batch - 1) // batch
         self.sizes = [min(batch, rows - b * batch) for b in range(self.nb)]
         dev = torch.device("cuda", device)
         self.tx = torch.empty((self.nb, 8, batch), dtype=torch.int32, device=dev)
         self.ty = torch.empty((self.nb, 8, batch), dtype=torch.int32, device=dev)
-        self.outs = torch.empty((self.nb, batch * k), dtype=torch.int64, device=dev)
+        self.outs = torch.empty((self.nb, batch * cap), dtype=torch.int64, device=dev)
         self.offs = torch.empty((self.nb, batch), dtype=torch.int32, device=dev)
         self.lens = torch.empty((self.nb, batch), dtype=torch.int32, device=dev)
         self.flags = torch.zeros((self.nb, batch), dtype=torch.uint8, device=dev)
@@ -136,12 +145,21 @@ class Table:
             g0 = first_global + b * batch
             _native.check(lib.cudasp_synth_tweak_columns(device, s0, g0, m, self.tx[b].data_ptr(),
                                                          self.ty[b].data_ptr(), st))
-            _native.check(lib.cudasp_synth_outputs(OUTPUT_SEED, g0, m, k, self.outs[b].data_ptr(),
-                                                   self.offs[b].data_ptr(), self.lens[b].data_ptr(), st))
+            if kmax:
+                _native.check(lib.cudasp_synth_output_lengths(OUTPUT_SEED, g0, m, kmax, self.lens[b].data_ptr(), st))
+                with torch.cuda.stream(dev_stream):
+                    ln = self.lens[b][:m].to(torch.int64)
+                    self.offs[b][:m] = (torch.cumsum(ln, 0) - ln).to(torch.int32)
+                _native.check(lib.cudasp_synth_output_values(OUTPUT_SEED, g0, m, self.offs[b].data_ptr(),
+                                                             self.lens[b].data_ptr(), self.outs[b].data_ptr(), st))
+            else:
+                _native.check(lib.cudasp_synth_outputs(OUTPUT_SEED, g0, m, k, self.outs[b].data_ptr(),
+                                                       self.offs[b].data_ptr(), self.lens[b].data_ptr(), st))
         torch.cuda.synchronize(dev)
         # Plant true values (computed by the product's own stage outputs; the
         # test suite checks those against the oracle): base value every 1000th
         # global row, label-0 value on the row after it when labels exist.
+        self.total_outputs = int(self.lens.sum().item()) if kmax else rows * k
         self.expected = 0
         per_batch = 2 * ((batch + PLANT_EVERY - 1) // PLANT_EVERY) + 2
         planter = Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=per_batch, device=device)
@@ -161,7 +179,7 @@ class Table:
             planter.row_values_device(gx, gy, t, vals)
             planter.sync()
             nbase = len(base_idx)
-            pos = it * k  # slot 0 of each planted row's outputs list
+            pos = self.offs[b][:m].index_select(0, it).to(torch.int64)  # slot 0 of each planted list
             self.outs[b].index_copy_(0, pos[:nbase], vals[0, :nbase])
             if lab_idx:
                 self.outs[b].index_copy_(0, pos[nbase:], vals[1, nbase:])
@@ -180,25 +198,48 @@ def _cols(self, arr, b):
 Table.cols = _cols
 
 
+def aggregate(world, backend, total_s, found, flagged, expected):
+    """Cross-rank reduction of one run: the job time is the MAX over ranks,
+    match counts are summed.  Control plane only (no data-path collective)."""
+    if world <= 1:
+        return total_s, found, flagged, expected
+    dev_t = "cuda" if backend == "nccl" else "cpu"
+    tt = torch.tensor([total_s], dtype=torch.float64, device=dev_t)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    cnt = torch.tensor([found, flagged, expected], dtype=torch.int64, device=dev_t)
+    dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    f, fl, e = (int(x) for x in cnt.tolist())
+    return float(tt.item()), f, fl, e
+
+
+def shard_first_row(rank, rows_per_rank):
+    """Global index of a rank's first row (weak scaling: rank r owns rows
+    [r * rows_per_rank, (r + 1) * rows_per_rank) of one conceptual table)."""
+    return rank * rows_per_rank
+
+
 def run_step(tab, scanners, streams, events=None):
+    """One pass over the rank's table.  Each batch is the two kernels of
+    cudasp_scan_device (stage A then stage B on the batch's stream); when
+    `events` is a list, HIP events bracket each launch on its stream (the
+    per-launch kernel durations of the roofline)."""
     tab.match_count.zero_()
     for b in range(tab.nb):
         s = b % len(scanners)
         st = streams[s]
+        m = tab.sizes[b]
         with torch.cuda.stream(st):
-            m = tab.sizes[b]
             if events is not None:
                 e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
                 e0.record(st)
-                scanners[s].stage_shared_secret(tab.tx[b], tab.ty[b], m, st)
+            scanners[s].stage_shared_secret(tab.tx[b], tab.ty[b], m, st)
+            if events is not None:
                 e1.record(st)
-                scanners[s].stage_match(tab.outs[b], tab.offs[b], tab.lens[b], m, tab.flags[b],
-                                        tab.match_rows[b], tab.match_count[b:b + 1], st)
+            scanners[s].stage_match(tab.outs[b], tab.offs[b], tab.lens[b], m, tab.flags[b],
+                                    tab.match_rows[b], tab.match_count[b:b + 1], st)
+            if events is not None:
                 e2.record(st)
                 events.append((e0, e1, e2))
-            else:
-                scanners[s].scan_device(tab.tx[b], tab.ty[b], tab.outs[b], tab.offs[b], tab.lens[b],
-                                        tab.flags[b][:m], tab.match_rows[b], tab.match_count[b:b + 1], stream=st)
 
 
 def cpu_baseline(tab, labels, sample_rows, threads):
@@ -208,7 +249,7 @@ def cpu_baseline(tab, labels, sample_rows, threads):
     x = tab.cols(tab.tx, 0)[:, :m].cpu().numpy().view(np.uint32)
     y = tab.cols(tab.ty, 0)[:, :m].cpu().numpy().view(np.uint32)
     tweaks = np.ascontiguousarray(np.concatenate([x.T, y.T], axis=1).astype("<u4")).view(np.uint8).reshape(m, 64)
-    outs = tab.outs[0][: m * tab.k].cpu().numpy()
+    outs = tab.outs[0].cpu().numpy()
     offs = tab.offs[0][:m].cpu().numpy().view(np.uint32)
     lens = tab.lens[0][:m].cpu().numpy().view(np.uint32)
     t0 = time.perf_counter()
@@ -216,8 +257,8 @@ def cpu_baseline(tab, labels, sample_rows, threads):
     dt = time.perf_counter() - t0
     gpu_flags = tab.flags[0][:m].cpu().numpy()
     return dict(value=m / dt, unit="tx/s", cores=threads, kind="port",
-                sample="first %d rows of the rank-0 table (batch 0), %d labels, %d outputs/row, "
-                       "oracle/cudasp_oracle.c with %d pthreads" % (m, len(labels), tab.k, threads),
+                sample="first %d rows of the rank-0 table (batch 0), %d labels, "
+                       "oracle/cudasp_oracle.c with %d pthreads" % (m, len(labels), threads),
                 seconds=round(dt, 3), flags_match_gpu=bool(np.array_equal(flags, gpu_flags)),
                 sample_matches=int(flags.sum()))
 
@@ -231,28 +272,35 @@ def main():
     ap.add_argument("--batch-size", type=int, default=300_000)
     ap.add_argument("--labels", type=int, default=0)
     ap.add_argument("--outputs-per-row", type=int, default=2)
+    ap.add_argument("--outputs-max", type=int, default=0,
+                    help="variable outputs per row, uniform in [1, N] (15 -> mean 8, config 5); 0 = fixed")
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--cpu-rows", type=int, default=300000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_k_shared_secret.json"))
+    ap.add_argument("--pmc-sq", default=os.path.join(ROOT, "profiles", "r01_pmc_sq_counters.json"))
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) for the barrier/max; gloo to rehearse "
+                    "several ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = local if world > 1 else 0
+    device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(args.dist_backend)
     lib = _native.load()
 
     labels = label_keys(args.labels)
     gen_stream = torch.cuda.Stream(device)
     t_setup = time.perf_counter()
     tab = Table(lib, device, args.rows, args.batch_size, args.outputs_per_row, labels,
-                first_global=rank * args.rows, dev_stream=gen_stream)
+                first_global=shard_first_row(rank, args.rows), dev_stream=gen_stream, kmax=args.outputs_max)
     streams = [torch.cuda.Stream(device) for _ in range(args.streams)]
     scanners = [Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=args.batch_size, device=device)
                 for _ in range(args.streams)]
@@ -267,33 +315,30 @@ def main():
     torch.cuda.synchronize(device)
 
     times = []
+    events = []
     for _ in range(args.steps):
         barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
-        run_step(tab, scanners, streams)
+        run_step(tab, scanners, streams, events=events)
         torch.cuda.synchronize(device)
         barrier()
         times.append(time.perf_counter() - t0)
     step_s = float(np.mean(times))
     total_s = float(np.sum(times))
-    if world > 1:
-        tt = torch.tensor([total_s], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        total_s = float(tt.item())
     found = int(tab.match_count.sum().item())
     flagged = int(tab.flags.sum().item())
+    total_s, found, flagged, expected = aggregate(world, args.dist_backend, total_s, found, flagged, tab.expected)
 
-    # Per-launch kernel durations (HIP events on the launching stream), one
-    # extra pass with each batch split into its two stage launches.
-    events = []
-    run_step(tab, scanners, streams, events=events)
-    torch.cuda.synchronize(device)
+    # Per-launch kernel durations over the timed region (HIP events on each
+    # launch's stream; with several streams a launch's span includes the time
+    # it shares the GPU with the other streams' kernels).
     ka = [e0.elapsed_time(e1) for e0, e1, _ in events]
     kb = [e1.elapsed_time(e2) for _, e1, e2 in events]
     ka_ms, kb_ms = float(np.mean(ka)), float(np.mean(kb))
     rows_per_launch = float(np.mean(tab.sizes))
-    algo_bytes = bytes_per_row(args.outputs_per_row) * rows_per_launch
+    mean_k = tab.total_outputs / args.rows
+    algo_bytes = bytes_per_row(mean_k) * rows_per_launch
     achieved_gbs = algo_bytes / (ka_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.pmc_summary):
@@ -302,21 +347,47 @@ def main():
 
     rows_total = args.rows * world * args.steps
     value = rows_total / total_s
+
+    # Integer-VALU roofline of the whole path: VALU wave-instructions per row
+    # of both kernels (rocprofv3 SQ_INSTS_VALU, profiles/) x this run's rows/s
+    # per GPU, against the measured VOP3 issue rate.
+    alu = None
+    if os.path.exists(args.pmc_sq):
+        with open(args.pmc_sq) as f:
+            sq = json.load(f)
+        per = sq["per_kernel"]
+        rpl = float(sq.get("rows_per_launch", 300000))
+        a = per.get("k_shared_secret", {}).get("SQ_INSTS_VALU")
+        bm = per.get("void k_match<false>", {}).get("SQ_INSTS_VALU")
+        if a and bm:
+            wi_per_row = (a + bm) / rpl
+            achieved_wi = wi_per_row * value / world
+            alu = dict(bound="valu", unit="wave-instr/s per GPU", achieved=achieved_wi, peak=VALU_WAVE_INSTR_PEAK,
+                       frac=achieved_wi / VALU_WAVE_INSTR_PEAK, measured_vop3_issue_rate=VOP3_WAVE_INSTR_MEASURED,
+                       frac_of_measured_vop3_rate=achieved_wi / VOP3_WAVE_INSTR_MEASURED,
+                       valu_wave_instr_per_64_rows=dict(k_shared_secret=a / rpl * 64, k_match=bm / rpl * 64),
+                       note="SQ_INSTS_VALU per row from %s (0 labels, 2 outputs/row); peak = nominal VALU "
+                            "issue rate; VOP3 integer ops issue at about half of it on gfx950" % os.path.basename(args.pmc_sq))
+
     result = dict(
         metric=METRIC, value=value, unit="tx/s", n_gpus=world, steps=args.steps, warmup=args.warmup,
         ms_per_step=total_s / args.steps * 1e3, higher_is_better=True, scaling="weak", vs_baseline=None,
         dtype="u32", data="synthetic",
-        config=dict(workload="32.7M-row synthetic tweak table per rank, %d labels, %d outputs/row, "
+        config=dict(workload="%.1fM-row synthetic tweak table per rank, %d labels, %s outputs/row, "
                              "batch_size %d, device-resident (BASELINE.json configs[3] shape; each rank "
-                             "scans its own table)" % (args.labels, args.outputs_per_row, args.batch_size),
+                             "scans its own table)" % (args.rows / 1e6, args.labels,
+                                                       ("1..%d (mean %.2f)" % (args.outputs_max, mean_k))
+                                                       if args.outputs_max else str(args.outputs_per_row),
+                                                       args.batch_size),
                     rows_per_rank=args.rows, batch_size=args.batch_size, labels=args.labels,
-                    outputs_per_row=args.outputs_per_row, streams=args.streams, parallelism="dp%d" % world),
+                    outputs_per_row=round(mean_k, 3), streams=args.streams, parallelism="dp%d" % world),
         roofline=dict(bound="hbm", achieved=achieved_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                       frac=achieved_gbs / HBM_PEAK_GBS, traffic=traffic,
                       kernel="k_shared_secret", kernel_ms=ka_ms, match_kernel_ms=kb_ms,
                       algorithmic_bytes_per_launch=algo_bytes, rows_per_launch=rows_per_launch,
                       note="integer-VALU-bound path; see alu_roofline"),
-        matches=dict(found=found, flagged=flagged, expected_planted_rank0=tab.expected),
+        alu_roofline=alu,
+        matches=dict(found=found, flagged=flagged, expected_planted=expected),
         setup_s=round(setup_s, 2),
     )
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

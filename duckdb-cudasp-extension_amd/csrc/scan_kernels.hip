@@ -246,6 +246,27 @@ __global__ __launch_bounds__(BLOCK) void k_synth_outputs(uint64_t seed, uint64_t
   }
 }
 
+// Variable-length outputs lists: pass 1 writes lengths uniform in [1, kmax]
+// (mean (kmax+1)/2), the caller scans them into offsets, pass 2 fills values.
+__global__ __launch_bounds__(BLOCK) void k_synth_output_lengths(uint64_t seed, uint64_t first, uint32_t n,
+                                                                uint32_t kmax, uint32_t* __restrict__ lens) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < n; row += stride)
+    lens[row] = 1u + (uint32_t)(splitmix64(~seed ^ (first + row)) % kmax);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_synth_output_values(uint64_t seed, uint64_t first, uint32_t n,
+                                                               const uint32_t* __restrict__ offs,
+                                                               const uint32_t* __restrict__ lens,
+                                                               int64_t* __restrict__ outs) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < n; row += stride) {
+    uint64_t g = first + row;
+    for (uint32_t j = 0; j < lens[row]; j++)
+      outs[(size_t)offs[row] + j] = (int64_t)splitmix64(seed ^ ((g << 4) + j));
+  }
+}
+
 // ------------------------------------------------------------- host helpers
 namespace {
 
@@ -592,6 +613,26 @@ int cudasp_synth_outputs(uint64_t seed, uint64_t first_index, uint32_t n, uint32
   if (!d_outputs || !d_offsets || !d_lengths) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   hipLaunchKernelGGL(k_synth_outputs, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, seed, first_index, n,
                      k, d_outputs, d_offsets, d_lengths);
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+int cudasp_synth_output_lengths(uint64_t seed, uint64_t first_index, uint32_t n, uint32_t kmax, uint32_t* d_lengths,
+                                void* stream) {
+  if (n == 0) return CUDASP_OK;
+  if (!d_lengths || kmax == 0) return set_error(CUDASP_ERR_INVALID_ARG, "invalid argument");
+  hipLaunchKernelGGL(k_synth_output_lengths, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, seed,
+                     first_index, n, kmax, d_lengths);
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+int cudasp_synth_output_values(uint64_t seed, uint64_t first_index, uint32_t n, const uint32_t* d_offsets,
+                               const uint32_t* d_lengths, int64_t* d_outputs, void* stream) {
+  if (n == 0) return CUDASP_OK;
+  if (!d_offsets || !d_lengths || !d_outputs) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
+  hipLaunchKernelGGL(k_synth_output_values, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, seed,
+                     first_index, n, d_offsets, d_lengths, d_outputs);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
 }

@@ -36,6 +36,8 @@ SIGNATURES = {
     "cudasp_stage_match_device": (_I32, [_P, _P, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "cudasp_synth_tweak_columns": (_I32, [_I32, _P, ctypes.c_uint64, _U32, _P, _P, _P]),
     "cudasp_synth_outputs": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _U32, _P, _P, _P, _P]),
+    "cudasp_synth_output_lengths": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _U32, _P, _P]),
+    "cudasp_synth_output_values": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _P, _P, _P, _P]),
     "LaunchBatchScan": (_P, [_P, _P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _U32, ctypes.c_size_t]),
     "RunBatchScanKernels": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _U32]),
     "FreeBatchScanState": (None, [_P]),

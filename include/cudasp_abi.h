@@ -117,6 +117,12 @@ int cudasp_synth_tweak_columns(int device, const uint8_t s0_le[32], uint64_t fir
                                uint32_t* d_x, uint32_t* d_y, void* stream);
 int cudasp_synth_outputs(uint64_t seed, uint64_t first_index, uint32_t n, uint32_t k, int64_t* d_outputs,
                          uint32_t* d_offsets, uint32_t* d_lengths, void* stream);
+/* Variable-length lists (mean (kmax+1)/2 outputs per row): lengths uniform in
+ * [1, kmax]; the caller exclusive-scans them into offsets, then the values. */
+int cudasp_synth_output_lengths(uint64_t seed, uint64_t first_index, uint32_t n, uint32_t kmax, uint32_t* d_lengths,
+                                void* stream);
+int cudasp_synth_output_values(uint64_t seed, uint64_t first_index, uint32_t n, const uint32_t* d_offsets,
+                               const uint32_t* d_lengths, int64_t* d_outputs, void* stream);
 
 /* -------------------------------------------- reference three-phase ABI */
 void* LaunchBatchScan(uint32_t** managed_points_x, uint32_t** managed_points_y, const uint32_t* h_scalar,

@@ -1,0 +1,18 @@
+# Round-1 measurement sweep on one MI355X (each GPU step bounded; stop at the first failure).
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out
+step() { local name=$1; shift; timeout -k 10 "$@" > $R/gpurun_out/$name.log 2>&1 || { echo "$name failed"; tail -30 $R/gpurun_out/$name.log; exit 1; }; tail -1 $R/gpurun_out/$name.log | cut -c1-600; }
+step pytest 400 python -m pytest tests -m gpu -x -q
+step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
+step bench_default 400 python bench.py
+step bench_cfg3 400 python bench.py --rows 9400000 --labels 1 --steps 3
+step bench_cfg5 600 python bench.py --rows 100000000 --labels 16 --outputs-max 15 --steps 2 --cpu-rows 50000
+step bench_2rank_gloo 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --rows 3000000 --steps 2 --dist-backend gloo
+cd /tmp && export TMPDIR=/tmp
+step prof_bench 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_bench -o bench -- python3 $R/bench.py --steps 2 --no-cpu-baseline
+step pmc_sq 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $R/gpurun_out/pmc_sq -o sq -- python3 $R/tools/quick_timing.py 300000 0
+step pmc_sq2 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM --output-format csv -d $R/gpurun_out/pmc_sq2 -o sq2 -- python3 $R/tools/quick_timing.py 300000 0
+step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -o fetch -- python3 $R/bench.py --rows 3000000 --steps 1 --warmup 0 --no-cpu-baseline
+step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -o write -- python3 $R/bench.py --rows 3000000 --steps 1 --warmup 0 --no-cpu-baseline
+echo all-done
