@@ -267,6 +267,25 @@ __global__ __launch_bounds__(BLOCK) void k_synth_output_values(uint64_t seed, ui
   }
 }
 
+__global__ __launch_bounds__(BLOCK) void k_debug_field_ops(int op, const uint32_t* __restrict__ a,
+                                                           const uint32_t* __restrict__ b,
+                                                           uint32_t* __restrict__ out, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe x, y, r;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    x.n[k] = a[(size_t)i * 10 + k];
+    y.n[k] = b[(size_t)i * 10 + k];
+  }
+  if (op == 0)
+    fe_mul(r, x, y);
+  else
+    fe_sqr(r, x);
+#pragma unroll
+  for (int k = 0; k < 10; k++) out[(size_t)i * 10 + k] = r.n[k];
+}
+
 // ------------------------------------------------------------- host helpers
 namespace {
 
@@ -634,6 +653,16 @@ int cudasp_synth_output_values(uint64_t seed, uint64_t first_index, uint32_t n, 
   hipLaunchKernelGGL(k_synth_output_values, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, seed,
                      first_index, n, d_offsets, d_lengths, d_outputs);
   HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+int cudasp_debug_field_ops(int op, const uint32_t* d_a, const uint32_t* d_b, uint32_t* d_out, uint32_t n) {
+  if (n == 0) return CUDASP_OK;
+  if (op != 0 && op != 1) return set_error(CUDASP_ERR_INVALID_ARG, "op must be 0 (mul) or 1 (sqr)");
+  if (!d_a || !d_b || !d_out) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
+  hipLaunchKernelGGL(k_debug_field_ops, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, 0, op, d_a, d_b, d_out, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
   return CUDASP_OK;
 }
 

@@ -107,6 +107,10 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
   for (int e = 1; e < VB_ENTRIES; e++) {
     fe zr;
     gej_add_ge(acc, acc, dge, &zr);
+    if (e == VB_ENTRIES - 1) {  // the only entry not rescaled below
+      fe_normalize_weak(acc.x);
+      fe_normalize_weak(acc.y);
+    }
     scr_store(sc, VB_ENTRY_X(e), acc.x);
     scr_store(sc, VB_ENTRY_Y(e), acc.y);
     scr_store(sc, VB_ZR(e - 1), zr);

@@ -13,10 +13,12 @@
 //
 // Magnitude convention (checked by the host emulation build, see
 // CUDASP_FE_CHECK): a value has magnitude m when limbs 0..8 are <= m*2^26 and
-// limb 9 <= m*2^22 (plus a 2^22 / 2^12 slack so that the "weak" outputs of
+// limb 9 <= m*2^22 (plus a 2^23 / 2^13 slack so that the "weak" outputs of
 // mul/sqr/normalize_weak, whose limbs may exceed 2^26 by a carry, count as 1).
-// mul/sqr accept m <= 8 and return m = 1.  fe_add adds magnitudes;
-// fe_sub<K>(r, a, b) and fe_negate<K> need mag(b) <= K and add 2K.
+// mul/sqr accept mag(a) * mag(b) <= MUL_MAG_MAX with each <= 31 and return
+// m = 1: the widest product column (column 9: eight full limb products plus
+// two with limb 9) stays below 8 * 408 * 2^52 + 2^52 < 2^64.  fe_add adds
+// magnitudes; fe_sub<K>(r, a, b) and fe_negate<K> need mag(b) <= K and add 2K.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,18 +39,41 @@ constexpr uint32_t R1 = 0x400u;
 // 2^256 mod p = 0x3D1 + 0x40 * 2^26
 constexpr uint32_t F0 = 0x3D1u;
 constexpr uint32_t F1 = 0x40u;
+constexpr uint32_t MUL_MAG_MAX = 400;
 
 #ifdef CUDASP_FE_CHECK
 // Host-emulation builds verify every magnitude precondition.
 void fe_check_fail(const char* what, int limb, uint32_t v);
 CUDASP_HD void fe_check_mag(const fe& a, uint32_t m, const char* what) {
   for (int i = 0; i < 9; i++)
-    if ((uint64_t)a.n[i] > (uint64_t)m * (1ull << 26) + (1ull << 22)) fe_check_fail(what, i, a.n[i]);
-  if ((uint64_t)a.n[9] > (uint64_t)m * (1ull << 22) + (1ull << 12)) fe_check_fail(what, 9, a.n[9]);
+    if ((uint64_t)a.n[i] > (uint64_t)m * (1ull << 26) + (1ull << 23)) fe_check_fail(what, i, a.n[i]);
+  if ((uint64_t)a.n[9] > (uint64_t)m * (1ull << 22) + (1ull << 13)) fe_check_fail(what, 9, a.n[9]);
+}
+// Smallest magnitude m that a's limbs satisfy.
+CUDASP_HD uint32_t fe_mag_of(const fe& a) {
+  uint64_t m = 1;
+  for (int i = 0; i < 9; i++)
+    if (a.n[i] > (1u << 23)) {
+      uint64_t need = ((uint64_t)a.n[i] - (1u << 23) + (1u << 26) - 1) >> 26;
+      if (need > m) m = need;
+    }
+  if (a.n[9] > (1u << 13)) {
+    uint64_t need = ((uint64_t)a.n[9] - (1u << 13) + (1u << 22) - 1) >> 22;
+    if (need > m) m = need;
+  }
+  return (uint32_t)m;
+}
+CUDASP_HD void fe_check_mul(const fe& a, const fe& b, const char* what) {
+  uint32_t ma = fe_mag_of(a), mb = fe_mag_of(b);
+  if (ma > 31) fe_check_fail(what, -1, ma);
+  if (mb > 31) fe_check_fail(what, -2, mb);
+  if (ma * mb > MUL_MAG_MAX) fe_check_fail(what, -3, ma * mb);
 }
 #define FE_CHECK(a, m, what) fe_check_mag(a, m, what)
+#define FE_CHECK_MUL(a, b, what) fe_check_mul(a, b, what)
 #else
 #define FE_CHECK(a, m, what) ((void)0)
+#define FE_CHECK_MUL(a, b, what) ((void)0)
 #endif
 
 CUDASP_HD void fe_set_int(fe& r, uint32_t v) {
@@ -202,8 +227,14 @@ CUDASP_HD uint32_t opaque_const(uint32_t v) {
 //      (no high-half carry chain)                                 2.85 ms  <- default
 //   2  explicit serial mad chains in inline asm: fewest VALU (184/148 per
 //      mul/sqr) but the compiler pads every asm result with s_nop  2.94 ms
+//   3  variant 1's arithmetic as ONE generated asm block per operation
+//      (secp256k1_fe_asm.inc, tools/gen_fe_asm.py): 172 / 127 instructions,
+//      every column one mad chain seeded with the previous carry; host
+//      builds use variant 1's C code
+//   4  as 3, scheduled for 2-way ILP (high column k+1 computed beside low
+//      column k; 175 / 130 instructions, 20 fixed temporaries)
 #ifndef CUDASP_FE_VARIANT
-#define CUDASP_FE_VARIANT 1
+#define CUDASP_FE_VARIANT 3
 #endif
 #if CUDASP_FE_VARIANT == 0
 // Reduction shared by mul and sqr.  c[0..18] are the product columns
@@ -257,8 +288,7 @@ CUDASP_HD void fe_reduce_columns(fe& r, const uint64_t c[19]) {
 }
 
 CUDASP_HD void fe_mul(fe& r, const fe& a, const fe& b) {
-  FE_CHECK(a, 8, "mul a");
-  FE_CHECK(b, 8, "mul b");
+  FE_CHECK_MUL(a, b, "mul");
   uint64_t c[19];
 #pragma unroll
   for (int k = 0; k < 19; k++) {
@@ -274,7 +304,7 @@ CUDASP_HD void fe_mul(fe& r, const fe& a, const fe& b) {
 }
 
 CUDASP_HD void fe_sqr(fe& r, const fe& a) {
-  FE_CHECK(a, 8, "sqr");
+  FE_CHECK_MUL(a, a, "sqr");
   uint32_t a2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) a2[i] = a.n[i] * 2;
@@ -293,7 +323,7 @@ CUDASP_HD void fe_sqr(fe& r, const fe& a) {
   fe_reduce_columns(r, c);
 }
 
-#elif CUDASP_FE_VARIANT == 1
+#elif CUDASP_FE_VARIANT == 1 || CUDASP_FE_VARIANT == 3 || CUDASP_FE_VARIANT == 4
 CUDASP_HD void fe_reduce_columns(fe& r, const uint64_t c[19]) {
   const uint32_t r0 = opaque_const(R0), r1 = opaque_const(R1);
   const uint32_t r0s = opaque_const(R0 << 6), r1s = opaque_const(R1 << 6);
@@ -335,9 +365,7 @@ CUDASP_HD void fe_reduce_columns(fe& r, const uint64_t c[19]) {
   for (int k = 3; k < 10; k++) r.n[k] = o[k];
 }
 
-CUDASP_HD void fe_mul(fe& r, const fe& a, const fe& b) {
-  FE_CHECK(a, 8, "mul a");
-  FE_CHECK(b, 8, "mul b");
+CUDASP_HD void fe_mul_c(fe& r, const fe& a, const fe& b) {
   uint64_t c[19];
 #pragma unroll
   for (int k = 0; k < 19; k++) {
@@ -352,8 +380,7 @@ CUDASP_HD void fe_mul(fe& r, const fe& a, const fe& b) {
   fe_reduce_columns(r, c);
 }
 
-CUDASP_HD void fe_sqr(fe& r, const fe& a) {
-  FE_CHECK(a, 8, "sqr");
+CUDASP_HD void fe_sqr_c(fe& r, const fe& a) {
   uint32_t a2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) a2[i] = a.n[i] * 2;
@@ -370,6 +397,32 @@ CUDASP_HD void fe_sqr(fe& r, const fe& a) {
     c[k] = s;
   }
   fe_reduce_columns(r, c);
+}
+
+#if CUDASP_FE_VARIANT >= 3 && defined(__HIP_DEVICE_COMPILE__)
+#include "secp256k1_fe_asm.inc"
+#endif
+
+CUDASP_HD void fe_mul(fe& r, const fe& a, const fe& b) {
+  FE_CHECK_MUL(a, b, "mul");
+#if CUDASP_FE_VARIANT == 3 && defined(__HIP_DEVICE_COMPILE__)
+  fe_mul_asm(r, a, b);
+#elif CUDASP_FE_VARIANT == 4 && defined(__HIP_DEVICE_COMPILE__)
+  fe_mul_asm_p(r, a, b);
+#else
+  fe_mul_c(r, a, b);
+#endif
+}
+
+CUDASP_HD void fe_sqr(fe& r, const fe& a) {
+  FE_CHECK_MUL(a, a, "sqr");
+#if CUDASP_FE_VARIANT == 3 && defined(__HIP_DEVICE_COMPILE__)
+  fe_sqr_asm(r, a);
+#elif CUDASP_FE_VARIANT == 4 && defined(__HIP_DEVICE_COMPILE__)
+  fe_sqr_asm_p(r, a);
+#else
+  fe_sqr_c(r, a);
+#endif
 }
 
 #else
@@ -479,13 +532,12 @@ CUDASP_HD void fe_mul_impl(fe& r, const fe& a, const fe& b) {
 }
 
 CUDASP_HD void fe_mul(fe& r, const fe& a, const fe& b) {
-  FE_CHECK(a, 8, "mul a");
-  FE_CHECK(b, 8, "mul b");
+  FE_CHECK_MUL(a, b, "mul");
   fe_mul_impl<false>(r, a, b);
 }
 
 CUDASP_HD void fe_sqr(fe& r, const fe& a) {
-  FE_CHECK(a, 8, "sqr");
+  FE_CHECK_MUL(a, a, "sqr");
   fe_mul_impl<true>(r, a, a);
 }
 

@@ -124,6 +124,13 @@ int cudasp_synth_output_lengths(uint64_t seed, uint64_t first_index, uint32_t n,
 int cudasp_synth_output_values(uint64_t seed, uint64_t first_index, uint32_t n, const uint32_t* d_offsets,
                                const uint32_t* d_lengths, int64_t* d_outputs, void* stream);
 
+/* Test hook (field arithmetic of the kernels, on the device): for i < n,
+ * out[i] = a[i] * b[i] (op 0) or a[i]^2 (op 1) mod p, each operand 10 x u32
+ * 26-bit limbs (row-major, 10 words per element, any magnitude the kernels
+ * accept: mag(a) * mag(b) <= 400, each <= 31); the result is magnitude 1,
+ * not fully reduced.  Device buffers; synchronous. */
+int cudasp_debug_field_ops(int op, const uint32_t* d_a, const uint32_t* d_b, uint32_t* d_out, uint32_t n);
+
 /* -------------------------------------------- reference three-phase ABI */
 void* LaunchBatchScan(uint32_t** managed_points_x, uint32_t** managed_points_y, const uint32_t* h_scalar,
                       const uint32_t* h_spend_pubkey_x, const uint32_t* h_spend_pubkey_y,
