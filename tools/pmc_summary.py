@@ -1,0 +1,86 @@
+"""Turn rocprofv3 --pmc counter-collection CSVs into the JSON summaries under
+profiles/ that bench.py reads.
+
+  python tools/pmc_summary.py sq   OUT.json  CSV [CSV ...]   # SQ_* / GRBM_* averages per dispatch
+  python tools/pmc_summary.py hbm  OUT.json  FETCH_CSV WRITE_CSV --rows N
+
+`sq`: per kernel, the average of every counter per dispatch (dispatches with the
+largest grid only for the scan kernels, so partial batches do not dilute).
+`hbm`: per kernel FETCH_SIZE / WRITE_SIZE in KiB per launch; FETCH_SIZE is
+doubled as MI355X_MICROARCH.md's HBM section prescribes for gfx950 (it reports
+half of wide coalesced reads); hbm_bytes_per_launch = 2 FETCH + WRITE of
+k_shared_secret, match_kernel_hbm_bytes_per_launch the same for k_match<false>.
+"""
+import argparse
+import collections
+import csv
+import json
+
+SCAN_KERNELS = ("k_shared_secret", "void k_match<false>", "void k_match<true>")
+
+
+def load(paths):
+    """{kernel: {counter: [(grid, value) per dispatch]}} (counters summed per dispatch)."""
+    per = collections.defaultdict(lambda: collections.defaultdict(dict))
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            k = r["Kernel_Name"].split("(")[0]
+            key = (p, r["Dispatch_Id"])
+            grid = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
+            c = r["Counter_Name"]
+            prev = per[k][c].get(key, (grid, 0.0))
+            per[k][c][key] = (grid, prev[1] + float(r["Counter_Value"]))
+    return per
+
+
+def averages(per):
+    out = {}
+    for k, counters in per.items():
+        out[k] = {}
+        for c, disp in counters.items():
+            vals = list(disp.values())
+            if k in SCAN_KERNELS:
+                gmax = max(g for g, _ in vals)
+                vals = [(g, v) for g, v in vals if g == gmax]
+            out[k][c] = sum(v for _, v in vals) / len(vals)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["sq", "hbm"])
+    ap.add_argument("out")
+    ap.add_argument("csvs", nargs="+")
+    ap.add_argument("--rows", type=int, default=300000)
+    ap.add_argument("--source", default="")
+    ap.add_argument("--algorithmic-bytes-per-row", type=float, default=89.0)
+    a = ap.parse_args()
+    if a.mode == "sq":
+        res = dict(source=a.source, rows_per_launch=a.rows, per_kernel=averages(load(a.csvs)))
+    else:
+        fetch = averages(load([a.csvs[0]]))
+        write = averages(load([a.csvs[1]]))
+        per = {}
+        for k in set(fetch) | set(write):
+            per[k] = dict(FETCH_SIZE_KiB_per_launch=fetch.get(k, {}).get("FETCH_SIZE", 0.0),
+                          WRITE_SIZE_KiB_per_launch=write.get(k, {}).get("WRITE_SIZE", 0.0))
+
+        def hbm(k):
+            v = per.get(k)
+            return None if v is None else (2 * v["FETCH_SIZE_KiB_per_launch"] + v["WRITE_SIZE_KiB_per_launch"]) * 1024
+
+        res = dict(source=a.source,
+                   correction="FETCH_SIZE doubled per MI355X_MICROARCH.md HBM section (gfx950 reports half of wide "
+                              "coalesced reads); WRITE_SIZE as reported; units KiB",
+                   per_kernel=per, kernel="k_shared_secret", hbm_bytes_per_launch=hbm("k_shared_secret"),
+                   match_kernel_hbm_bytes_per_launch=hbm("void k_match<false>"), rows_per_launch=a.rows,
+                   algorithmic_bytes_per_launch=a.algorithmic_bytes_per_row * a.rows)
+    json.dump(res, open(a.out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "per_kernel"}, indent=1))
+    for k in SCAN_KERNELS:
+        if k in res["per_kernel"]:
+            print(k, json.dumps(res["per_kernel"][k]))
+
+
+if __name__ == "__main__":
+    main()
