@@ -95,7 +95,8 @@ HPoint hp_generator() {
   return hp_from_bytes(gbytes);
 }
 
-// 2^(16 i) G for i = 0..16 (the last one is 2^256 G), computed once.
+// 2^(FB_BITS i) G for i = 0..FB_WINDOWS (the last one is the recoding
+// constant 2^(FB_BITS FB_WINDOWS) G), computed once.
 struct GenPowers {
   HPoint q[FB_WINDOWS + 1];
   GenPowers() {
@@ -103,7 +104,7 @@ struct GenPowers {
     for (int i = 0; i <= FB_WINDOWS; i++) {
       q[i] = cur;
       if (i == FB_WINDOWS) break;
-      for (int d = 0; d < 16; d++) cur = hp_add(cur, cur);
+      for (int d = 0; d < FB_BITS; d++) cur = hp_add(cur, cur);
     }
   }
 };

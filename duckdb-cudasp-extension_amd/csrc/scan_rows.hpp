@@ -18,16 +18,25 @@ namespace cudasp {
 // Variable-base window: odd multiples 1,3,...,15 of T (width-5 NAF digits).
 constexpr int VB_ENTRIES = 8;
 constexpr int NAF_MAX = 136;
-// Fixed-base table: 16 windows x 32768 odd multiples, 64 bytes per entry.
-constexpr int FB_WINDOWS = 16;
-constexpr int FB_ENTRIES = 32768;
+// Fixed-base table: FB_WINDOWS windows of FB_BITS-bit signed odd digits, each
+// with FB_ENTRIES odd multiples (2j+1) 2^(FB_BITS i) G, 64 bytes per entry.
+// t (256 bits, made odd) = sum_i d_i 2^(FB_BITS i) + 2^(FB_BITS FB_WINDOWS),
+// so P0 = t G costs FB_WINDOWS gathers + mixed additions.  Default 22 bits:
+// 12 windows, 1.5 GiB per device (16 bits: 16 windows, 32 MiB).
+#ifndef CUDASP_FB_BITS
+#define CUDASP_FB_BITS 22
+#endif
+constexpr int FB_BITS = CUDASP_FB_BITS;
+static_assert(FB_BITS >= 8 && FB_BITS <= 24, "fixed-base window width");
+constexpr int FB_WINDOWS = (256 + FB_BITS - 1) / FB_BITS;
+constexpr uint32_t FB_ENTRIES = 1u << (FB_BITS - 1);
 constexpr int FB_WORDS = 16;
 
 // Per-query constants, passed to the kernels by value.
 struct ScanConsts {
   uint32_t mid[8];      // SHA-256 state after the constant block H(tag)||H(tag)
-  uint32_t c_odd[16];   // 2^256 G                (x[8], y[8], normalized LE words)
-  uint32_t c_even[16];  // 2^256 G - G            (used when the hash t is even)
+  uint32_t c_odd[16];   // 2^(FB_BITS FB_WINDOWS) G      (x[8], y[8], normalized LE words)
+  uint32_t c_even[16];  // 2^(FB_BITS FB_WINDOWS) G - G  (used when the hash t is even)
   uint32_t spend[16];   // B, the spend public key (normalized)
   uint32_t naf_len;     // digits in each GLV half
   uint32_t label_count;
@@ -205,9 +214,11 @@ CUDASP_HD bool outputs_contain(const int64_t* outputs, uint32_t off, uint32_t le
 // no x coordinate exists, the row cannot match through it.
 constexpr int64_t LABEL_INFINITY = (int64_t)0x8000000000000000ull;
 
-CUDASP_HD void fb_entry(ge& P, const uint32_t* table, int window, uint32_t bits16) {
-  bool neg = (bits16 & 0x8000u) == 0;
-  uint32_t j = (bits16 ^ (neg ? 0x7FFFu : 0u)) & 0x7FFFu;
+// Entry for the digit d = 2 b + 1 - 2^FB_BITS of window `window` (b = the
+// window's FB_BITS bits): |d| = 2j + 1, negated when b < 2^(FB_BITS-1).
+CUDASP_HD void fb_entry(ge& P, const uint32_t* table, int window, uint32_t bits) {
+  bool neg = (bits & FB_ENTRIES) == 0;
+  uint32_t j = (bits ^ (neg ? FB_ENTRIES - 1 : 0u)) & (FB_ENTRIES - 1);
   const uint32_t* e = table + ((size_t)window * FB_ENTRIES + j) * FB_WORDS;
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t w[16];
@@ -226,7 +237,8 @@ CUDASP_HD void fb_entry(ge& P, const uint32_t* table, int window, uint32_t bits1
 
 // P = t*G (Jacobian) from the fixed-base table.  t: 8 LE words, any 256-bit
 // value (not reduced mod n, like the reference, src/cudasp_gpu.cu:862-877;
-// n*G = O makes that irrelevant).  c_odd / c_even: 2^256 G and 2^256 G - G.
+// n*G = O makes that irrelevant).  c_odd / c_even: 2^(FB_BITS FB_WINDOWS) G
+// and that minus G.
 CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb_table, const uint32_t* c_odd,
                               const uint32_t* c_even) {
   // t even -> use t+1 and add -G at the end (odd-digit recoding needs an odd
@@ -237,17 +249,18 @@ CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb
   t[8] = 0;
   bool even = (t[0] & 1u) == 0;
   t[0] |= 1u;
-  // t = sum_{i<16} d_i 2^(16 i) + 2^256 with odd d_i = 2 b_i + 1 - 2^16,
-  // b_i = bits [16i+1, 16i+16] of t.  2^256 G (- G) is the constant c_odd / c_even.
+  // t = sum_{i<W} d_i 2^(w i) + 2^(w W) with odd d_i = 2 b_i + 1 - 2^w,
+  // b_i = bits [w i + 1, w i + w] of t (w = FB_BITS, W = FB_WINDOWS; bits past
+  // 255 are 0).  2^(w W) G (- G) is the constant c_odd / c_even.
   // The window loop is not unrolled (16 mixed additions would blow the
   // instruction cache), so t is consumed by shifting instead of indexing a
   // register array with the loop counter (that would spill to scratch).
 #pragma unroll 1
   for (int i = 0; i < FB_WINDOWS; i++) {
-    uint32_t bits = (t[0] >> 1) & 0xFFFFu;
+    uint32_t bits = (t[0] >> 1) & ((FB_ENTRIES << 1) - 1);
 #pragma unroll
-    for (int q = 0; q < 8; q++) t[q] = (t[q] >> 16) | (t[q + 1] << 16);
-    t[8] >>= 16;
+    for (int q = 0; q < 8; q++) t[q] = (t[q] >> FB_BITS) | (t[q + 1] << (32 - FB_BITS));
+    t[8] >>= FB_BITS;
     ge P;
     fb_entry(P, fb_table, i, bits);
     if (i == 0) {
@@ -344,7 +357,7 @@ CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const
 
 // Fixed-base table entry (2j+1) * 2^(16 window) * G from the window base Q.
 CUDASP_HD void fb_build_entry(uint32_t out[16], const ge& Q, uint32_t j) {
-  uint32_t m = 2 * j + 1;  // 1..65535
+  uint32_t m = 2 * j + 1;  // 1 .. 2^FB_BITS - 1
   int top = 31 - __builtin_clz(m);
   gej R;
   gej_set_ge(R, Q);

@@ -56,12 +56,19 @@ void words_from_row(uint32_t x[8], uint32_t y[8], const uint8_t* row) {
   }
 }
 
-// Lazily filled copy of the device fixed-base table.
+// Lazily filled copy of the device fixed-base table.  The arrays come from
+// calloc, so only the pages of entries actually built are ever touched (the
+// full table is 1.5 GiB at the default 22-bit windows).
 struct LazyTable {
-  std::vector<uint32_t> table;
-  std::vector<uint8_t> filled;
+  uint32_t* table;
+  uint8_t* filled;
   std::vector<uint32_t> bases;
-  LazyTable() : table((size_t)FB_WINDOWS * FB_ENTRIES * FB_WORDS), filled((size_t)FB_WINDOWS * FB_ENTRIES), bases(fb_window_bases()) {}
+  LazyTable()
+      : table((uint32_t*)calloc((size_t)FB_WINDOWS * FB_ENTRIES * FB_WORDS, 4)),
+        filled((uint8_t*)calloc((size_t)FB_WINDOWS * FB_ENTRIES, 1)),
+        bases(fb_window_bases()) {
+    if (!table || !filled) abort();
+  }
   void ensure(int window, uint32_t j) {
     size_t idx = (size_t)window * FB_ENTRIES + j;
     if (filled[idx]) return;
@@ -70,18 +77,18 @@ struct LazyTable {
     fb_build_entry(&table[idx * FB_WORDS], Q, j);
     filled[idx] = 1;
   }
-  // Same recoding as row_match: t made odd, b_i = bits [16i+1, 16i+16].
+  // Same recoding as fixed_base_mul: t made odd, b_i = bits [w i + 1, w i + w].
   void ensure_for(const uint32_t t_in[8]) {
     uint32_t t[9];
     for (int i = 0; i < 8; i++) t[i] = t_in[i];
     t[8] = 0;
     t[0] |= 1u;
     for (int i = 0; i < FB_WINDOWS; i++) {
-      uint32_t bits = (t[0] >> 1) & 0xFFFFu;
-      for (int q = 0; q < 8; q++) t[q] = (t[q] >> 16) | (t[q + 1] << 16);
-      t[8] >>= 16;
-      bool neg = (bits & 0x8000u) == 0;
-      ensure(i, (bits ^ (neg ? 0x7FFFu : 0u)) & 0x7FFFu);
+      uint32_t bits = (t[0] >> 1) & ((FB_ENTRIES << 1) - 1);
+      for (int q = 0; q < 8; q++) t[q] = (t[q] >> FB_BITS) | (t[q + 1] << (32 - FB_BITS));
+      t[8] >>= FB_BITS;
+      bool neg = (bits & FB_ENTRIES) == 0;
+      ensure(i, (bits ^ (neg ? FB_ENTRIES - 1 : 0u)) & (FB_ENTRIES - 1));
     }
   }
 };
@@ -160,6 +167,13 @@ int emu_midstate(uint32_t mid[8]) {
   return 0;
 }
 
+int emu_fb_layout(int* bits, int* windows, uint32_t* entries) {
+  *bits = FB_BITS;
+  *windows = FB_WINDOWS;
+  *entries = FB_ENTRIES;
+  return 0;
+}
+
 int emu_fb_entry(uint32_t window, uint32_t j, uint32_t out[16]) {
   std::vector<uint32_t> bases = fb_window_bases();
   ge Q;
@@ -232,7 +246,7 @@ int emu_row_values(const uint8_t scan[32], const uint8_t spend[64], const uint8_
       for (int j = 0; j < 8; j++) t_out[8 * (size_t)r + j] = t[j];
     tab.ensure_for(t);
     uint32_t off = offs ? offs[r] : 0, len = lens ? lens[r] : 0;
-    bool hit = row_match(t, tab.table.data(), k, labels.data(), outputs, off, len, sb, vals.data(), 1);
+    bool hit = row_match(t, tab.table, k, labels.data(), outputs, off, len, sb, vals.data(), 1);
     if (values)
       for (uint32_t j = 0; j <= L; j++) values[(size_t)r * (1 + L) + j] = vals[j];
     if (flags) flags[r] = hit ? 1 : 0;

@@ -31,6 +31,7 @@ def emu():
     V = ctypes.c_void_p
     lib.emu_row_values.argtypes = [V, V, V, ctypes.c_uint32, V, ctypes.c_uint32, V, V, V, V, V, V]
     lib.emu_fb_entry.argtypes = [ctypes.c_uint32, ctypes.c_uint32, V]
+    lib.emu_fb_layout.argtypes = [V, V, V]
     lib.emu_wnaf.argtypes = [V, ctypes.c_int, V, ctypes.c_int]
     return lib
 
@@ -115,14 +116,28 @@ def test_wnaf(emu):
         assert ln == (nz[-1] + 1 if nz else 0)
 
 
+def fb_layout(emu):
+    bits, windows, entries = ctypes.c_int(), ctypes.c_int(), ctypes.c_uint32()
+    emu.emu_fb_layout(ctypes.byref(bits), ctypes.byref(windows), ctypes.byref(entries))
+    return bits.value, windows.value, entries.value
+
+
+def test_fixed_base_layout(emu):
+    bits, windows, entries = fb_layout(emu)
+    assert entries == 1 << (bits - 1) and windows * bits >= 256 > (windows - 1) * bits
+
+
 def test_fixed_base_entries(emu):
     rng = random.Random(13)
+    bits, windows, entries = fb_layout(emu)
     out = (ctypes.c_uint32 * 16)()
-    for w, j in [(0, 0), (0, 32767), (15, 0), (15, 32767)] + [(rng.randrange(16), rng.randrange(32768)) for _ in range(6)]:
+    cases = [(0, 0), (0, entries - 1), (windows - 1, 0), (windows - 1, entries - 1)]
+    cases += [(rng.randrange(windows), rng.randrange(entries)) for _ in range(6)]
+    for w, j in cases:
         emu.emu_fb_entry(w, j, out)
         x = sum(out[i] << (32 * i) for i in range(8))
         y = sum(out[8 + i] << (32 * i) for i in range(8))
-        assert (x, y) == _mul((2 * j + 1) << (16 * w))
+        assert (x, y) == _mul((2 * j + 1) << (bits * w))
 
 
 def _values(emu, scan, spend, labels, tweaks, outs=None, offs=None, lens=None):
