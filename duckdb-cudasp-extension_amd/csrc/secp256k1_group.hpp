@@ -89,6 +89,69 @@ CUDASP_HD void gej_add_ge(gej& r, const gej& a, const ge& b, fe* zr = nullptr) {
   fe_sub<1>(r.y, v, t);           // Y3 = R (V - X3) - Y1 HHH         (3)
 }
 
+// Co-Z initial doubling with update (Meloni 2007, "DBLU"), 1M + 5S: for an
+// affine T (normalized), d = 2T and t = T with the same Z = 2 T.y.
+// Output: d.x 5, d.y 17, d.z 2; t.x 1, t.y 8, t.z 2.
+CUDASP_HD void gej_dblu(gej& d, gej& t, const ge& T) {
+  fe B, E, L, S, M, u;
+  FE_CHECK(T.x, 1, "dblu x");
+  FE_CHECK(T.y, 1, "dblu y");
+  fe_sqr(B, T.x);          // B = X1^2                           (1)
+  fe_sqr(E, T.y);          // E = Y1^2                           (1)
+  fe_sqr(L, E);            // L = E^2                            (1)
+  fe_add(u, T.x, E);       //                                    (2)
+  fe_sqr(u, u);            //                                    (1)
+  fe_sub<1>(u, u, B);      //                                    (3)
+  fe_sub<1>(u, u, L);      //                                    (5)
+  fe_add(S, u, u);         // S = 2((X1+E)^2 - B - L) = 4 X1 Y1^2 (10)
+  fe_normalize_weak(S);    //                                    (1)
+  fe_mul_int(M, B, 3);     // M = 3B                             (3)
+  fe_sqr(d.x, M);          //                                    (1)
+  fe_add(u, S, S);         //                                    (2)
+  fe_sub<2>(d.x, d.x, u);  // X(2T) = M^2 - 2S                   (5)
+  fe_sub<5>(u, S, d.x);    // S - X(2T)                          (11)
+  fe_mul(d.y, M, u);       //                                    (1)
+  fe_mul_int(L, L, 8);     // 8L = 8 Y1^4                        (8)
+  fe_sub<8>(d.y, d.y, L);  // Y(2T) = M (S - X) - 8L             (17)
+  fe_add(d.z, T.y, T.y);   // Z = 2 Y1                           (2)
+  t.x = S;                 // T = (X1 (2Y1)^2, Y1 (2Y1)^3, 2Y1)
+  t.y = L;
+  t.z = d.z;
+}
+
+// Co-Z addition with update (Meloni 2007, "ZADDU"), 5M + 2S: p and q share Z;
+// r = p + q and p becomes p with r's Z.  zr (if given) receives Z(r) / Z =
+// X(p) - X(q) (mag 15).  Not for p == +-q.  r may not alias p or q.
+// Input: p.x <= 5, p.y <= 17, p.z <= 2; q.x <= 5, q.y <= 8, q.z == p.z.
+// Output: r.x 5, r.y 3, r.z 1; p.x 1, p.y 1, p.z 1.
+CUDASP_HD void gej_zaddu(gej& r, gej& p, const gej& q, fe* zr = nullptr) {
+  fe dx, dy, C, W1, W2, A1, t;
+  FE_CHECK(p.x, 5, "zaddu p.x");
+  FE_CHECK(p.y, 17, "zaddu p.y");
+  FE_CHECK(p.z, 2, "zaddu p.z");
+  FE_CHECK(q.x, 5, "zaddu q.x");
+  FE_CHECK(q.y, 8, "zaddu q.y");
+  fe_sub<5>(dx, p.x, q.x);     // X1 - X2                          (15)
+  fe_sub<8>(dy, p.y, q.y);     // Y1 - Y2                          (33)
+  fe_normalize_weak(dy);       //                                  (1)
+  fe_sqr(C, dx);               // C = (X1 - X2)^2                  (1)
+  fe_mul(W1, p.x, C);          // W1 = X1 C                        (1)
+  fe_mul(W2, q.x, C);          // W2 = X2 C                        (1)
+  fe_sub<1>(t, W1, W2);        //                                  (3)
+  fe_mul(A1, p.y, t);          // A1 = Y1 (W1 - W2)                17 * 3 -> (1)
+  fe_sqr(r.x, dy);             // D = (Y1 - Y2)^2                  (1)
+  fe_sub<1>(r.x, r.x, W1);     //                                  (3)
+  fe_sub<1>(r.x, r.x, W2);     // X3 = D - W1 - W2                 (5)
+  fe_sub<5>(t, W1, r.x);       // W1 - X3                          (11)
+  fe_mul(r.y, dy, t);          //                                  (1)
+  fe_sub<1>(r.y, r.y, A1);     // Y3 = (Y1 - Y2)(W1 - X3) - A1     (3)
+  fe_mul(r.z, p.z, dx);        // Z3 = Z (X1 - X2)                 2 * 15 -> (1)
+  if (zr) *zr = dx;
+  p.x = W1;
+  p.y = A1;
+  p.z = r.z;
+}
+
 // Affine coordinates of a Jacobian point given 1/Z; fully normalized.
 CUDASP_HD void gej_to_ge_zinv(ge& r, const gej& a, const fe& zinv) {
   fe zi2, zi3;
