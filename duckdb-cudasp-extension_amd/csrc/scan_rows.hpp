@@ -71,7 +71,12 @@ constexpr int VB_ENTRY_X(int e) { return e * 20; }
 constexpr int VB_ENTRY_Y(int e) { return e * 20 + 10; }
 constexpr int VB_ZR(int i) { return VB_ENTRIES * 20 + i * 10; }
 constexpr int VB_CZ = VB_ENTRIES * 20 + (VB_ENTRIES - 1) * 10;
-constexpr int VB_SCRATCH_WORDS = VB_CZ + 10;
+// beta * x of every entry (the x of phi(entry)), when CUDASP_PHI_TABLE.
+#ifndef CUDASP_PHI_TABLE
+#define CUDASP_PHI_TABLE 1
+#endif
+constexpr int VB_ENTRY_XB(int e) { return VB_CZ + 10 + e * 10; }
+constexpr int VB_SCRATCH_WORDS = VB_CZ + 10 + (CUDASP_PHI_TABLE ? VB_ENTRIES * 10 : 0);
 
 CUDASP_HD int8_t uniform_digit(const int8_t* p, int i) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -91,11 +96,9 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
   fe_from_u32x8(T.x, tx);
   fe_from_u32x8(T.y, ty);
 
-#ifndef CUDASP_COZ
-#define CUDASP_COZ 1
-#endif
-#if CUDASP_COZ
   // --- odd multiples {1,3,...,15} T with one shared Z (no inversion) --------
+  fe beta;
+  fe_beta(beta);
   // Co-Z arithmetic (Meloni): DBLU gives D = 2T and T with a common Z, then
   // each ZADDU adds D to the last odd multiple and moves D to the new Z (5M+2S
   // per entry instead of a mixed addition's 8M+3S).  The entries, each with its
@@ -116,6 +119,11 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
       if (e == VB_ENTRIES - 1) {  // the only entry not rescaled below
         fe_normalize_weak(acc.x);
         fe_normalize_weak(acc.y);
+#if CUDASP_PHI_TABLE
+        fe xb;
+        fe_mul(xb, acc.x, beta);
+        scr_store(sc, VB_ENTRY_XB(e), xb);
+#endif
       }
       scr_store(sc, VB_ENTRY_X(e), acc.x);
       scr_store(sc, VB_ENTRY_Y(e), acc.y);
@@ -123,46 +131,6 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
     }
     scr_store(sc, VB_CZ, acc.z);  // Zg
   }
-#else
-  // --- odd multiples {1,3,...,15} T with one shared Z (no inversion) --------
-  // D = 2T.  On the isomorphic curve E' (scale C = D.z), D is affine (D.x, D.y)
-  // and T maps to (x C^2, y C^3); the odd multiples are built there with mixed
-  // additions, then brought to the Z of the last one through the recorded Z
-  // ratios.  With that common Z taken as 1 (curve E''), every entry is affine
-  // and the main loop uses mixed additions only; the final Z is multiplied back
-  // by C * Zg.
-  gej D;
-  gej_set_ge(D, T);
-  gej_double(D, D);
-  fe c2, c3;
-  fe_sqr(c2, D.z);
-  fe_mul(c3, c2, D.z);
-  ge dge;
-  dge.x = D.x;
-  dge.y = D.y;
-  gej acc;
-  fe_mul(acc.x, T.x, c2);
-  fe_mul(acc.y, T.y, c3);
-  fe_set_int(acc.z, 1);
-  scr_store(sc, VB_ENTRY_X(0), acc.x);
-  scr_store(sc, VB_ENTRY_Y(0), acc.y);
-  for (int e = 1; e < VB_ENTRIES; e++) {
-    fe zr;
-    gej_add_ge(acc, acc, dge, &zr);
-    if (e == VB_ENTRIES - 1) {  // the only entry not rescaled below
-      fe_normalize_weak(acc.x);
-      fe_normalize_weak(acc.y);
-    }
-    scr_store(sc, VB_ENTRY_X(e), acc.x);
-    scr_store(sc, VB_ENTRY_Y(e), acc.y);
-    scr_store(sc, VB_ZR(e - 1), zr);
-  }
-  {
-    fe cz;
-    fe_mul(cz, D.z, acc.z);  // C * Zg
-    scr_store(sc, VB_CZ, cz);
-  }
-#endif
   {
     fe ratio;
     scr_load(ratio, sc, VB_ZR(VB_ENTRIES - 2));
@@ -176,6 +144,10 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
       fe_mul(y, y, r3);
       scr_store(sc, VB_ENTRY_X(e), x);
       scr_store(sc, VB_ENTRY_Y(e), y);
+#if CUDASP_PHI_TABLE
+      fe_mul(x, x, beta);
+      scr_store(sc, VB_ENTRY_XB(e), x);
+#endif
       if (e > 0) {
         fe z;
         scr_load(z, sc, VB_ZR(e - 1));
@@ -185,51 +157,6 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
   }
 
   // --- S'' = k1*T'' + k2*phi(T'') with uniform NAF digits -------------------
-  fe beta;
-  fe_beta(beta);
-#ifndef CUDASP_PREFETCH
-#define CUDASP_PREFETCH 0
-#endif
-#if CUDASP_PREFETCH
-  gej R;
-  bool inf = true;
-  // The table entries for step i are loaded before step i's doubling, so the
-  // scratch latency overlaps the doubling's arithmetic.
-  for (int i = (int)naf_len - 1; i >= 0; --i) {
-    int d0 = uniform_digit(naf, i), d1 = uniform_digit(naf, NAF_MAX + i);
-    ge P0, P1;
-    if (d0 != 0) {
-      int e = (d0 < 0 ? -d0 : d0) >> 1;
-      scr_load(P0.x, sc, VB_ENTRY_X(e));
-      scr_load(P0.y, sc, VB_ENTRY_Y(e));
-    }
-    if (d1 != 0) {
-      int e = (d1 < 0 ? -d1 : d1) >> 1;
-      scr_load(P1.x, sc, VB_ENTRY_X(e));
-      scr_load(P1.y, sc, VB_ENTRY_Y(e));
-    }
-    if (!inf) gej_double(R, R);
-    if (d0 != 0) {
-      if (d0 < 0) ge_neg(P0, P0);
-      if (inf) {
-        gej_set_ge(R, P0);
-        inf = false;
-      } else {
-        gej_add_ge(R, R, P0);
-      }
-    }
-    if (d1 != 0) {
-      fe_mul(P1.x, P1.x, beta);
-      if (d1 < 0) ge_neg(P1, P1);
-      if (inf) {
-        gej_set_ge(R, P1);
-        inf = false;
-      } else {
-        gej_add_ge(R, R, P1);
-      }
-    }
-  }
-#else
   gej R;
   bool inf = true;
   for (int i = (int)naf_len - 1; i >= 0; --i) {
@@ -240,9 +167,13 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
       if (d != 0) {
         int e = (d < 0 ? -d : d) >> 1;
         ge P;
+#if CUDASP_PHI_TABLE
+        scr_load(P.x, sc, half ? VB_ENTRY_XB(e) : VB_ENTRY_X(e));
+#else
         scr_load(P.x, sc, VB_ENTRY_X(e));
-        scr_load(P.y, sc, VB_ENTRY_Y(e));
         if (half) fe_mul(P.x, P.x, beta);
+#endif
+        scr_load(P.y, sc, VB_ENTRY_Y(e));
         if (d < 0) ge_neg(P, P);
         if (inf) {
           gej_set_ge(R, P);
@@ -254,7 +185,6 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
     }
   }
 
-#endif
 
   // --- back to E, affine, serialize, hash -----------------------------------
   fe cz, zf, zi;
