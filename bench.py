@@ -224,6 +224,9 @@ def run_step(tab, scanners, streams, events=None):
     `events` is a list, HIP events bracket each launch on its stream (the
     per-launch kernel durations of the roofline)."""
     tab.match_count.zero_()
+    cur = torch.cuda.current_stream()
+    for st in streams:
+        st.wait_stream(cur)  # the counters are zeroed before any batch counts into them
     for b in range(tab.nb):
         s = b % len(scanners)
         st = streams[s]

@@ -61,10 +61,28 @@ constexpr int BLOCK = 256;
 #endif
 // Grid cap for the grid-stride kernels; also bounds the per-slot scratch.
 constexpr uint32_t MAX_BLOCKS = 4096;
+// Rows per thread in stage A / stage B: the rows of a thread share one field
+// inversion (Montgomery's trick, pend_invert in scan_rows.hpp).  Tuned on
+// MI355X; see DESIGN.md.
+#ifndef CUDASP_ROWS_A
+#define CUDASP_ROWS_A 4
+#endif
+#ifndef CUDASP_ROWS_B
+#define CUDASP_ROWS_B 4
+#endif
+constexpr int ROWS_A = CUDASP_ROWS_A;
+constexpr int ROWS_B = CUDASP_ROWS_B;
+static_assert(ROWS_A >= 1 && ROWS_A <= 8 && ROWS_B >= 1 && ROWS_B <= 8, "rows per thread");
+// Scratch words per slot: stage A's odd-multiple table + its pending rows;
+// stage B's label prefix products (10 L) + its pending rows.
+constexpr uint32_t VSCRATCH_WORDS = VB_SCRATCH_WORDS + 40 * ROWS_A;
+inline uint32_t lscratch_words(uint32_t label_count) { return 10 * label_count + 40 * ROWS_B; }
 }  // namespace
 
 // ----------------------------------------------------------------- kernels
 
+// Stage A: thread `slot` takes the rows g, g + G, ... (G = ceil(n / ROWS_A)) of
+// each of its groups g, so every row access stays coalesced.
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const uint32_t* __restrict__ tx,
                                                          const uint32_t* __restrict__ ty, uint32_t n,
                                                          const int8_t* __restrict__ naf, ScanConsts k,
@@ -72,20 +90,59 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
                                                          uint32_t* __restrict__ t_out) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  Scratch sc{vscr, stride, slot};
-  for (uint32_t row = slot; row < n; row += stride) {
-    uint32_t x[8], y[8], t[8];
+  const Scratch sc = make_scratch(vscr, stride, slot);
+  if constexpr (ROWS_A == 1) {
+    for (uint32_t row = slot; row < n; row += stride) {
+      uint32_t x[8], y[8], t[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      x[j] = tx[(size_t)j * n + row];
-      y[j] = ty[(size_t)j * n + row];
+      for (int w = 0; w < 8; w++) {
+        x[w] = tx[(size_t)w * n + row];
+        y[w] = ty[(size_t)w * n + row];
+      }
+      row_shared_secret(t, x, y, naf, k.naf_len, k.mid, sc);
+#pragma unroll
+      for (int w = 0; w < 8; w++) t_out[(size_t)w * n + row] = t[w];
     }
-    row_shared_secret(t, x, y, naf, k.naf_len, k.mid, sc);
+    return;
+  }
+  const uint32_t G = (n + ROWS_A - 1) / ROWS_A;
+  constexpr int PB = VB_SCRATCH_WORDS;
+  for (uint32_t g = slot; g < G; g += stride) {
+    int count = 0;
+#pragma unroll 1
+    for (int j = 0; j < ROWS_A; j++) {
+      const uint32_t row = g + (uint32_t)j * G;
+      if (row >= n) break;
+      uint32_t x[8], y[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) t_out[(size_t)j * n + row] = t[j];
+      for (int w = 0; w < 8; w++) {
+        x[w] = tx[(size_t)w * n + row];
+        y[w] = ty[(size_t)w * n + row];
+      }
+      gej R;
+      row_shared_secret_point(R, x, y, naf, k.naf_len, sc);
+      pend_store(sc, PB, j, R);
+      count = j + 1;
+    }
+    pend_invert<ROWS_A>(sc, PB, count);
+#pragma unroll 1
+    for (int j = 0; j < count; j++) {
+      const uint32_t row = g + (uint32_t)j * G;
+      gej R;
+      fe zi;
+      pend_load(R, sc, PB, j);
+      scr_load(zi, sc, PEND_ZI(PB, j));
+      uint32_t t[8];
+      row_shared_secret_finish(t, R, zi, k.mid);
+#pragma unroll
+      for (int w = 0; w < 8; w++) t_out[(size_t)w * n + row] = t[w];
+    }
   }
 }
 
+// Stage B: rows g, g + G, ... (G = ceil(n / ROWS_B)) per thread as in stage A;
+// the block walks its groups together so that the compaction ballots see
+// consecutive rows of full waves.
 template <bool VALUES>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t* __restrict__ t_in, uint32_t n,
                                                  const uint32_t* __restrict__ fb, ScanConsts k,
@@ -99,29 +156,58 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
                                                  int64_t* __restrict__ values) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  Scratch sc{lscr, stride, slot};
-  // The whole block walks the rows together so that ballots see full waves.
-  for (uint32_t row0 = blockIdx.x * blockDim.x; row0 < n; row0 += stride) {
-    const uint32_t row = row0 + threadIdx.x;
-    const bool valid = row < n;
-    bool hit = false;
-    if (valid) {
-      uint32_t t[8];
+  const Scratch sc = make_scratch(lscr, stride, slot);
+  const uint32_t G = (n + ROWS_B - 1) / ROWS_B;
+  const int PB = 10 * (int)k.label_count;
+  for (uint32_t g0 = blockIdx.x * blockDim.x; g0 < G; g0 += stride) {
+    const uint32_t g = g0 + threadIdx.x;
+    int count = 0;
+    if (ROWS_B > 1 && g < G) {
+#pragma unroll 1
+      for (int j = 0; j < ROWS_B; j++) {
+        const uint32_t row = g + (uint32_t)j * G;
+        if (row >= n) break;
+        uint32_t t[8];
 #pragma unroll
-      for (int j = 0; j < 8; j++) t[j] = t_in[(size_t)j * n + row];
-      uint32_t off = VALUES ? 0u : offs[row];
-      uint32_t len = VALUES ? 0u : lens[row];
-      hit = row_match(t, fb, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
-      if (!VALUES) flags[row] = hit ? 1 : 0;
+        for (int w = 0; w < 8; w++) t[w] = t_in[(size_t)w * n + row];
+        gej R;
+        row_match_point(R, t, fb, k);
+        pend_store(sc, PB, j, R);
+        count = j + 1;
+      }
+      pend_invert<ROWS_B>(sc, PB, count);
     }
-    if (!VALUES && match_rows != nullptr) {
-      const uint64_t m = __ballot(hit);
-      if (m) {
-        const uint32_t lane = threadIdx.x & 63u;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(match_count, (uint32_t)__popcll(m));
-        base = __shfl(base, 0);
-        if (hit) match_rows[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = row;
+#pragma unroll 1
+    for (int j = 0; j < ROWS_B; j++) {
+      const uint32_t row = g + (uint32_t)j * G;
+      bool hit = false;
+      if (ROWS_B == 1 && g < n) {
+        uint32_t t[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) t[w] = t_in[(size_t)w * n + row];
+        uint32_t off = VALUES ? 0u : offs[row];
+        uint32_t len = VALUES ? 0u : lens[row];
+        hit = row_match(t, fb, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
+        if (!VALUES) flags[row] = hit ? 1 : 0;
+      } else if (j < count) {
+        gej R;
+        fe zi;
+        pend_load(R, sc, PB, j);
+        scr_load(zi, sc, PEND_ZI(PB, j));
+        uint32_t off = VALUES ? 0u : offs[row];
+        uint32_t len = VALUES ? 0u : lens[row];
+        hit = row_match_finish(R, zi, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
+        if (!VALUES) flags[row] = hit ? 1 : 0;
+      }
+      if (!VALUES && match_rows != nullptr) {
+        const uint64_t m = __ballot(hit);
+        if (m) {
+          const uint32_t lane = threadIdx.x & 63u;
+          uint32_t base = 0;
+          if (lane == 0) base = atomicAdd(match_count, (uint32_t)__popcll(m));
+          base = __shfl(base, 0);
+          if (hit) match_rows[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = row;
+        }
       }
     }
   }
@@ -332,9 +418,9 @@ struct cudasp_scanner {
   uint32_t label_count = 0;
   uint32_t capacity = 0;
   uint32_t* d_t = nullptr;         // 8 x capacity
-  uint32_t* d_vscratch = nullptr;  // VB_SCRATCH_WORDS x slots
-  uint32_t* d_lscratch = nullptr;  // 10 L x slots
-  uint32_t slots = 0;
+  uint32_t* d_vscratch = nullptr;  // VSCRATCH_WORDS x slots_a
+  uint32_t* d_lscratch = nullptr;  // lscratch_words(L) x slots_b
+  uint32_t slots_a = 0, slots_b = 0;
   // host-path staging
   uint8_t* d_rows = nullptr;   // capacity x 64
   uint32_t* d_tx = nullptr;    // 8 x capacity
@@ -353,6 +439,17 @@ uint32_t grid_for(uint32_t n) {
   if (blocks > MAX_BLOCKS) blocks = MAX_BLOCKS;
   if (blocks == 0) blocks = 1;
   return blocks;
+}
+
+// Blocks for a batch of n rows in stage A / B (one thread per group of
+// ROWS_A / ROWS_B rows), within the scratch slots the scanner allocated.
+uint32_t grid_a(const cudasp_scanner* s, uint32_t n) {
+  uint32_t b = grid_for((n + ROWS_A - 1) / ROWS_A);
+  return b * BLOCK > s->slots_a ? s->slots_a / BLOCK : b;
+}
+uint32_t grid_b(const cudasp_scanner* s, uint32_t n) {
+  uint32_t b = grid_for((n + ROWS_B - 1) / ROWS_B);
+  return b * BLOCK > s->slots_b ? s->slots_b / BLOCK : b;
 }
 
 struct DeviceGuard {
@@ -383,17 +480,16 @@ int launch_pipeline(cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, c
                     uint32_t* match_count, int64_t* values, uint32_t* t_out, hipStream_t st) {
   if (n == 0) return CUDASP_OK;
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
-  uint32_t blocks = grid_for(n);
-  if (blocks * BLOCK > s->slots) blocks = s->slots / BLOCK;
+  const uint32_t blocks_a = grid_a(s, n), blocks_b = grid_b(s, n);
   uint32_t* t = t_out ? t_out : s->d_t;
-  hipLaunchKernelGGL(k_shared_secret, dim3(blocks), dim3(BLOCK), 0, st, tx, ty, n, s->d_naf, s->consts,
+  hipLaunchKernelGGL(k_shared_secret, dim3(blocks_a), dim3(BLOCK), 0, st, tx, ty, n, s->d_naf, s->consts,
                      s->d_vscratch, t);
   HIP_TRY(hipGetLastError());
   if (values) {
-    hipLaunchKernelGGL(k_match<true>, dim3(blocks), dim3(BLOCK), 0, st, t, n, s->d_fb, s->consts, s->d_labels,
+    hipLaunchKernelGGL(k_match<true>, dim3(blocks_b), dim3(BLOCK), 0, st, t, n, s->d_fb, s->consts, s->d_labels,
                        nullptr, nullptr, nullptr, s->d_lscratch, nullptr, nullptr, nullptr, values);
   } else {
-    hipLaunchKernelGGL(k_match<false>, dim3(blocks), dim3(BLOCK), 0, st, t, n, s->d_fb, s->consts, s->d_labels,
+    hipLaunchKernelGGL(k_match<false>, dim3(blocks_b), dim3(BLOCK), 0, st, t, n, s->d_fb, s->consts, s->d_labels,
                        outputs, offs, lens, s->d_lscratch, flags, match_rows, match_count, nullptr);
   }
   HIP_TRY(hipGetLastError());
@@ -451,7 +547,21 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
     delete s;
     return rc;
   }
-  s->slots = grid_for(max_rows) * BLOCK;
+  // One scratch slot per thread of the largest launch; each scratch buffer is
+  // kept below 4 GiB (32-bit buffer offsets, make_scratch) by capping the grid,
+  // the kernels' grid-stride loops take the remaining rows.
+  auto slots_for = [](uint32_t groups, uint64_t words_per_slot) {
+    uint64_t cap_blocks = ((1ull << 32) - 1) / (words_per_slot * 4 * BLOCK);
+    uint64_t blocks = grid_for(groups);
+    if (blocks > cap_blocks) blocks = cap_blocks ? cap_blocks : 1;
+    return (uint32_t)blocks * BLOCK;
+  };
+  s->slots_a = slots_for((max_rows + ROWS_A - 1) / ROWS_A, VSCRATCH_WORDS);
+  s->slots_b = slots_for((max_rows + ROWS_B - 1) / ROWS_B, lscratch_words(label_count));
+  if ((uint64_t)lscratch_words(label_count) * 4 * BLOCK > (1ull << 32) - 1) {
+    delete s;
+    return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys (%u)", label_count);
+  }
 #define ALLOC(ptr, bytes)                                                                          \
   do {                                                                                             \
     hipError_t e_ = hipMalloc(&(ptr), (bytes) ? (bytes) : 4);                                      \
@@ -463,8 +573,8 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
   ALLOC(s->d_naf, naf.size());
   ALLOC(s->d_labels, labels.size() * 4);
   ALLOC(s->d_t, (size_t)8 * max_rows * 4);
-  ALLOC(s->d_vscratch, (size_t)VB_SCRATCH_WORDS * s->slots * 4);
-  ALLOC(s->d_lscratch, (size_t)10 * label_count * s->slots * 4);
+  ALLOC(s->d_vscratch, (size_t)VSCRATCH_WORDS * s->slots_a * 4);
+  ALLOC(s->d_lscratch, (size_t)lscratch_words(label_count) * s->slots_b * 4);
 #undef ALLOC
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
@@ -576,9 +686,7 @@ int cudasp_stage_shared_secret_device(cudasp_scanner* s, const uint32_t* d_tweak
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
   DeviceGuard g(s->device);
   hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-  uint32_t blocks = grid_for(n);
-  if (blocks * BLOCK > s->slots) blocks = s->slots / BLOCK;
-  hipLaunchKernelGGL(k_shared_secret, dim3(blocks), dim3(BLOCK), 0, st, d_tweak_x, d_tweak_y, n, s->d_naf,
+  hipLaunchKernelGGL(k_shared_secret, dim3(grid_a(s, n)), dim3(BLOCK), 0, st, d_tweak_x, d_tweak_y, n, s->d_naf,
                      s->consts, s->d_vscratch, d_t);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
@@ -594,10 +702,8 @@ int cudasp_stage_match_device(cudasp_scanner* s, const uint32_t* d_t, const int6
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
   DeviceGuard g(s->device);
   hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-  uint32_t blocks = grid_for(n);
-  if (blocks * BLOCK > s->slots) blocks = s->slots / BLOCK;
   bool compact = d_match_rows && d_match_count;
-  hipLaunchKernelGGL(k_match<false>, dim3(blocks), dim3(BLOCK), 0, st, d_t, n, s->d_fb, s->consts, s->d_labels,
+  hipLaunchKernelGGL(k_match<false>, dim3(grid_b(s, n)), dim3(BLOCK), 0, st, d_t, n, s->d_fb, s->consts, s->d_labels,
                      d_outputs, d_output_offsets, d_output_lengths, s->d_lscratch, d_match_flags,
                      compact ? d_match_rows : nullptr, compact ? d_match_count : nullptr, nullptr);
   HIP_TRY(hipGetLastError());

@@ -54,16 +54,49 @@ struct Scratch {
   uint32_t* s;
   uint32_t stride;
   uint32_t slot;
+#if defined(__HIP_DEVICE_COMPILE__)
+  __amdgpu_buffer_rsrc_t rsrc;
+#endif
 };
+
+// Word w of a slot lives at s[w * stride + slot] (coalesced across a wave).
+// On the device every access is a buffer load/store with the column offset
+// w * stride * 4 in a scalar register and the lane offset slot * 4 in a VGPR:
+// no 64-bit per-lane address exists for the compiler to hoist out of the loops
+// and keep live (that spilled registers in stage A).  The scanner keeps each
+// scratch buffer below 4 GiB (32-bit offsets).
+CUDASP_HD Scratch make_scratch(uint32_t* s, uint32_t stride, uint32_t slot) {
+  Scratch sc;
+  sc.s = s;
+  sc.stride = stride;
+  sc.slot = slot;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // word 3 = 0x00020000: raw 32-bit buffer access on gfx9-family (CDNA) parts
+  sc.rsrc = __builtin_amdgcn_make_buffer_rsrc(s, 0, (int)0xFFFFFFFFu, 0x00020000);
+#endif
+  return sc;
+}
 
 CUDASP_HD void scr_store(const Scratch& sc, int base, const fe& a) {
 #pragma unroll
-  for (int l = 0; l < 10; l++) sc.s[(size_t)(base + l) * sc.stride + sc.slot] = a.n[l];
+  for (int l = 0; l < 10; l++) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_raw_buffer_store_b32(a.n[l], sc.rsrc, sc.slot * 4u, (uint32_t)(base + l) * sc.stride * 4u, 0);
+#else
+    sc.s[(size_t)(base + l) * sc.stride + sc.slot] = a.n[l];
+#endif
+  }
 }
 
 CUDASP_HD void scr_load(fe& a, const Scratch& sc, int base) {
 #pragma unroll
-  for (int l = 0; l < 10; l++) a.n[l] = sc.s[(size_t)(base + l) * sc.stride + sc.slot];
+  for (int l = 0; l < 10; l++) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    a.n[l] = __builtin_amdgcn_raw_buffer_load_b32(sc.rsrc, sc.slot * 4u, (uint32_t)(base + l) * sc.stride * 4u, 0);
+#else
+    a.n[l] = sc.s[(size_t)(base + l) * sc.stride + sc.slot];
+#endif
+  }
 }
 
 // Scratch layout of stage A (u32 words per row).
@@ -86,12 +119,11 @@ CUDASP_HD int8_t uniform_digit(const int8_t* p, int i) {
 #endif
 }
 
-// Stage A.  tx, ty: the tweak point, 8 LE u32 words each (normal form, the
-// reference's layout).  naf: 2 * NAF_MAX digits (GLV half 1, then half 2, signs
-// folded in).  Writes t (8 LE words of the BE digest read as an integer).
-CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const uint32_t ty[8],
-                                 const int8_t* naf, uint32_t naf_len, const uint32_t mid[8],
-                                 const Scratch& sc) {
+// Stage A, first half: S = d T as a Jacobian point of the original curve.
+// tx, ty: the tweak point, 8 LE u32 words each (normal form, the reference's
+// layout).  naf: 2 * NAF_MAX digits (GLV half 1, then half 2, signs folded in).
+CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint32_t ty[8], const int8_t* naf,
+                                       uint32_t naf_len, const Scratch& sc) {
   ge T;
   fe_from_u32x8(T.x, tx);
   fe_from_u32x8(T.y, ty);
@@ -157,7 +189,6 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
   }
 
   // --- S'' = k1*T'' + k2*phi(T'') with uniform NAF digits -------------------
-  gej R;
   bool inf = true;
   for (int i = (int)naf_len - 1; i >= 0; --i) {
     if (!inf) gej_double(R, R);
@@ -186,17 +217,95 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
   }
 
 
-  // --- back to E, affine, serialize, hash -----------------------------------
-  fe cz, zf, zi;
+  // --- back to the original curve: Z times the common table Z -------------
+  fe cz;
   scr_load(cz, sc, VB_CZ);
-  fe_mul(zf, R.z, cz);
-  fe_inv(zi, zf);
+  fe_mul(R.z, R.z, cz);
+}
+
+// Stage A, second half: from S (Jacobian) and 1/Z, serialize and hash.
+// Writes t (8 LE words of the BE digest read as an integer).
+CUDASP_HD void row_shared_secret_finish(uint32_t t_out[8], const gej& R, const fe& zi, const uint32_t mid[8]) {
   ge S;
   gej_to_ge_zinv(S, R, zi);
   uint32_t sx[8], sy[8];
   fe_to_u32x8(sx, S.x);
   fe_to_u32x8(sy, S.y);
   bip352_shared_secret_hash(t_out, mid, sx, sy[0] & 1u);
+}
+
+// Stage A for one row (one inversion per row).
+CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const uint32_t ty[8],
+                                 const int8_t* naf, uint32_t naf_len, const uint32_t mid[8],
+                                 const Scratch& sc) {
+  gej R;
+  row_shared_secret_point(R, tx, ty, naf, naf_len, sc);
+  fe zi;
+  fe_inv(zi, R.z);
+  row_shared_secret_finish(t_out, R, zi, mid);
+}
+
+// --- pending points: K rows per thread share one field inversion ------------
+// Per pending row j, 40 scratch words from `base`: X, Y, Z, then the prefix
+// product (replaced by 1/Z by pend_invert).
+CUDASP_HD int PEND_X(int base, int j) { return base + 40 * j; }
+CUDASP_HD int PEND_Y(int base, int j) { return base + 40 * j + 10; }
+CUDASP_HD int PEND_Z(int base, int j) { return base + 40 * j + 20; }
+CUDASP_HD int PEND_ZI(int base, int j) { return base + 40 * j + 30; }
+
+CUDASP_HD void pend_store(const Scratch& sc, int base, int j, const gej& R) {
+  scr_store(sc, PEND_X(base, j), R.x);
+  scr_store(sc, PEND_Y(base, j), R.y);
+  scr_store(sc, PEND_Z(base, j), R.z);
+}
+
+CUDASP_HD void pend_load(gej& R, const Scratch& sc, int base, int j) {
+  scr_load(R.x, sc, PEND_X(base, j));
+  scr_load(R.y, sc, PEND_Y(base, j));
+  scr_load(R.z, sc, PEND_Z(base, j));
+}
+
+// 1/Z of the pending rows j < count (Montgomery's trick: 3 multiplications per
+// row and one inversion).  A zero Z gets 0, exactly like fe_inv per row: if the
+// product is 0, every row falls back to its own inversion.  One fe_inv call
+// site, so the (large) inversion is inlined once.
+template <int K>
+CUDASP_HD void pend_invert(const Scratch& sc, int base, int count) {
+  fe acc, z;
+  fe_set_int(acc, 1);
+#pragma unroll 1
+  for (int j = 0; j < count; j++) {
+    scr_store(sc, PEND_ZI(base, j), acc);  // prefix product of Z_0 .. Z_(j-1)
+    scr_load(z, sc, PEND_Z(base, j));
+    fe_mul(acc, acc, z);
+  }
+  fe accn = acc;
+  fe_normalize(accn);
+  const bool zero = fe_is_zero_norm(accn);
+  const int rounds = zero ? count : 1;
+#pragma unroll 1
+  for (int r = 0; r < rounds; r++) {
+    fe x, xi;
+    if (zero)
+      scr_load(x, sc, PEND_Z(base, r));
+    else
+      x = acc;
+    fe_inv(xi, x);
+    if (zero) {
+      scr_store(sc, PEND_ZI(base, r), xi);
+    } else {
+      // xi = 1 / (Z_0 ... Z_(count-1)); peel the rows off from the last one.
+#pragma unroll 1
+      for (int j = count - 1; j >= 0; j--) {
+        fe pre, zi;
+        scr_load(pre, sc, PEND_ZI(base, j));
+        fe_mul(zi, xi, pre);
+        scr_store(sc, PEND_ZI(base, j), zi);
+        scr_load(z, sc, PEND_Z(base, j));
+        fe_mul(xi, xi, z);
+      }
+    }
+  }
 }
 
 CUDASP_HD void ge_from_words(ge& r, const uint32_t* w) {
@@ -283,12 +392,8 @@ CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb
   gej_add_ge(R, R, C);
 }
 
-// Stage B.  Returns whether the row matches; if values != nullptr, writes the
-// base value and one value per label (values[j * vstride]).
-CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k,
-                         const uint32_t* labels, const int64_t* outputs, uint32_t off, uint32_t len,
-                         const Scratch& sc, int64_t* values, uint32_t vstride) {
-  gej R;
+// Stage B, first half: F = t G + B as a Jacobian point.
+CUDASP_HD void row_match_point(gej& R, const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k) {
   fixed_base_mul(R, t_in, fb_table, k.c_odd, k.c_even);  // P0 = t*G
   // B is added on its own (not folded into c_*), so F = P0 + B is the same
   // single chord addition as the reference's even for a spend key that is not
@@ -296,8 +401,15 @@ CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const
   ge B;
   ge_from_words(B, k.spend);
   gej_add_ge(R, R, B);  // F = P0 + B (Jacobian)
-  fe zi;
-  fe_inv(zi, R.z);
+}
+
+// Stage B, second half: from F (Jacobian) and 1/Z, the compare values and the
+// match.  Returns whether the row matches; if values != nullptr, writes the
+// base value and one value per label (values[j * vstride]).  sc: the label
+// scratch (10 L words per slot).
+CUDASP_HD bool row_match_finish(const gej& R, const fe& zi, const ScanConsts& k, const uint32_t* labels,
+                                const int64_t* outputs, uint32_t off, uint32_t len, const Scratch& sc,
+                                int64_t* values, uint32_t vstride) {
   ge F;
   gej_to_ge_zinv(F, R, zi);
   int64_t v = fe_upper64(F.x);
@@ -362,6 +474,17 @@ CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const
     if (!infinity) hit = hit || outputs_contain(outputs, off, len, vj);
   }
   return hit;
+}
+
+// Stage B for one row (one inversion per row).
+CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k,
+                         const uint32_t* labels, const int64_t* outputs, uint32_t off, uint32_t len,
+                         const Scratch& sc, int64_t* values, uint32_t vstride) {
+  gej R;
+  row_match_point(R, t_in, fb_table, k);
+  fe zi;
+  fe_inv(zi, R.z);
+  return row_match_finish(R, zi, k, labels, outputs, off, len, sc, values, vstride);
 }
 
 // Fixed-base table entry (2j+1) * 2^(16 window) * G from the window base Q.

@@ -2,7 +2,10 @@
 
 Thin Python face of ``cudasp_scanner_*`` (include/cudasp_abi.h).  Device
 buffers are torch tensors (PyTorch is only the allocator / stream provider
-here); host buffers are numpy arrays.
+here); host buffers are numpy arrays.  The device-path methods run on `stream`
+or, when it is None, on torch's current stream of the scanner's device (so
+they are ordered after the torch work that produced their inputs, as any torch
+op would be); sync() waits for both that stream and the scanner's own.
 """
 import ctypes
 
@@ -66,18 +69,24 @@ class Scanner:
         self.close()
 
     # ----------------------------------------------------------- device path
+    def _stream(self, stream):
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(torch.device("cuda", self.device))
+        return ctypes.c_void_p(stream.cuda_stream)
+
     def scan_device(self, tweak_x, tweak_y, outputs, offsets, lengths, flags, match_rows=None,
                     match_count=None, stream=None):
         """Asynchronous scan of device-resident columns (torch tensors)."""
         n = int(flags.numel())
-        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        st = self._stream(stream)
         _native.check(self._lib.cudasp_scan_device(
             self._h, _ptr(tweak_x), _ptr(tweak_y), _ptr(outputs), _ptr(offsets), _ptr(lengths), n,
             _ptr(flags), _ptr(match_rows), _ptr(match_count), st))
 
     def row_values_device(self, tweak_x, tweak_y, t_out, values, stream=None):
         n = int(tweak_x.numel() // 8)
-        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        st = self._stream(stream)
         _native.check(self._lib.cudasp_row_values_device(
             self._h, _ptr(tweak_x), _ptr(tweak_y), n, _ptr(t_out), _ptr(values), st))
 
@@ -91,7 +100,7 @@ class Scanner:
                                       device=torch.device("cuda", self.device))
             t_out = self._t
         self._t_last = t_out
-        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        st = self._stream(stream)
         _native.check(self._lib.cudasp_stage_shared_secret_device(
             self._h, _ptr(tweak_x), _ptr(tweak_y), int(n), _ptr(t_out), st))
 
@@ -99,12 +108,14 @@ class Scanner:
                     t_in=None):
         """Launch only stage B on the t of the previous stage_shared_secret."""
         t_in = self._t_last if t_in is None else t_in
-        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        st = self._stream(stream)
         _native.check(self._lib.cudasp_stage_match_device(
             self._h, _ptr(t_in), _ptr(outputs), _ptr(offsets), _ptr(lengths), int(n), _ptr(flags),
             _ptr(match_rows), _ptr(match_count), st))
 
     def sync(self):
+        import torch
+        torch.cuda.current_stream(torch.device("cuda", self.device)).synchronize()
         _native.check(self._lib.cudasp_scanner_sync(self._h))
 
     # ------------------------------------------------------------- host path

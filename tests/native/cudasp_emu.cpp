@@ -167,6 +167,28 @@ int emu_midstate(uint32_t mid[8]) {
   return 0;
 }
 
+// pend_invert<4> over `count` (<= 4) field elements (32 B LE each): the
+// shared-inversion path the kernels use for several rows per thread.
+int emu_pend_invert(const uint8_t* zs, int count, uint8_t* out) {
+  std::vector<uint32_t> scr(200);
+  Scratch sc{scr.data(), 1, 0};
+  for (int j = 0; j < count; j++) {
+    gej R;
+    fe_set_int(R.x, 0);
+    fe_set_int(R.y, 0);
+    fe_from_bytes(R.z, zs + 32 * j);
+    pend_store(sc, 0, j, R);
+  }
+  pend_invert<4>(sc, 0, count);
+  for (int j = 0; j < count; j++) {
+    fe zi;
+    scr_load(zi, sc, PEND_ZI(0, j));
+    fe_normalize(zi);
+    fe_to_bytes(out + 32 * j, zi);
+  }
+  return 0;
+}
+
 int emu_fb_layout(int* bits, int* windows, uint32_t* entries) {
   *bits = FB_BITS;
   *windows = FB_WINDOWS;

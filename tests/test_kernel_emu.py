@@ -32,6 +32,7 @@ def emu():
     lib.emu_row_values.argtypes = [V, V, V, ctypes.c_uint32, V, ctypes.c_uint32, V, V, V, V, V, V]
     lib.emu_fb_entry.argtypes = [ctypes.c_uint32, ctypes.c_uint32, V]
     lib.emu_fb_layout.argtypes = [V, V, V]
+    lib.emu_pend_invert.argtypes = [ctypes.c_char_p, ctypes.c_int, V]
     lib.emu_wnaf.argtypes = [V, ctypes.c_int, V, ctypes.c_int]
     return lib
 
@@ -206,3 +207,17 @@ def test_exceptional_labels(emu):
     _, ov = oracle.scan(bytes.fromhex(k["scan_key"]), bytes.fromhex(k["spend_key"]), labels,
                         golden_io.tweak_array([k["tweak"]]), want_values=True)
     assert list(ov[0]) == list(v[0])
+
+
+def test_shared_inversion(emu):
+    """pend_invert: several rows' Z inverted with one field inversion; a zero Z
+    gets 0 (like fe_inv) without spoiling the other rows."""
+    rng = random.Random(29)
+    cases = [[rng.randrange(1, P) for _ in range(4)], [rng.randrange(1, P)], [0, rng.randrange(1, P), 5],
+             [rng.randrange(1, P), 0], [0, 0, 0, 0], [P - 1, 1, 2, 3]]
+    for zs in cases:
+        buf = b"".join(z.to_bytes(32, "little") for z in zs)
+        out = (ctypes.c_uint8 * (32 * len(zs)))()
+        emu.emu_pend_invert(buf, len(zs), out)
+        got = [int.from_bytes(bytes(out[32 * j:32 * j + 32]), "little") for j in range(len(zs))]
+        assert got == [pow(z, P - 2, P) if z % P else 0 for z in zs], zs
