@@ -160,16 +160,110 @@ int ensure_outputs_cap(HostSlot& s, size_t need) {
   return CUDASP_OK;
 }
 
-// Per-thread GPU state, created on the first row: scanner, stream, pinned and
-// device buffers for both slots (cap_rows = batch_size - 1 + one chunk).
+// GPU state of an executor thread (scanner, stream, pinned host and device
+// buffers of both slots).  It is created on the thread's first row and, when
+// the thread's local state is freed, parked in a process-wide pool instead of
+// being released: the next query's threads take it back and only rebind the
+// keys (cudasp_scanner_set_keys), so a query pays no pinned-memory or device
+// allocations once the pool is warm.
+struct GpuCtx {
+  int device = -1;
+  uint32_t cap_rows = 0;
+  cudasp_scanner* scanner = nullptr;
+  hipStream_t stream = nullptr;
+  HostSlot slots[2];
+};
+
+constexpr size_t POOL_MAX = 64;
+std::mutex g_pool_mu;
+std::vector<GpuCtx*> g_pool;
+
+void reset_slot_state(HostSlot& s) {
+  s.txid_bytes.clear();
+  s.txid_offset.clear();
+  s.txid_size.clear();
+  s.heights.clear();
+  s.rows = 0;
+  s.n_outputs = 0;
+  s.in_flight = false;
+  s.launched_rows = 0;
+}
+
+void release_ctx(GpuCtx* c) {
+  DeviceSet dg(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (HostSlot& s : c->slots) {
+    void* host[] = {s.h_tweaks, s.h_offs, s.h_lens, s.h_flags, s.h_outputs};
+    for (void* p : host)
+      if (p) (void)hipHostFree(p);
+    void* dev[] = {s.d_rows, s.d_tx, s.d_ty, s.d_offs, s.d_lens, s.d_flags, s.d_outputs};
+    for (void* p : dev)
+      if (p) (void)hipFree(p);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->scanner) cudasp_scanner_destroy(c->scanner);
+  delete c;
+}
+
+// A pooled context for (device, at least cap_rows), or nullptr.
+GpuCtx* pool_take(int device, uint32_t cap_rows) {
+  std::lock_guard<std::mutex> lock(g_pool_mu);
+  for (size_t i = 0; i < g_pool.size(); i++) {
+    GpuCtx* c = g_pool[i];
+    if (c->device == device && c->cap_rows >= cap_rows) {
+      g_pool[i] = g_pool.back();
+      g_pool.pop_back();
+      return c;
+    }
+  }
+  return nullptr;
+}
+
+void pool_put(GpuCtx* c) {
+  {
+    std::lock_guard<std::mutex> lock(g_pool_mu);
+    if (g_pool.size() < POOL_MAX) {
+      g_pool.push_back(c);
+      return;
+    }
+  }
+  release_ctx(c);
+}
+
+void ctx_to_local(GpuCtx* c, cudasp_tf_local& l) {
+  l.cap_rows = c->cap_rows;
+  l.scanner = c->scanner;
+  l.stream = c->stream;
+  for (int i = 0; i < 2; i++) {
+    l.slots[i] = std::move(c->slots[i]);
+    reset_slot_state(l.slots[i]);
+  }
+  l.cur = 0;
+  c->scanner = nullptr;
+  c->stream = nullptr;
+  delete c;
+}
+
 int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
   if (l.scanner) return CUDASP_OK;
   DeviceSet dg(l.assigned_gpu);
-  l.cap_rows = (uint32_t)(b.batch_size + CUDASP_TF_VECTOR_SIZE);
-  int rc = cudasp_scanner_create(l.assigned_gpu, (const uint8_t*)b.scan_private_key_data.data(),
-                                 (const uint8_t*)b.spend_public_key_data.data(),
-                                 (const uint8_t*)b.label_keys_flat.data(), (uint32_t)b.label_keys_data.size(),
-                                 l.cap_rows, &l.scanner);
+  const uint32_t cap_rows = (uint32_t)(b.batch_size + CUDASP_TF_VECTOR_SIZE);
+  const auto* scan = (const uint8_t*)b.scan_private_key_data.data();
+  const auto* spend = (const uint8_t*)b.spend_public_key_data.data();
+  const auto* labels = (const uint8_t*)b.label_keys_flat.data();
+  const auto nlabels = (uint32_t)b.label_keys_data.size();
+  if (GpuCtx* c = pool_take(l.assigned_gpu, cap_rows)) {
+    int rc = cudasp_scanner_set_keys(c->scanner, scan, spend, labels, nlabels);
+    if (rc != CUDASP_OK) {
+      pool_put(c);
+      return host_fail(rc, "Failed to bind scanner on GPU %d: %s", l.assigned_gpu, cudasp_last_error());
+    }
+    ctx_to_local(c, l);
+    return CUDASP_OK;
+  }
+  l.cap_rows = cap_rows;
+  int rc = cudasp_scanner_create(l.assigned_gpu, scan, spend, labels, nlabels, l.cap_rows, &l.scanner);
   if (rc != CUDASP_OK)
     return host_fail(rc, "Failed to create scanner on GPU %d: %s", l.assigned_gpu, cudasp_last_error());
   HOST_HIP(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
@@ -192,23 +286,29 @@ int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
   return CUDASP_OK;
 }
 
+// Park the thread's GPU state in the pool (after its work has drained).
 void free_local_gpu(cudasp_tf_local& l) {
   if (!l.scanner && !l.stream) return;
-  DeviceSet dg(l.assigned_gpu);
-  if (l.stream) (void)hipStreamSynchronize(l.stream);
-  for (HostSlot& s : l.slots) {
-    void* host[] = {s.h_tweaks, s.h_offs, s.h_lens, s.h_flags, s.h_outputs};
-    for (void* p : host)
-      if (p) (void)hipHostFree(p);
-    void* dev[] = {s.d_rows, s.d_tx, s.d_ty, s.d_offs, s.d_lens, s.d_flags, s.d_outputs};
-    for (void* p : dev)
-      if (p) (void)hipFree(p);
-    if (s.done) (void)hipEventDestroy(s.done);
+  GpuCtx* c = new GpuCtx();
+  c->device = l.assigned_gpu;
+  c->cap_rows = l.cap_rows;
+  c->scanner = l.scanner;
+  c->stream = l.stream;
+  for (int i = 0; i < 2; i++) {
+    c->slots[i] = std::move(l.slots[i]);
+    l.slots[i] = HostSlot();
   }
-  if (l.stream) (void)hipStreamDestroy(l.stream);
-  if (l.scanner) cudasp_scanner_destroy(l.scanner);
   l.scanner = nullptr;
   l.stream = nullptr;
+  {
+    DeviceSet dg(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+  }
+  if (!c->scanner || !c->stream) {
+    release_ctx(c);
+    return;
+  }
+  pool_put(c);
 }
 
 // AccumulateInput (src/cudasp_extension.cu:154-224), into the current slot.
@@ -421,6 +521,20 @@ void cudasp_tf_local_free(cudasp_tf_local* l) {
 }
 
 int cudasp_tf_local_gpu(const cudasp_tf_local* l) { return l ? l->assigned_gpu : -1; }
+
+void cudasp_tf_release_pool(void) {
+  std::vector<GpuCtx*> all;
+  {
+    std::lock_guard<std::mutex> lock(g_pool_mu);
+    all.swap(g_pool);
+  }
+  for (GpuCtx* c : all) release_ctx(c);
+}
+
+uint32_t cudasp_tf_pool_size(void) {
+  std::lock_guard<std::mutex> lock(g_pool_mu);
+  return (uint32_t)g_pool.size();
+}
 
 int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
                        const cudasp_tf_chunk* chunk) {

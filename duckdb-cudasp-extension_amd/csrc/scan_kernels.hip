@@ -416,6 +416,7 @@ struct cudasp_scanner {
   int8_t* d_naf = nullptr;
   uint32_t* d_labels = nullptr;
   uint32_t label_count = 0;
+  uint32_t label_cap = 0;  // label keys the label buffers are sized for
   uint32_t capacity = 0;
   uint32_t* d_t = nullptr;         // 8 x capacity
   uint32_t* d_vscratch = nullptr;  // VSCRATCH_WORDS x slots_a
@@ -539,6 +540,7 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
   s->device = device;
   s->capacity = max_rows;
   s->label_count = label_count;
+  s->label_cap = label_count;
 
   // --- device state --------------------------------------------------------
   DeviceGuard g(device);
@@ -592,6 +594,48 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
 }
 
 void cudasp_scanner_destroy(cudasp_scanner* s) { free_scanner(s); }
+
+int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32],
+                            const uint8_t spend_public_key[64], const uint8_t* label_keys, uint32_t label_count) {
+  g_last_error.clear();
+  if (!s || !scan_private_key || !spend_public_key || (label_count > 0 && !label_keys))
+    return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  ScanConsts consts;
+  std::vector<int8_t> naf;
+  std::vector<uint32_t> labels;
+  std::string err;
+  int prc = prepare_scan(scan_private_key, spend_public_key, label_keys, label_count, consts, naf, labels, err);
+  if (prc != CUDASP_OK) return set_error(prc, "%s", err.c_str());
+  if ((uint64_t)lscratch_words(label_count) * 4 * BLOCK > (1ull << 32) - 1)
+    return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys (%u)", label_count);
+  DeviceGuard g(s->device);
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  if (label_count > s->label_cap) {
+    // grow the label keys and the label scratch (same slot count when it fits)
+    uint32_t* d_labels = nullptr;
+    uint32_t* d_lscratch = nullptr;
+    uint64_t words = lscratch_words(label_count);
+    uint64_t cap_slots = ((1ull << 32) - 1) / (words * 4 * BLOCK) * BLOCK;
+    uint32_t slots_b = (uint32_t)(s->slots_b < cap_slots ? s->slots_b : cap_slots);
+    HIP_TRY(hipMalloc(&d_labels, labels.size() * 4));
+    hipError_t e = hipMalloc(&d_lscratch, (size_t)words * slots_b * 4);
+    if (e != hipSuccess) {
+      (void)hipFree(d_labels);
+      return set_error(CUDASP_ERR_HIP, "hipMalloc failed: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(s->d_labels);
+    (void)hipFree(s->d_lscratch);
+    s->d_labels = d_labels;
+    s->d_lscratch = d_lscratch;
+    s->slots_b = slots_b;
+    s->label_cap = label_count;
+  }
+  HIP_TRY(hipMemcpy(s->d_naf, naf.data(), naf.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_labels, labels.data(), labels.size() * 4, hipMemcpyHostToDevice));
+  s->consts = consts;
+  s->label_count = label_count;
+  return CUDASP_OK;
+}
 
 int cudasp_scanner_sync(cudasp_scanner* s) {
   if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");

@@ -27,6 +27,7 @@ SIGNATURES = {
     "cudasp_device_count": (_I32, []),
     "cudasp_scanner_create": (_I32, [_I32, _P, _P, _P, _U32, _U32, ctypes.POINTER(_P)]),
     "cudasp_scanner_destroy": (None, [_P]),
+    "cudasp_scanner_set_keys": (_I32, [_P, _P, _P, _P, _U32]),
     "cudasp_scan_device": (_I32, [_P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "cudasp_scan_host": (_I32, [_P, _P, _P, ctypes.c_size_t, _P, _P, _U32, _P]),
     "cudasp_row_values_device": (_I32, [_P, _P, _P, _U32, _P, _P, _P]),

@@ -51,6 +51,16 @@ class Scanner:
         self._h = h
         self._lib = lib
 
+    def set_keys(self, scan_private_key, spend_public_key, label_keys=()):
+        """Rebind to another query's keys, keeping the device buffers
+        (cudasp_scanner_set_keys)."""
+        scan = _as_bytes(scan_private_key, 32, "scan_private_key")
+        spend = _as_bytes(spend_public_key, 64, "spend_public_key")
+        labels = [_as_bytes(l, 64, "label key") for l in label_keys]
+        lab = b"".join(labels) if labels else None
+        _native.check(self._lib.cudasp_scanner_set_keys(self._h, scan, spend, lab, len(labels)))
+        self.label_count = len(labels)
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.cudasp_scanner_destroy(self._h)

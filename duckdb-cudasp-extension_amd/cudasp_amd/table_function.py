@@ -72,6 +72,8 @@ _HOST_SIGNATURES = {
     "cudasp_tf_local_init": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     "cudasp_tf_local_free": (None, [_P]),
     "cudasp_tf_local_gpu": (ctypes.c_int, [_P]),
+    "cudasp_tf_release_pool": (None, []),
+    "cudasp_tf_pool_size": (ctypes.c_uint32, []),
     "cudasp_tf_function": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Chunk)]),
     "cudasp_tf_final": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Output)]),
 }
@@ -178,6 +180,16 @@ def _make_chunk(rows):
     c = _Chunk(n, txid_ptrs, txid_size, txid_valid, height, height_valid, tweak_ptrs, tweak_size, tweak_valid,
                list_offset, list_length, list_valid, cv, cvalid)
     return keep, c
+
+
+def pool_size():
+    """GPU contexts parked in the host's cross-query pool (cudasp_tf_pool_size)."""
+    return int(_lib().cudasp_tf_pool_size())
+
+
+def release_pool():
+    """Free the host's pooled GPU contexts (cudasp_tf_release_pool)."""
+    _lib().cudasp_tf_release_pool()
 
 
 def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size=None, threads=1,

@@ -67,6 +67,13 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
                           const uint8_t* label_keys, uint32_t label_count, uint32_t max_rows,
                           cudasp_scanner** out);
 void cudasp_scanner_destroy(cudasp_scanner* s);
+/* Rebind an existing scanner (its device buffers, streams and capacity kept)
+ * to another query's keys: same validation and errors as create.  Must not be
+ * called while a batch of the scanner is in flight.  Lets a host keep scanners
+ * across queries instead of reallocating them (the reference allocates its
+ * solver state per batch, src/cudasp_gpu.cu:445-669). */
+int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32],
+                            const uint8_t spend_public_key[64], const uint8_t* label_keys, uint32_t label_count);
 
 /* Device-resident batch, asynchronous on `stream` (a hipStream_t; NULL = the
  * scanner's own stream).  Inputs: tweak x and y columns (8 x n each,

@@ -70,6 +70,13 @@ int cudasp_tf_num_gpus(const cudasp_tf_global* g);
 int cudasp_tf_local_init(cudasp_tf_global* g, cudasp_tf_local** out);
 void cudasp_tf_local_free(cudasp_tf_local* l);
 int cudasp_tf_local_gpu(const cudasp_tf_local* l);
+/* The GPU state of a freed local state (scanner, stream, pinned and device
+ * batch buffers) is kept in a process-wide pool (at most 64 entries) and
+ * reused by later queries with the same device and batch capacity.
+ * cudasp_tf_release_pool frees every pooled entry; cudasp_tf_pool_size
+ * reports how many are parked. */
+void cudasp_tf_release_pool(void);
+uint32_t cudasp_tf_pool_size(void);
 
 /* One input chunk (<= 2048 rows) of the input table, columns by position:
  * 0 txid BLOB, 1 height INTEGER, 2 tweak_key BLOB, 3 outputs BIGINT[]

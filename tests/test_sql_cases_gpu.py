@@ -86,3 +86,59 @@ def test_wrong_tweak_size_is_an_error(gpu):
     from cudasp_amd import CudaspError, cudasp_scan
     with pytest.raises(CudaspError):
         cudasp_scan([(b"t", 1, b"\x01" * 63, [1])], b"\x01" * 32, b"\x02" * 64, [])
+
+
+def test_pooled_contexts_across_queries(gpu):
+    """The host parks each thread's GPU state after a query and the next query
+    reuses it with new keys (cudasp_scanner_set_keys): results must not
+    depend on whether a context is fresh or pooled, including a change of the
+    label count between queries."""
+    from cudasp_amd import cudasp_scan, pool_size, release_pool
+    sc = golden_io.load("sql_cases.json")
+    release_pool()
+    assert pool_size() == 0
+    first = None
+    for rnd in range(2):  # round 0 starts from an empty pool, round 1 from a warm one
+        got = []
+        for q in sc["queries"]:
+            out = cudasp_scan(_table(sc, q), bytes.fromhex(q["scan_key"]), bytes.fromhex(q["spend_key"]),
+                              [bytes.fromhex(l) for l in q["label_keys"]], batch_size=q["batch_size"], threads=2)
+            got.append(sorted(out))
+            assert pool_size() > 0
+        if first is None:
+            first = got
+        assert got == first
+    release_pool()
+    assert pool_size() == 0
+
+
+def test_scanner_set_keys(gpu):
+    """A rebound scanner gives the same values as a fresh one."""
+    import numpy as np
+    import torch
+    from cudasp_amd import Scanner
+    rr = golden_io.load("random_rows.json")
+    rows = rr["rows"][:256]
+    scan, spend = bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"])
+    labels = [bytes.fromhex(l) for l in rr["label_keys"]]
+    x, y = golden_io.tweak_columns(golden_io.tweak_array([r["tweak"] for r in rows]))
+    n = len(rows)
+    dx = torch.from_numpy(x.view(np.int32).copy()).cuda()
+    dy = torch.from_numpy(y.view(np.int32).copy()).cuda()
+
+    def values(s, nl):
+        t = torch.zeros((8, n), dtype=torch.int32, device="cuda")
+        v = torch.zeros((1 + nl, n), dtype=torch.int64, device="cuda")
+        s.row_values_device(dx, dy, t, v)
+        s.sync()
+        return v.cpu().numpy()
+
+    with Scanner(scan, spend, labels, max_rows=n) as fresh:
+        want = values(fresh, len(labels))
+    other = bytes([7]) * 32
+    with Scanner(other, spend, [], max_rows=n) as s:
+        values(s, 0)
+        s.set_keys(scan, spend, labels)  # grows the label buffers
+        assert (values(s, len(labels)) == want).all()
+        s.set_keys(scan, spend, labels[:1])
+        assert (values(s, 1) == want[:2]).all()
