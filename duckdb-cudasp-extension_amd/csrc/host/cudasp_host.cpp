@@ -347,6 +347,89 @@ int accumulate(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const cudasp_tf
   return CUDASP_OK;
 }
 
+// Columnar rows [r0, r1) of `c` (Arrow layout, cudasp_tf_columns) into the
+// current slot, same row rules as accumulate().  Without validity bitmaps and
+// with 64-byte tweaks the four columns are appended with bulk copies.
+inline bool bit(const uint8_t* bm, uint64_t i) { return bm == nullptr || ((bm[i >> 3] >> (i & 7)) & 1u); }
+
+int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const cudasp_tf_columns& c, uint64_t r0,
+                       uint64_t r1) {
+  int rc = ensure_local_gpu(b, l);
+  if (rc != CUDASP_OK) return rc;
+  HostSlot& s = l.slots[l.cur];
+  const uint64_t n = r1 - r0;
+  const int32_t* txo = c.txid_offsets + c.txid_offset;
+  const int32_t* lo = c.list_offsets + c.list_offset;
+  auto tweak_ptr = [&](uint64_t i, uint32_t* size) -> const uint8_t* {
+    if (c.tweak_offsets) {
+      const int32_t* to = c.tweak_offsets + c.tweak_offset;
+      *size = (uint32_t)(to[i + 1] - to[i]);
+      return c.tweak_data + to[i];
+    }
+    *size = (uint32_t)c.tweak_fixed_width;
+    return c.tweak_data + (c.tweak_offset + i) * (uint64_t)c.tweak_fixed_width;
+  };
+  bool fast = !c.txid_validity && !c.height_validity && !c.tweak_validity && !c.list_validity && !c.child_validity;
+  if (fast && c.tweak_offsets) {
+    const int32_t* to = c.tweak_offsets + c.tweak_offset;
+    fast = (uint64_t)(to[r1] - to[r0]) == n * TWEAK_KEY_SIZE;  // every value 64 bytes
+  } else if (fast) {
+    fast = c.tweak_fixed_width == (int32_t)TWEAK_KEY_SIZE;
+  }
+  if (fast) {
+    const uint32_t r = s.rows;
+    uint32_t sz;
+    memcpy(s.h_tweaks + (size_t)r * TWEAK_KEY_SIZE, tweak_ptr(r0, &sz), n * TWEAK_KEY_SIZE);
+    s.heights.insert(s.heights.end(), c.height + c.height_offset + r0, c.height + c.height_offset + r1);
+    const size_t tbase = s.txid_bytes.size();
+    s.txid_bytes.insert(s.txid_bytes.end(), c.txid_data + txo[r0], c.txid_data + txo[r1]);
+    const uint64_t first = (uint64_t)lo[r0], total = (uint64_t)lo[r1] - first;
+    rc = ensure_outputs_cap(s, s.n_outputs + total);
+    if (rc != CUDASP_OK) return rc;
+    memcpy(s.h_outputs + s.n_outputs, c.child_values + c.child_offset + first, total * sizeof(int64_t));
+    for (uint64_t i = r0; i < r1; i++) {
+      const uint32_t row = r + (uint32_t)(i - r0);
+      s.txid_offset.push_back(tbase + (size_t)(txo[i] - txo[r0]));
+      s.txid_size.push_back((uint32_t)(txo[i + 1] - txo[i]));
+      s.h_offs[row] = (uint32_t)(s.n_outputs + ((uint64_t)lo[i] - first));
+      s.h_lens[row] = (uint32_t)(lo[i + 1] - lo[i]);
+    }
+    s.n_outputs += total;
+    s.rows = r + (uint32_t)n;
+    return CUDASP_OK;
+  }
+  for (uint64_t i = r0; i < r1; i++) {
+    if (!(bit(c.txid_validity, c.txid_offset + i) && bit(c.height_validity, c.height_offset + i) &&
+          bit(c.tweak_validity, c.tweak_offset + i)))
+      continue;
+    uint32_t tsize;
+    const uint8_t* tw = tweak_ptr(i, &tsize);
+    if (tsize != TWEAK_KEY_SIZE)
+      return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", tsize);
+    const uint32_t r = s.rows;
+    s.txid_offset.push_back(s.txid_bytes.size());
+    s.txid_size.push_back((uint32_t)(txo[i + 1] - txo[i]));
+    s.txid_bytes.insert(s.txid_bytes.end(), c.txid_data + txo[i], c.txid_data + txo[i + 1]);
+    s.heights.push_back(c.height[c.height_offset + i]);
+    memcpy(s.h_tweaks + (size_t)r * TWEAK_KEY_SIZE, tw, TWEAK_KEY_SIZE);
+    s.h_offs[r] = (uint32_t)s.n_outputs;
+    uint32_t len = 0;
+    if (bit(c.list_validity, c.list_offset + i)) {
+      rc = ensure_outputs_cap(s, s.n_outputs + (uint64_t)(lo[i + 1] - lo[i]));
+      if (rc != CUDASP_OK) return rc;
+      for (int64_t k = lo[i]; k < lo[i + 1]; k++) {
+        if (bit(c.child_validity, c.child_offset + (uint64_t)k)) {
+          s.h_outputs[s.n_outputs++] = c.child_values[c.child_offset + (uint64_t)k];
+          len++;
+        }
+      }
+    }
+    s.h_lens[r] = len;
+    s.rows = r + 1;
+  }
+  return CUDASP_OK;
+}
+
 // Collect a finished batch's matches into the global list (ProcessBatch
 // :378-392) and reset the slot.
 int harvest(cudasp_tf_global& g, cudasp_tf_local& l, HostSlot& s) {
@@ -543,6 +626,26 @@ int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp
     int rc = accumulate(*b, *l, *chunk);
     if (rc != CUDASP_OK) return rc;
     // ShouldProcessBatch: accumulated >= batch_size (:416-418).
+    if (l->rows() >= b->batch_size) {
+      rc = launch_batch(*b, *g, *l);
+      if (rc != CUDASP_OK) return rc;
+    }
+  }
+  return CUDASP_TF_NEED_MORE_INPUT;
+}
+
+int cudasp_tf_function_columns(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
+                               const cudasp_tf_columns* cols) {
+  if (!b || !g || !l || !cols) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
+  const cudasp_tf_columns& c = *cols;
+  if (c.count > 0 && (!c.txid_offsets || !c.txid_data || !c.height || !c.tweak_data || !c.list_offsets ||
+                      (!c.tweak_offsets && c.tweak_fixed_width <= 0)))
+    return host_fail(CUDASP_ERR_INVALID_ARG, "missing column buffer");
+  // DuckDB-sized pieces, with the same trigger as cudasp_tf_function.
+  for (uint64_t r0 = 0; r0 < c.count; r0 += CUDASP_TF_VECTOR_SIZE) {
+    const uint64_t r1 = r0 + CUDASP_TF_VECTOR_SIZE < c.count ? r0 + CUDASP_TF_VECTOR_SIZE : c.count;
+    int rc = accumulate_columns(*b, *l, c, r0, r1);
+    if (rc != CUDASP_OK) return rc;
     if (l->rows() >= b->batch_size) {
       rc = launch_batch(*b, *g, *l);
       if (rc != CUDASP_OK) return rc;

@@ -59,6 +59,30 @@ class _Output(ctypes.Structure):
     ]
 
 
+class _Columns(ctypes.Structure):
+    _fields_ = [
+        ("count", ctypes.c_uint64),
+        ("txid_offsets", ctypes.c_void_p),
+        ("txid_data", ctypes.c_void_p),
+        ("txid_validity", ctypes.c_void_p),
+        ("txid_offset", ctypes.c_uint64),
+        ("height", ctypes.c_void_p),
+        ("height_validity", ctypes.c_void_p),
+        ("height_offset", ctypes.c_uint64),
+        ("tweak_offsets", ctypes.c_void_p),
+        ("tweak_data", ctypes.c_void_p),
+        ("tweak_validity", ctypes.c_void_p),
+        ("tweak_offset", ctypes.c_uint64),
+        ("tweak_fixed_width", ctypes.c_int32),
+        ("list_offsets", ctypes.c_void_p),
+        ("list_validity", ctypes.c_void_p),
+        ("list_offset", ctypes.c_uint64),
+        ("child_values", ctypes.c_void_p),
+        ("child_validity", ctypes.c_void_p),
+        ("child_offset", ctypes.c_uint64),
+    ]
+
+
 _P = ctypes.c_void_p
 _HOST_SIGNATURES = {
     "cudasp_tf_bind": (ctypes.c_int, [ctypes.c_uint32, _BlobArg, _BlobArg, ctypes.c_int, ctypes.POINTER(_BlobArg),
@@ -76,6 +100,7 @@ _HOST_SIGNATURES = {
     "cudasp_tf_pool_size": (ctypes.c_uint32, []),
     "cudasp_tf_function": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Chunk)]),
     "cudasp_tf_final": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Output)]),
+    "cudasp_tf_function_columns": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Columns)]),
 }
 
 _host = None
@@ -244,6 +269,131 @@ def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size
         if errors:
             raise errors[0]
         return results
+    finally:
+        for l in locals_:
+            lib.cudasp_tf_local_free(l)
+        lib.cudasp_tf_global_free(g)
+
+
+# ------------------------------------------------------------ Arrow columns
+def _addr(buf):
+    return None if buf is None else buf.address
+
+
+def _arrow_pieces(data, piece_rows):
+    """Record batches of `data` (pa.Table, pa.RecordBatch or an iterable of
+    record batches), columns cast to the layouts cudasp_tf_columns takes,
+    sliced into pieces of at most piece_rows rows."""
+    import pyarrow as pa
+    if isinstance(data, pa.Table):
+        batches = data.to_batches()
+    elif isinstance(data, pa.RecordBatch):
+        batches = [data]
+    else:
+        batches = list(data)
+    out = []
+    for rb in batches:
+        if rb.num_columns < 4:
+            raise InvalidInputException("cudasp_scan input needs 4 columns (txid, height, tweak_key, outputs)")
+        txid, height, tweak, outs = (rb.column(i) for i in range(4))
+        if not pa.types.is_binary(txid.type):
+            txid = txid.cast(pa.binary())
+        if not pa.types.is_int32(height.type):
+            height = height.cast(pa.int32())
+        if not (pa.types.is_binary(tweak.type) or pa.types.is_fixed_size_binary(tweak.type)):
+            tweak = tweak.cast(pa.binary())
+        if not (pa.types.is_list(outs.type) and pa.types.is_int64(outs.type.value_type)):
+            outs = outs.cast(pa.list_(pa.int64()))
+        for start in range(0, len(txid), piece_rows):
+            m = min(piece_rows, len(txid) - start)
+            out.append((txid.slice(start, m), height.slice(start, m), tweak.slice(start, m), outs.slice(start, m)))
+    return out
+
+
+def _columns(txid, height, tweak, outs):
+    """cudasp_tf_columns over pyarrow arrays (buffers stay owned by the arrays)."""
+    import pyarrow as pa
+    c = _Columns()
+    c.count = len(txid)
+    tb = txid.buffers()
+    c.txid_validity, c.txid_offsets, c.txid_data = _addr(tb[0]) if txid.null_count else None, _addr(tb[1]), _addr(tb[2])
+    c.txid_offset = txid.offset
+    hb = height.buffers()
+    c.height_validity, c.height = _addr(hb[0]) if height.null_count else None, _addr(hb[1])
+    c.height_offset = height.offset
+    wb = tweak.buffers()
+    c.tweak_validity = _addr(wb[0]) if tweak.null_count else None
+    if pa.types.is_fixed_size_binary(tweak.type):
+        c.tweak_offsets, c.tweak_data, c.tweak_fixed_width = None, _addr(wb[1]), tweak.type.byte_width
+    else:
+        c.tweak_offsets, c.tweak_data, c.tweak_fixed_width = _addr(wb[1]), _addr(wb[2]), 0
+    c.tweak_offset = tweak.offset
+    lb = outs.buffers()
+    c.list_validity, c.list_offsets = _addr(lb[0]) if outs.null_count else None, _addr(lb[1])
+    c.list_offset = outs.offset
+    child = outs.values
+    cb = child.buffers()
+    c.child_validity, c.child_values = _addr(cb[0]) if child.null_count else None, _addr(cb[1])
+    c.child_offset = child.offset
+    return c
+
+
+def cudasp_scan_arrow(data, scan_private_key, spend_public_key, label_keys, batch_size=None, threads=1,
+                      piece_rows=65536):
+    """cudasp_scan over Arrow data (a pyarrow Table / RecordBatch / iterable of
+    record batches, e.g. pyarrow.parquet.read_table(...) or DuckDB's
+    .arrow()), with the same four columns by position.  Rows reach the
+    batch buffers through cudasp_tf_function_columns (bulk copies from the
+    Arrow buffers); the semantics and batches equal cudasp_scan's.  Returns a
+    pyarrow Table (txid binary, height int32, tweak_key binary) in unspecified
+    row order, like the reference."""
+    import pyarrow as pa
+    lib = _lib()
+    bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size)
+    pieces = _arrow_pieces(data, piece_rows)
+    g = _P()
+    _native.check(lib.cudasp_tf_init(bound._h, ctypes.byref(g)))
+    locals_ = []
+    try:
+        for _ in range(threads):
+            l = _P()
+            _native.check(lib.cudasp_tf_local_init(g, ctypes.byref(l)))
+            locals_.append(l)
+        errors = []
+        results = []
+        res_lock = threading.Lock()
+
+        def worker(t):
+            try:
+                for pi in range(t, len(pieces), threads):
+                    cols = _columns(*pieces[pi])
+                    rc = lib.cudasp_tf_function_columns(bound._h, g, locals_[t], ctypes.byref(cols))
+                    if rc < 0:
+                        _native.check(rc)
+                out = _Output()
+                while True:
+                    rc = lib.cudasp_tf_final(bound._h, g, locals_[t], ctypes.byref(out))
+                    if rc < 0:
+                        _native.check(rc)
+                    got = [(ctypes.string_at(out.txid_data[i], out.txid_size[i]), out.height[i],
+                            ctypes.string_at(out.tweak_data[i], out.tweak_size[i])) for i in range(out.count)]
+                    with res_lock:
+                        results.extend(got)
+                    if rc != TF_HAVE_MORE_OUTPUT:
+                        break
+            except Exception as e:  # surfaced after join
+                errors.append(e)
+
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        if errors:
+            raise errors[0]
+        return pa.table({"txid": pa.array([r[0] for r in results], pa.binary()),
+                         "height": pa.array([r[1] for r in results], pa.int32()),
+                         "tweak_key": pa.array([r[2] for r in results], pa.binary())})
     finally:
         for l in locals_:
             lib.cudasp_tf_local_free(l)

@@ -106,6 +106,47 @@ typedef struct {
 int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
                        const cudasp_tf_chunk* chunk);
 
+/* Columnar input: a run of rows of the same four
+ * columns as Arrow arrays, so Parquet/Arrow data (or DuckDB's Arrow export)
+ * feeds the batch buffers with bulk copies instead of per-row pointers.
+ * Buffers follow the Arrow C data layout; each column carries its Arrow array
+ * offset (element offset into its buffers); validity bitmaps are LSB-first and
+ * may be NULL (= all valid).
+ *   txid:    binary (int32 offsets[count+1], data)
+ *   height:  int32 values
+ *   tweak:   binary (int32 offsets) or, when tweak_offsets is NULL,
+ *            fixed_size_binary of tweak_fixed_width bytes
+ *   outputs: list<int64> (int32 offsets[count+1] into the child array, which
+ *            has its own offset and validity)
+ * Row semantics are those of cudasp_tf_function (NULL txid/height/tweak rows
+ * skipped, tweak length 64 enforced, NULL list = no outputs, NULL elements
+ * dropped); rows are consumed in 2048-row pieces with the same batch trigger,
+ * so batches are identical to feeding the same rows as DuckDB chunks. */
+typedef struct {
+  uint64_t count;
+  const int32_t* txid_offsets;
+  const uint8_t* txid_data;
+  const uint8_t* txid_validity;
+  uint64_t txid_offset;
+  const int32_t* height;
+  const uint8_t* height_validity;
+  uint64_t height_offset;
+  const int32_t* tweak_offsets;
+  const uint8_t* tweak_data;
+  const uint8_t* tweak_validity;
+  uint64_t tweak_offset;
+  int32_t tweak_fixed_width;
+  const int32_t* list_offsets;
+  const uint8_t* list_validity;
+  uint64_t list_offset;
+  const int64_t* child_values;
+  const uint8_t* child_validity;
+  uint64_t child_offset;
+} cudasp_tf_columns;
+
+int cudasp_tf_function_columns(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
+                               const cudasp_tf_columns* cols);
+
 /* One output chunk: up to 2048 matching rows (txid, height, tweak_key).  The
  * pointers stay valid until the global state is freed. */
 typedef struct {

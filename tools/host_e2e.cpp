@@ -64,6 +64,9 @@ int main(int argc, char** argv) {
   int64_t batch = argc > 3 ? atoll(argv[3]) : 300000;
   int nlabels = argc > 4 ? atoi(argv[4]) : 0;
   int k = argc > 5 ? atoi(argv[5]) : 2;
+  // "rows": DuckDB-style 2048-row chunks of per-row pointers (cudasp_tf_function);
+  // "columns": Arrow-layout column runs (cudasp_tf_function_columns).
+  const bool columnar = argc > 6 && strcmp(argv[6], "columns") == 0;
   uint8_t scan[32], spend[64], label[64];
   hex2bin(SCAN_HEX, scan);
   hex2bin(SPEND_HEX, spend);
@@ -78,6 +81,12 @@ int main(int argc, char** argv) {
   std::vector<int32_t> heights(rows);
   std::vector<int64_t> outputs(rows * (uint64_t)k);
   std::vector<uint64_t> list_off(rows), list_len(rows, (uint64_t)k);
+  // Arrow-layout offsets for the columnar mode (int32, rows + 1 entries)
+  std::vector<int32_t> txid_offsets(rows + 1), list_off32(rows + 1);
+  for (uint64_t i = 0; i <= rows; i++) {
+    txid_offsets[i] = (int32_t)(i * 32);
+    list_off32[i] = (int32_t)(i * k);
+  }
   uint8_t s0[32];
   synth_s0(s0);
   const uint32_t chunk = 1u << 22;
@@ -158,7 +167,38 @@ int main(int argc, char** argv) {
     std::atomic<uint64_t> emitted{0};
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
-    for (int t = 0; t < threads; t++) {
+    for (int t = 0; t < threads && columnar; t++) {
+      th.emplace_back([&, t]() {
+        const uint64_t piece = 65536;
+        for (;;) {
+          uint64_t c0 = next.fetch_add(piece);
+          if (c0 >= rows) break;
+          cudasp_tf_columns c{};
+          c.count = std::min<uint64_t>(piece, rows - c0);
+          c.txid_offsets = txid_offsets.data();
+          c.txid_data = txids.data();
+          c.txid_offset = c0;
+          c.height = heights.data();
+          c.height_offset = c0;
+          c.tweak_data = tweaks.data();
+          c.tweak_fixed_width = 64;
+          c.tweak_offset = c0;
+          c.list_offsets = list_off32.data();
+          c.list_offset = c0;
+          c.child_values = outputs.data();
+          CK(cudasp_tf_function_columns(bd, gs, ls[t], &c));
+        }
+        cudasp_tf_output* out = new cudasp_tf_output;
+        for (;;) {
+          int rc = cudasp_tf_final(bd, gs, ls[t], out);
+          CK(rc);
+          emitted += out->count;
+          if (rc != CUDASP_TF_HAVE_MORE_OUTPUT) break;
+        }
+        delete out;
+      });
+    }
+    for (int t = 0; t < threads && !columnar; t++) {
       th.emplace_back([&, t]() {
         std::vector<const uint8_t*> txp(CUDASP_TF_VECTOR_SIZE), twp(CUDASP_TF_VECTOR_SIZE);
         std::vector<uint32_t> txs(CUDASP_TF_VECTOR_SIZE, 32), tws(CUDASP_TF_VECTOR_SIZE, 64);
@@ -207,11 +247,12 @@ int main(int argc, char** argv) {
   double secs;
   uint64_t found;
   run(&secs, &found);
-  printf("{\"what\": \"table-function host end-to-end (host memory -> matches, PCIe-inclusive)\", "
+  printf("{\"what\": \"table-function host end-to-end (host memory -> matches, PCIe-inclusive)\", \"input\": \"%s\", "
          "\"rows\": %llu, \"threads\": %d, \"batch_size\": %lld, \"labels\": %d, \"outputs_per_row\": %d, "
          "\"seconds\": %.4f, \"tx_per_s\": %.1f, \"matches\": %llu, \"planted\": %llu, \"warmup_seconds\": %.3f, "
          "\"generate_seconds\": %.2f, \"devices\": %d}\n",
-         (unsigned long long)rows, threads, (long long)batch, nlabels, k, secs, rows / secs,
+         columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)rows, threads, (long long)batch, nlabels,
+         k, secs, rows / secs,
          (unsigned long long)found, (unsigned long long)planted, warm_s, gen_s, cudasp_device_count());
   return found == planted ? 0 : 2;
 }
