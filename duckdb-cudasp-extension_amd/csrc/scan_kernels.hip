@@ -75,8 +75,8 @@ constexpr int ROWS_B = CUDASP_ROWS_B;
 static_assert(ROWS_A >= 1 && ROWS_A <= 8 && ROWS_B >= 1 && ROWS_B <= 8, "rows per thread");
 // Scratch words per slot: stage A's odd-multiple table + its pending rows;
 // stage B's label prefix products (10 L) + its pending rows.
-constexpr uint32_t VSCRATCH_WORDS = VB_SCRATCH_WORDS + 40 * ROWS_A;
-inline uint32_t lscratch_words(uint32_t label_count) { return 10 * label_count + 40 * ROWS_B; }
+constexpr uint32_t VSCRATCH_WORDS = VB_SCRATCH_WORDS + PEND_WORDS * ROWS_A;
+inline uint32_t lscratch_words(uint32_t label_count) { return FW * label_count + PEND_WORDS * ROWS_B; }
 }  // namespace
 
 // ----------------------------------------------------------------- kernels
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
   const uint32_t stride = gridDim.x * blockDim.x;
   const Scratch sc = make_scratch(lscr, stride, slot);
   const uint32_t G = (n + ROWS_B - 1) / ROWS_B;
-  const int PB = 10 * (int)k.label_count;
+  const int PB = FW * (int)k.label_count;
   for (uint32_t g0 = blockIdx.x * blockDim.x; g0 < G; g0 += stride) {
     const uint32_t g = g0 + threadIdx.x;
     int count = 0;
@@ -360,16 +360,16 @@ __global__ __launch_bounds__(BLOCK) void k_debug_field_ops(int op, const uint32_
   if (i >= n) return;
   fe x, y, r;
 #pragma unroll
-  for (int k = 0; k < 10; k++) {
-    x.n[k] = a[(size_t)i * 10 + k];
-    y.n[k] = b[(size_t)i * 10 + k];
+  for (int k = 0; k < FE_LIMBS; k++) {
+    x.n[k] = a[(size_t)i * FE_LIMBS + k];
+    y.n[k] = b[(size_t)i * FE_LIMBS + k];
   }
   if (op == 0)
     fe_mul(r, x, y);
   else
     fe_sqr(r, x);
 #pragma unroll
-  for (int k = 0; k < 10; k++) out[(size_t)i * 10 + k] = r.n[k];
+  for (int k = 0; k < FE_LIMBS; k++) out[(size_t)i * FE_LIMBS + k] = r.n[k];
 }
 
 // ------------------------------------------------------------- host helpers
@@ -803,6 +803,17 @@ int cudasp_synth_output_values(uint64_t seed, uint64_t first_index, uint32_t n, 
   hipLaunchKernelGGL(k_synth_output_values, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, seed,
                      first_index, n, d_offsets, d_lengths, d_outputs);
   HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+int cudasp_field_layout(int* limbs, int* bits, int* mul_mag_max, int* sqr_mag_max, int* limb_mag_max) {
+  if (!limbs || !bits || !mul_mag_max || !sqr_mag_max || !limb_mag_max)
+    return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  *limbs = FE_LIMBS;
+  *bits = FE_BITS;
+  *mul_mag_max = (int)MUL_MAG_MAX;
+  *sqr_mag_max = (int)SQR_MAG_MAX;
+  *limb_mag_max = (int)LIMB_MAG_MAX;
   return CUDASP_OK;
 }
 

@@ -79,7 +79,7 @@ CUDASP_HD Scratch make_scratch(uint32_t* s, uint32_t stride, uint32_t slot) {
 
 CUDASP_HD void scr_store(const Scratch& sc, int base, const fe& a) {
 #pragma unroll
-  for (int l = 0; l < 10; l++) {
+  for (int l = 0; l < FE_LIMBS; l++) {
 #if defined(__HIP_DEVICE_COMPILE__)
     __builtin_amdgcn_raw_buffer_store_b32(a.n[l], sc.rsrc, sc.slot * 4u, (uint32_t)(base + l) * sc.stride * 4u, 0);
 #else
@@ -90,7 +90,7 @@ CUDASP_HD void scr_store(const Scratch& sc, int base, const fe& a) {
 
 CUDASP_HD void scr_load(fe& a, const Scratch& sc, int base) {
 #pragma unroll
-  for (int l = 0; l < 10; l++) {
+  for (int l = 0; l < FE_LIMBS; l++) {
 #if defined(__HIP_DEVICE_COMPILE__)
     a.n[l] = __builtin_amdgcn_raw_buffer_load_b32(sc.rsrc, sc.slot * 4u, (uint32_t)(base + l) * sc.stride * 4u, 0);
 #else
@@ -100,16 +100,18 @@ CUDASP_HD void scr_load(fe& a, const Scratch& sc, int base) {
 }
 
 // Scratch layout of stage A (u32 words per row).
-constexpr int VB_ENTRY_X(int e) { return e * 20; }
-constexpr int VB_ENTRY_Y(int e) { return e * 20 + 10; }
-constexpr int VB_ZR(int i) { return VB_ENTRIES * 20 + i * 10; }
-constexpr int VB_CZ = VB_ENTRIES * 20 + (VB_ENTRIES - 1) * 10;
+// (FE_LIMBS words per field element)
+constexpr int FW = FE_LIMBS;
+constexpr int VB_ENTRY_X(int e) { return e * 2 * FW; }
+constexpr int VB_ENTRY_Y(int e) { return e * 2 * FW + FW; }
+constexpr int VB_ZR(int i) { return VB_ENTRIES * 2 * FW + i * FW; }
+constexpr int VB_CZ = VB_ENTRIES * 2 * FW + (VB_ENTRIES - 1) * FW;
 // beta * x of every entry (the x of phi(entry)), when CUDASP_PHI_TABLE.
 #ifndef CUDASP_PHI_TABLE
 #define CUDASP_PHI_TABLE 1
 #endif
-constexpr int VB_ENTRY_XB(int e) { return VB_CZ + 10 + e * 10; }
-constexpr int VB_SCRATCH_WORDS = VB_CZ + 10 + (CUDASP_PHI_TABLE ? VB_ENTRIES * 10 : 0);
+constexpr int VB_ENTRY_XB(int e) { return VB_CZ + FW + e * FW; }
+constexpr int VB_SCRATCH_WORDS = VB_CZ + FW + (CUDASP_PHI_TABLE ? VB_ENTRIES * FW : 0);
 
 CUDASP_HD int8_t uniform_digit(const int8_t* p, int i) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -246,12 +248,13 @@ CUDASP_HD void row_shared_secret(uint32_t t_out[8], const uint32_t tx[8], const 
 }
 
 // --- pending points: K rows per thread share one field inversion ------------
-// Per pending row j, 40 scratch words from `base`: X, Y, Z, then the prefix
-// product (replaced by 1/Z by pend_invert).
-CUDASP_HD int PEND_X(int base, int j) { return base + 40 * j; }
-CUDASP_HD int PEND_Y(int base, int j) { return base + 40 * j + 10; }
-CUDASP_HD int PEND_Z(int base, int j) { return base + 40 * j + 20; }
-CUDASP_HD int PEND_ZI(int base, int j) { return base + 40 * j + 30; }
+// Per pending row j, PEND_WORDS scratch words from `base`: X, Y, Z, then the
+// prefix product (replaced by 1/Z by pend_invert).
+constexpr int PEND_WORDS = 4 * FW;
+CUDASP_HD int PEND_X(int base, int j) { return base + PEND_WORDS * j; }
+CUDASP_HD int PEND_Y(int base, int j) { return base + PEND_WORDS * j + FW; }
+CUDASP_HD int PEND_Z(int base, int j) { return base + PEND_WORDS * j + 2 * FW; }
+CUDASP_HD int PEND_ZI(int base, int j) { return base + PEND_WORDS * j + 3 * FW; }
 
 CUDASP_HD void pend_store(const Scratch& sc, int base, int j, const gej& R) {
   scr_store(sc, PEND_X(base, j), R.x);
@@ -437,7 +440,7 @@ CUDASP_HD bool row_match_finish(const gej& R, const fe& zi, const ScanConsts& k,
     } else {
       fe_set_int(d, 1);
     }
-    scr_store(sc, (int)j * 10, accp);
+    scr_store(sc, (int)j * FW, accp);
     fe_mul(accp, accp, d);
   }
   fe inv;
@@ -460,7 +463,7 @@ CUDASP_HD bool row_match_finish(const gej& R, const fe& zi, const ScanConsts& k,
       fe_set_int(num, 0);
       infinity = true;
     }
-    scr_load(pre, sc, j * 10);
+    scr_load(pre, sc, j * FW);
     fe_mul(dinv, inv, pre);
     fe_mul(inv, inv, d);
     fe lam, x3;

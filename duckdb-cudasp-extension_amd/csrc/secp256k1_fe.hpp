@@ -25,7 +25,36 @@
 
 #define CUDASP_HD __host__ __device__ __forceinline__
 
+// Limb layout: 9 x 29 bits (secp256k1_fe29.hpp, default: 118 / 82 mads per
+// mul / sqr) or 10 x 26 bits (this file: 143 / 98, more headroom).  A/B on
+// MI355X: profiles/r01_stage_ab_fe_layouts.txt.
+#ifndef CUDASP_FE_LIMBS
+#define CUDASP_FE_LIMBS 9
+#endif
+
 namespace cudasp {
+// Small constants as opaque scalar registers on the device, so that the
+// compiler keeps "x * 0x400" as one v_mad_u64_u32 instead of rewriting it as a
+// 64-bit shift + add (two VOP3 instructions).
+CUDASP_HD uint32_t opaque_const(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("s_mov_b32 %0, %1" : "=s"(r) : "i"(v));
+  return r;
+#else
+  return v;
+#endif
+}
+
+}  // namespace cudasp
+
+#if CUDASP_FE_LIMBS == 9
+#include "secp256k1_fe29.hpp"
+#elif CUDASP_FE_LIMBS == 10
+namespace cudasp {
+
+constexpr int FE_LIMBS = 10;
+constexpr int FE_BITS = 26;
 
 struct fe {
   uint32_t n[10];
@@ -40,6 +69,8 @@ constexpr uint32_t R1 = 0x400u;
 constexpr uint32_t F0 = 0x3D1u;
 constexpr uint32_t F1 = 0x40u;
 constexpr uint32_t MUL_MAG_MAX = 400;
+constexpr uint32_t SQR_MAG_MAX = 20;
+constexpr uint32_t LIMB_MAG_MAX = 31;
 
 #ifdef CUDASP_FE_CHECK
 // Host-emulation builds verify every magnitude precondition.
@@ -75,12 +106,8 @@ CUDASP_HD void fe_check_mul(const fe& a, const fe& b, const char* what) {
 #define FE_CHECK(a, m, what) ((void)0)
 #define FE_CHECK_MUL(a, b, what) ((void)0)
 #endif
-
-CUDASP_HD void fe_set_int(fe& r, uint32_t v) {
-  r.n[0] = v;
-#pragma unroll
-  for (int i = 1; i < 10; i++) r.n[i] = 0;
-}
+#define FE_CHECK_SQR(a, what) FE_CHECK_MUL(a, a, what)
+#define FE_CHECK_SUM(a, what) ((void)0)
 
 // 8 little-endian u32 words (the reference's limb layout,
 // src/cudasp_extension.cu:59-85) -> 10x26.  Input must be < 2^256.
@@ -190,33 +217,6 @@ CUDASP_HD void fe_normalize(fe& r) {
     r.n[4] = t4 & M26; r.n[5] = t5 & M26; r.n[6] = t6 & M26; r.n[7] = t7 & M26;
     r.n[8] = t8 & M26; r.n[9] = t9 & M22;
   }
-}
-
-CUDASP_HD bool fe_is_zero_norm(const fe& a) {
-  uint32_t z = 0;
-#pragma unroll
-  for (int i = 0; i < 10; i++) z |= a.n[i];
-  return z == 0;
-}
-
-CUDASP_HD bool fe_equal_norm(const fe& a, const fe& b) {
-  uint32_t z = 0;
-#pragma unroll
-  for (int i = 0; i < 10; i++) z |= a.n[i] ^ b.n[i];
-  return z == 0;
-}
-
-// Small constants as opaque scalar registers on the device, so that the
-// compiler keeps "x * 0x400" as one v_mad_u64_u32 instead of rewriting it as a
-// 64-bit shift + add (two VOP3 instructions).
-CUDASP_HD uint32_t opaque_const(uint32_t v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t r;
-  asm("s_mov_b32 %0, %1" : "=s"(r) : "i"(v));
-  return r;
-#else
-  return v;
-#endif
 }
 
 // Field multiply/square code shapes (A/B-tested on MI355X, stage A of 300k rows,
@@ -543,6 +543,34 @@ CUDASP_HD void fe_sqr(fe& r, const fe& a) {
 
 #endif
 
+}  // namespace cudasp
+#else
+#error "CUDASP_FE_LIMBS must be 9 or 10"
+#endif
+
+// ----------------------------------------------- layout-independent helpers
+namespace cudasp {
+
+CUDASP_HD void fe_set_int(fe& r, uint32_t v) {
+  r.n[0] = v;
+#pragma unroll
+  for (int i = 1; i < FE_LIMBS; i++) r.n[i] = 0;
+}
+
+CUDASP_HD bool fe_is_zero_norm(const fe& a) {
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) z |= a.n[i];
+  return z == 0;
+}
+
+CUDASP_HD bool fe_equal_norm(const fe& a, const fe& b) {
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) z |= a.n[i] ^ b.n[i];
+  return z == 0;
+}
+
 CUDASP_HD void fe_sqr_n(fe& r, const fe& a, int n) {
   fe_sqr(r, a);
   for (int i = 1; i < n; i++) fe_sqr(r, r);
@@ -589,7 +617,7 @@ CUDASP_HD void fe_inv_fermat(fe& r, const fe& a) {
 // Conditional select: r = c ? a : b (per lane).
 CUDASP_HD void fe_cmov(fe& r, const fe& a, bool c) {
 #pragma unroll
-  for (int i = 0; i < 10; i++) r.n[i] = c ? a.n[i] : r.n[i];
+  for (int i = 0; i < FE_LIMBS; i++) r.n[i] = c ? a.n[i] : r.n[i];
 }
 
 }  // namespace cudasp

@@ -17,6 +17,9 @@ namespace cudasp {
 CUDASP_HD void fe_inv(fe& r, const fe& a) { fe_inv_safegcd(r, a); }
 }  // namespace cudasp
 
+#if CUDASP_FE_LIMBS == 9
+#include "secp256k1_group29.hpp"
+#else
 namespace cudasp {
 
 struct ge {
@@ -177,3 +180,4 @@ CUDASP_HD void ge_neg(ge& r, const ge& a) {
 }
 
 }  // namespace cudasp
+#endif

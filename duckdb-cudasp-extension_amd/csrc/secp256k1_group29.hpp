@@ -1,0 +1,170 @@
+// secp256k1 group operations for the 9 x 29-bit field layout
+// (CUDASP_FE_LIMBS=9; included by secp256k1_group.hpp instead of the 10 x 26
+// formulas).  Same functions and meaning; the formulas are chosen and the
+// weak normalizations placed for the tight magnitude budget of
+// secp256k1_fe29.hpp (mul: mag(a) * mag(b) <= 7, sqr: <= 2, sums <= 7).
+//
+// Point contract shared by the main-loop operations: a Jacobian point fed to
+// gej_double / gej_add_ge has x <= 1, y <= 2, z <= 2 (y = 2: a point set from a
+// negated affine entry); both return points with x = y = z = 1.  Affine operands: x <= 1, y <= 2 (a normalized y, or its
+// negation).
+#pragma once
+
+namespace cudasp {
+
+struct ge {
+  fe x, y;
+};
+
+struct gej {
+  fe x, y, z;
+};
+
+// r = 2a (3M + 4S, the halved form: Z3 = Y1 Z1, L = 3/2 X1^2,
+// X3 = L^2 - 2 X1 Y1^2, Y3 = -(L (X3 - X1 Y1^2) + Y1^4)).  r may alias a.
+CUDASP_HD void gej_double(gej& r, const gej& a) {
+  fe S, L, T, U;
+  FE_CHECK(a.x, 1, "dbl x");
+  FE_CHECK(a.y, 2, "dbl y");
+  FE_CHECK(a.z, 2, "dbl z");
+  fe_mul(r.z, a.z, a.y);   // Z3 = Y1 Z1                         2 * 2 -> (1)
+  fe_sqr(S, a.y);          // S = Y1^2                           (1)
+  fe_sqr(L, a.x);          //                                    (1)
+  fe_mul_int(L, L, 3);     //                                    (3)
+  fe_half(L, L);           // L = 3/2 X1^2                       (2.5)
+  fe_normalize_weak(L);    //                                    (1)
+  fe_mul(T, S, a.x);       //                                    (1)
+  fe_negate<1>(T, T);      // T = -X1 S                          (2)
+  fe_sqr(r.x, L);          //                                    (1)
+  fe_add_to(r.x, T);       //                                    (3)
+  fe_add_to(r.x, T);       // X3 = L^2 + 2T                      (5)
+  fe_normalize_weak(r.x);  //                                    (1)
+  fe_add(U, r.x, T);       // X3 + T                             (3)
+  fe_sqr(S, S);            // S^2                                (1)
+  fe_mul(r.y, L, U);       //                                    (1)
+  fe_add_to(r.y, S);       //                                    (2)
+  fe_negate<2>(r.y, r.y);  // Y3 = -(L (X3 + T) + S^2)           (3)
+  fe_normalize_weak(r.y);  //                                    (1)
+}
+
+// Mixed addition r = a + b (b affine), 8M + 3S (madd-2004-hmv).  r may alias a.
+// If zr != nullptr it receives Z3 / Z1 (= H, mag 1).
+CUDASP_HD void gej_add_ge(gej& r, const gej& a, const ge& b, fe* zr = nullptr) {
+  fe z1z1, z1z1z1, u2, s2, h, rr, hh, hhh, v, t;
+  FE_CHECK(a.x, 1, "add a.x");
+  FE_CHECK(a.y, 2, "add a.y");
+  FE_CHECK(a.z, 2, "add a.z");
+  FE_CHECK(b.x, 1, "add b.x");
+  FE_CHECK(b.y, 2, "add b.y");
+  fe_sqr(z1z1, a.z);              // Z1^2                             (1)
+  fe_mul(z1z1z1, z1z1, a.z);      // Z1^3                             (1)
+  fe_mul(u2, b.x, z1z1);          // U2 = X2 Z1^2                     (1)
+  fe_mul(s2, b.y, z1z1z1);        // S2 = Y2 Z1^3                     (1)
+  fe_sub<1>(h, u2, a.x);          // H = U2 - X1                      (3)
+  fe_normalize_weak(h);           //                                  (1)
+  fe_sub<2>(rr, s2, a.y);         // R = S2 - Y1                      (4)
+  fe_normalize_weak(rr);          //                                  (1)
+  fe_mul(r.z, a.z, h);            // Z3 = Z1 H                        (1)
+  if (zr) *zr = h;
+  fe_sqr(hh, h);                  // HH                               (1)
+  fe_mul(hhh, h, hh);             // HHH                              (1)
+  fe_mul(v, a.x, hh);             // V = X1 HH                        (1)
+  fe_mul(t, a.y, hhh);            // Y1 HHH                           2 * 1 -> (1)
+  fe_sqr(r.x, rr);                // R^2                              (1)
+  fe_sub<1>(r.x, r.x, hhh);       //                                  (3)
+  fe_sub<1>(r.x, r.x, v);         //                                  (5)
+  fe_sub<1>(r.x, r.x, v);         // X3 = R^2 - HHH - 2V              (7)
+  fe_normalize_weak(r.x);         //                                  (1)
+  fe_sub<1>(v, v, r.x);           // V - X3                           (3)
+  fe_mul(v, rr, v);               //                                  (1)
+  fe_sub<1>(r.y, v, t);           // Y3 = R (V - X3) - Y1 HHH         (3)
+  fe_normalize_weak(r.y);         //                                  (1)
+}
+
+// Co-Z initial doubling with update: for an affine, normalized T, d = 2T and
+// t = T with the same Z = T.y.  The halved doubling already forms
+// X1 Y1^2 and Y1^4, which are T's coordinates at Z = Y1.
+// Output: d = (1, 1, 1), t = (1, 1, 1).
+CUDASP_HD void gej_dblu(gej& d, gej& t, const ge& T) {
+  fe S, L, XS, U;
+  FE_CHECK(T.x, 1, "dblu x");
+  FE_CHECK(T.y, 1, "dblu y");
+  fe_sqr(S, T.y);           // S = Y1^2                          (1)
+  fe_sqr(L, T.x);
+  fe_mul_int(L, L, 3);
+  fe_half(L, L);            // L = 3/2 X1^2                      (2.5)
+  fe_normalize_weak(L);     //                                   (1)
+  fe_mul(XS, T.x, S);       // X1 S                              (1)
+  fe_sqr(d.x, L);
+  fe_sub<1>(d.x, d.x, XS);  //                                   (3)
+  fe_sub<1>(d.x, d.x, XS);  // X(2T) = L^2 - 2 X1 S              (5)
+  fe_normalize_weak(d.x);   //                                   (1)
+  fe_sub<1>(U, d.x, XS);    // X3 - X1 S                         (3)
+  fe_mul(d.y, L, U);        //                                   (1)
+  fe_sqr(S, S);             // Y1^4                              (1)
+  fe_add_to(d.y, S);        //                                   (2)
+  fe_negate<2>(d.y, d.y);   // Y(2T) = -(L (X3 - X1 S) + Y1^4)   (3)
+  fe_normalize_weak(d.y);   //                                   (1)
+  d.z = T.y;                // Z = Y1
+  t.x = XS;                 // T = (X1 Y1^2, Y1^4, Y1)
+  t.y = S;
+  t.z = T.y;
+}
+
+// Co-Z addition with update (Meloni 2007, "ZADDU"), 5M + 2S: p and q share Z;
+// r = p + q and p becomes p with r's Z.  zr (if given) receives Z(r) / Z =
+// X(p) - X(q) (mag 1).  Not for p == +-q.  r may not alias p or q.
+// Input: p = (1, 1, 1), q = (1, 3, 1).  Output: r = (1, 3, 1), p = (1, 1, 1).
+CUDASP_HD void gej_zaddu(gej& r, gej& p, const gej& q, fe* zr = nullptr) {
+  fe dx, dy, C, W1, W2, A1, t;
+  FE_CHECK(p.x, 1, "zaddu p.x");
+  FE_CHECK(p.y, 1, "zaddu p.y");
+  FE_CHECK(q.x, 1, "zaddu q.x");
+  FE_CHECK(q.y, 3, "zaddu q.y");
+  fe_sub<1>(dx, p.x, q.x);     // X1 - X2                          (3)
+  fe_normalize_weak(dx);       //                                  (1)
+  fe_sub<3>(dy, p.y, q.y);     // Y1 - Y2                          (5)
+  fe_normalize_weak(dy);       //                                  (1)
+  fe_sqr(C, dx);               // C = (X1 - X2)^2                  (1)
+  fe_mul(W1, p.x, C);          // W1 = X1 C                        (1)
+  fe_mul(W2, q.x, C);          // W2 = X2 C                        (1)
+  fe_sub<1>(t, W1, W2);        //                                  (3)
+  fe_mul(A1, p.y, t);          // A1 = Y1 (W1 - W2)                (1)
+  fe_sqr(r.x, dy);             // D = (Y1 - Y2)^2                  (1)
+  fe_sub<1>(r.x, r.x, W1);     //                                  (3)
+  fe_sub<1>(r.x, r.x, W2);     // X3 = D - W1 - W2                 (5)
+  fe_normalize_weak(r.x);      //                                  (1)
+  fe_sub<1>(t, W1, r.x);       // W1 - X3                          (3)
+  fe_mul(r.y, dy, t);          //                                  (1)
+  fe_sub<1>(r.y, r.y, A1);     // Y3 = (Y1 - Y2)(W1 - X3) - A1     (3)
+  fe_mul(r.z, p.z, dx);        // Z3 = Z (X1 - X2)                 (1)
+  if (zr) *zr = dx;
+  p.x = W1;
+  p.y = A1;
+  p.z = r.z;
+}
+
+// Affine coordinates of a Jacobian point given 1/Z; fully normalized.
+CUDASP_HD void gej_to_ge_zinv(ge& r, const gej& a, const fe& zinv) {
+  fe zi2, zi3;
+  fe_sqr(zi2, zinv);
+  fe_mul(zi3, zi2, zinv);
+  fe_mul(r.x, a.x, zi2);
+  fe_mul(r.y, a.y, zi3);
+  fe_normalize(r.x);
+  fe_normalize(r.y);
+}
+
+CUDASP_HD void gej_set_ge(gej& r, const ge& a) {
+  r.x = a.x;
+  r.y = a.y;
+  fe_set_int(r.z, 1);
+}
+
+// -a for a with y of magnitude <= 1; r.y has magnitude 2.
+CUDASP_HD void ge_neg(ge& r, const ge& a) {
+  r.x = a.x;
+  fe_negate<1>(r.y, a.y);
+}
+
+}  // namespace cudasp

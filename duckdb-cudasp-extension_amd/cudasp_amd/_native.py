@@ -40,6 +40,7 @@ SIGNATURES = {
     "cudasp_synth_output_lengths": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _U32, _P, _P]),
     "cudasp_synth_output_values": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _P, _P, _P, _P]),
     "cudasp_debug_field_ops": (_I32, [ctypes.c_int, _P, _P, _P, _U32]),
+    "cudasp_field_layout": (_I32, [_P, _P, _P, _P, _P]),
     "LaunchBatchScan": (_P, [_P, _P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _U32, ctypes.c_size_t]),
     "RunBatchScanKernels": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _U32]),
     "FreeBatchScanState": (None, [_P]),

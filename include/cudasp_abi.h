@@ -131,11 +131,14 @@ int cudasp_synth_output_lengths(uint64_t seed, uint64_t first_index, uint32_t n,
 int cudasp_synth_output_values(uint64_t seed, uint64_t first_index, uint32_t n, const uint32_t* d_offsets,
                                const uint32_t* d_lengths, int64_t* d_outputs, void* stream);
 
-/* Test hook (field arithmetic of the kernels, on the device): for i < n,
- * out[i] = a[i] * b[i] (op 0) or a[i]^2 (op 1) mod p, each operand 10 x u32
- * 26-bit limbs (row-major, 10 words per element, any magnitude the kernels
- * accept: mag(a) * mag(b) <= 400, each <= 31); the result is magnitude 1,
- * not fully reduced.  Device buffers; synchronous. */
+/* Test hooks (field arithmetic of the kernels, on the device).
+ * cudasp_field_layout: the build's limb layout (10 x 26 or 9 x 29 bits, top
+ * limb 22 / 24 bits) and its multiplication magnitude limits.
+ * cudasp_debug_field_ops: for i < n, out[i] = a[i] * b[i] (op 0) or a[i]^2
+ * (op 1) mod p, operands `limbs` u32 limbs each (row-major, any magnitude the
+ * kernels accept); the result has magnitude 1, not fully reduced.  Device
+ * buffers; synchronous. */
+int cudasp_field_layout(int* limbs, int* bits, int* mul_mag_max, int* sqr_mag_max, int* limb_mag_max);
 int cudasp_debug_field_ops(int op, const uint32_t* d_a, const uint32_t* d_b, uint32_t* d_out, uint32_t n);
 
 /* -------------------------------------------- reference three-phase ABI */

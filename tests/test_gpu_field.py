@@ -1,16 +1,17 @@
-"""GPU: the kernels' field multiply / square (secp256k1_fe.hpp; on gfx950 the
-generated asm blocks of secp256k1_fe_asm.inc) against Python integers, over the
-whole input range the group formulas rely on: operand magnitudes with
-mag(a) * mag(b) <= 400 (each <= 31), random limbs and every limb at its maximum.
-The result must be congruent mod p and of magnitude 1."""
+"""GPU: the kernels' field multiply / square (secp256k1_fe.hpp /
+secp256k1_fe29.hpp; on gfx950 the generated asm blocks) against Python
+integers, over the whole input range the group formulas rely on: every operand
+magnitude pair the build's layout allows (cudasp_field_layout: 10 x 26 limbs
+take mag(a) * mag(b) <= 400, 9 x 29 limbs <= 9), random limbs and every limb at
+its maximum.  The result must be congruent mod p and of magnitude 1."""
+import ctypes
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 P = 2**256 - 2**32 - 977
-MAG_PAIRS = [(1, 1), (2, 1), (8, 8), (7, 17), (17, 7), (15, 15), (20, 20), (31, 12), (12, 31), (16, 25), (1, 31),
-             (31, 1), (3, 35 // 3)]
 
 
 @pytest.fixture(scope="module")
@@ -21,24 +22,35 @@ def torch():
     return torch
 
 
-def limb_bounds(m):
-    b = np.full(10, m * (1 << 26) + (1 << 23), dtype=np.uint64)
-    b[9] = m * (1 << 22) + (1 << 13)
+@pytest.fixture(scope="module")
+def layout(torch):
+    from cudasp_amd import _native
+    v = [ctypes.c_int() for _ in range(5)]
+    _native.check(_native.load().cudasp_field_layout(*[ctypes.byref(x) for x in v]))
+    limbs, bits, mul_max, sqr_max, limb_max = (x.value for x in v)
+    top = 256 - bits * (limbs - 1)
+    slack = (1 << 23, 1 << 13) if bits == 26 else (1 << 16, 1 << 11)
+    return dict(limbs=limbs, bits=bits, top=top, mul_max=mul_max, sqr_max=sqr_max, limb_max=limb_max, slack=slack)
+
+
+def limb_bounds(lay, m):
+    b = np.full(lay["limbs"], m * (1 << lay["bits"]) + lay["slack"][0], dtype=np.uint64)
+    b[-1] = m * (1 << lay["top"]) + lay["slack"][1]
     return b
 
 
-def operands(rng, m, count):
-    hi = limb_bounds(m)
-    a = (rng.random((count, 10)) * (hi + 1)).astype(np.uint64)
+def operands(lay, rng, m, count):
+    hi = limb_bounds(lay, m)
+    a = (rng.random((count, lay["limbs"])) * (hi + 1)).astype(np.uint64)
     a[0] = hi           # every limb at its maximum
     a[1] = 0
     a[2] = hi
-    a[2, 9] = 0
+    a[2, -1] = 0
     return np.minimum(a, hi).astype(np.uint32)
 
 
-def value(limbs):
-    return sum(int(v) << (26 * k) for k, v in enumerate(limbs))
+def value(lay, limbs):
+    return sum(int(v) << (lay["bits"] * k) for k, v in enumerate(limbs))
 
 
 def run(torch, op, a, b):
@@ -51,35 +63,44 @@ def run(torch, op, a, b):
     return out.cpu().numpy().view(np.uint32)
 
 
-def check(a, b, r, sqr):
-    bound = limb_bounds(1)
-    assert (r.astype(np.uint64) <= bound).all(), "result not of magnitude 1"
+def check(lay, a, b, r, sqr):
+    assert (r.astype(np.uint64) <= limb_bounds(lay, 1)).all(), "result not of magnitude 1"
     for i in range(a.shape[0]):
-        va = value(a[i])
-        vb = va if sqr else value(b[i])
-        assert value(r[i]) % P == (va * vb) % P, (i, a[i], b[i], r[i])
+        va = value(lay, a[i])
+        vb = va if sqr else value(lay, b[i])
+        assert value(lay, r[i]) % P == (va * vb) % P, (i, a[i], b[i], r[i])
 
 
-@pytest.mark.parametrize("ma,mb", MAG_PAIRS)
-def test_mul_magnitudes(torch, ma, mb):
-    rng = np.random.default_rng(1000 * ma + mb)
-    a = operands(rng, ma, 2048)
-    b = operands(rng, mb, 2048)
-    check(a, b, run(torch, 0, a, b), sqr=False)
+def mag_pairs(lay):
+    top, lim = lay["mul_max"], lay["limb_max"]
+    pairs = {(1, 1), (1, lim), (lim, 1)}
+    for ma in range(1, lim + 1):
+        mb = min(lim, top // ma)
+        pairs.add((ma, mb))
+    return sorted(pairs)
 
 
-@pytest.mark.parametrize("m", [1, 2, 8, 17, 20])
-def test_sqr_magnitudes(torch, m):
-    rng = np.random.default_rng(7 + m)
-    a = operands(rng, m, 2048)
-    check(a, a, run(torch, 1, a, a), sqr=True)
+def test_mul_magnitudes(torch, layout):
+    for ma, mb in mag_pairs(layout):
+        rng = np.random.default_rng(1000 * ma + mb)
+        a = operands(layout, rng, ma, 1024)
+        b = operands(layout, rng, mb, 1024)
+        check(layout, a, b, run(torch, 0, a, b), sqr=False)
 
 
-def test_mul_reduced_edge_values(torch):
+def test_sqr_magnitudes(torch, layout):
+    for m in range(1, layout["sqr_max"] + 1):
+        rng = np.random.default_rng(7 + m)
+        a = operands(layout, rng, m, 1024)
+        check(layout, a, a, run(torch, 1, a, a), sqr=True)
+
+
+def test_mul_reduced_edge_values(torch, layout):
     """Values around p and 2^256 in normal form."""
     vals = [0, 1, 2, P - 1, P - 2, P, P + 1, 2**256 - 1, 2**255, 2**32 + 977, 2**26 - 1, 2**52]
-    rows = [[(v >> (26 * k)) & (2**26 - 1) if k < 9 else v >> 234 for k in range(10)] for v in vals]
+    bits, n = layout["bits"], layout["limbs"]
+    rows = [[(v >> (bits * k)) & (2**bits - 1) if k < n - 1 else v >> (bits * (n - 1)) for k in range(n)] for v in vals]
     a = np.array([x for x in rows for _ in rows], dtype=np.uint32)
     b = np.array([y for _ in rows for y in rows], dtype=np.uint32)
-    check(a, b, run(torch, 0, a, b), sqr=False)
-    check(a, a, run(torch, 1, a, a), sqr=True)
+    check(layout, a, b, run(torch, 0, a, b), sqr=False)
+    check(layout, a, a, run(torch, 1, a, a), sqr=True)

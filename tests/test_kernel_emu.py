@@ -22,9 +22,10 @@ GY = 0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8
 LAMBDA = 0x5363ad4cc05c30e0a5261c028812645a122e22ea20816678df02967c1b23bd72
 
 
-@pytest.fixture(scope="module")
-def emu():
-    path = os.path.join(HERE, "native", "libcudasp_emu.so")
+@pytest.fixture(scope="module", params=["libcudasp_emu.so", "libcudasp_emu29.so"], ids=["10x26", "9x29"])
+def emu(request):
+    """The kernel math host-compiled once per field layout (tests/native)."""
+    path = os.path.join(HERE, "native", request.param)
     if not os.path.exists(path):
         subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])
     lib = ctypes.CDLL(path)

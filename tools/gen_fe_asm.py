@@ -27,6 +27,7 @@ M26 = "0x3ffffff"
 M22 = "0x3fffff"
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "duckdb-cudasp-extension_amd", "csrc",
                    "secp256k1_fe_asm.inc")
+OUT29 = os.path.join(os.path.dirname(OUT), "secp256k1_fe29_asm.inc")
 
 
 def pair(i):
@@ -120,6 +121,125 @@ def gen(sqr):
     ins.append("v_lshl_add_u32 %s, %s, 12, %s" % (lo(W), uhi, lo(W)))   # + uhi (F1<<6) = uhi << 12
     ins.append("v_add_u32 %%[o2], %%[o2], %s" % lo(W))
     return ins
+
+
+class Layout:
+    """Limb layout: n limbs of `bits` bits, the top one `top` bits (n*bits ..
+    256); 2^(n*bits) = r0 + r1*2^bits and 2^256 = f0 + f1*2^bits (mod p)."""
+
+    def __init__(self, n, bits, top, r0, r1, f0, f1, top_has_hi):
+        self.n, self.bits, self.top, self.r0, self.r1, self.f0, self.f1 = n, bits, top, r0, r1, f0, f1
+        self.s = 32 - bits              # hi * 2^32 = (hi << s) * 2^bits
+        self.top_has_hi = top_has_hi    # the wrapped term hi(H_(n-2)) * (r1 << s) may exceed 32 bits
+        self.mask = "0x%x" % ((1 << bits) - 1)
+        self.tmask = "0x%x" % ((1 << top) - 1)
+
+
+L26 = Layout(10, 26, 22, 0x3D10, 0x400, 0x3D1, 0x40, True)
+L29 = Layout(9, 29, 24, 0x7A20, 0x100, 0x3D1, 0x8, False)
+
+
+def product_terms_l(lay, k, sqr):
+    t = []
+    for i in range(lay.n):
+        j = k - i
+        if j < 0 or j >= lay.n:
+            continue
+        if sqr:
+            if j > i:
+                t.append(("%[d" + str(i) + "]", "%[a" + str(j) + "]"))
+            elif j == i:
+                t.append(("%[a" + str(i) + "]", "%[a" + str(i) + "]"))
+        else:
+            t.append(("%[a" + str(i) + "]", "%[b" + str(j) + "]"))
+    return t
+
+
+def gen_layout(lay, sqr):
+    """gen() for any Layout (serial schedule)."""
+    n = lay.n
+    ins = []
+    H = [2 * m for m in range(n - 1)]
+    ACC, Z, Y, W = 2 * (n - 1), 2 * (n - 1) + 2, 2 * (n - 1) + 4, 2 * (n - 1) + 6
+
+    def mad(dst, x, y, acc):
+        ins.append("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (dst, x, y, acc))
+
+    cols = [product_terms_l(lay, n + m, sqr) for m in range(n - 1)]
+    depth = max(len(c) for c in cols)
+    for d in range(depth):
+        for m in range(n - 1):
+            if d < len(cols[m]):
+                x, y = cols[m][d]
+                mad(pair(H[m]), x, y, "0" if d == 0 else pair(H[m]))
+    mad(pair(W), hi(H[n - 2]), "%[r1s]", "0")  # wraps to weight 2^(n bits)
+    for k in range(n):
+        terms = []
+        if k < n - 1:
+            terms.append((lo(H[k]), "%[r0]"))
+        if k == 0:
+            terms.append((lo(W), "%[r0]"))
+        if 1 <= k <= n - 1:
+            terms += [(lo(H[k - 1]), "%[r1]"), (hi(H[k - 1]), "%[r0s]")]
+        if k == 1:
+            terms.append((lo(W), "%[r1]"))
+            if lay.top_has_hi:
+                terms.append((hi(W), "%[r0s]"))
+        if 2 <= k <= n - 1 and k - 2 <= n - 3:
+            terms.append((hi(H[k - 2]), "%[r1s]"))
+        if k == 2 and lay.top_has_hi:
+            terms.append((hi(W), "%[r1s]"))
+        terms += product_terms_l(lay, k, sqr)
+        for m_, (x, y) in enumerate(terms):
+            mad(pair(ACC), x, y, "0" if (k == 0 and m_ == 0) else pair(ACC))
+        if k == 0:
+            ins += ["v_and_b32 %s, %s, %s" % (lo(Z), lay.mask, lo(ACC)), "v_mov_b32 %s, 0" % hi(Z)]
+        elif k == 1:
+            ins += ["v_and_b32 %s, %s, %s" % (lo(Y), lay.mask, lo(ACC)), "v_mov_b32 %s, 0" % hi(Y)]
+        elif k < n - 1:
+            ins.append("v_and_b32 %%[o%d], %s, %s" % (k, lay.mask, lo(ACC)))
+        else:
+            ins.append("v_and_b32 %%[o%d], %s, %s" % (k, lay.tmask, lo(ACC)))
+        ins.append("v_lshrrev_b64 %s, %d, %s" % (pair(ACC), lay.bits if k < n - 1 else lay.top, pair(ACC)))
+    ulo, uhi = lo(ACC), hi(ACC)
+    t = lo(W)
+    f1s_shift = (lay.f1 << lay.s).bit_length() - 1
+    assert (lay.f1 << lay.s) == 1 << f1s_shift
+    ins += [("v_mad_u64_u32 %s, vcc, %s, %%[f0], %s" % (pair(Z), ulo, pair(Z))),
+            "v_and_b32 %%[o0], %s, %s" % (lay.mask, lo(Z)),
+            "v_alignbit_b32 %s, %s, %s, %d" % (t, hi(Z), lo(Z), lay.bits),
+            "v_add_u32 %s, %s, %s" % (lo(Y), lo(Y), t),
+            "v_mad_u64_u32 %s, vcc, %s, %d, %s" % (pair(Y), ulo, lay.f1, pair(Y)),
+            "v_mad_u64_u32 %s, vcc, %s, %%[f0s], %s" % (pair(Y), uhi, pair(Y)),
+            "v_and_b32 %%[o1], %s, %s" % (lay.mask, lo(Y)),
+            "v_alignbit_b32 %s, %s, %s, %d" % (t, hi(Y), lo(Y), lay.bits),
+            "v_lshl_add_u32 %s, %s, %d, %s" % (t, uhi, f1s_shift, t),
+            "v_add_u32 %%[o2], %%[o2], %s" % t]
+    return ins, 2 * (n - 1) + 8
+
+
+def emit_layout(lay, name, sqr):
+    ins, ntmp = gen_layout(lay, sqr)
+    n = lay.n
+    body = "\n".join('      "%s\\n"' % s for s in ins)
+    outs = ", ".join('[o%d] "=&v"(r.n[%d])' % (k, k) for k in range(n))
+    if sqr:
+        inl = ['[a%d] "v"(a.n[%d])' % (i, i) for i in range(n)] + ['[d%d] "v"(d[%d])' % (i, i) for i in range(n - 1)]
+    else:
+        inl = ['[a%d] "v"(a.n[%d])' % (i, i) for i in range(n)] + ['[b%d] "v"(b.n[%d])' % (i, i) for i in range(n)]
+    inl += ['[r0] "s"(c_r0)', '[r1] "s"(c_r1)', '[r0s] "s"(c_r0s)', '[r1s] "s"(c_r1s)', '[f0] "s"(c_f0)',
+            '[f0s] "s"(c_f0s)']
+    clob = ", ".join(['"vcc"'] + ['"v%d"' % (BASE + i) for i in range(ntmp)])
+    sig = "fe& r, const fe& a" if sqr else "fe& r, const fe& a, const fe& b"
+    pre = ""
+    if sqr:
+        pre = "  uint32_t d[%d];\n#pragma unroll\n  for (int i = 0; i < %d; i++) d[i] = a.n[i] << 1;\n" % (n - 1, n - 1)
+    return ("__device__ __forceinline__ void %s(%s) {\n%s"
+            "  const uint32_t c_r0 = opaque_const(R0), c_r1 = opaque_const(R1);\n"
+            "  const uint32_t c_r0s = opaque_const(R0 << %d), c_r1s = opaque_const(R1 << %d);\n"
+            "  const uint32_t c_f0 = opaque_const(F0), c_f0s = opaque_const(F0 << %d);\n"
+            "  asm(\n%s\n      : %s\n      : %s\n      : %s);\n}\n"
+            % (name, sig, pre, lay.s, lay.s, lay.s, body, outs, ",\n        ".join(inl), clob)), len(ins), ntmp
 
 
 def interleave(a, b):
@@ -240,6 +360,8 @@ def main():
     sqr, ns = emit("fe_sqr_asm", True)
     pmul, pnm = emit("fe_mul_asm_p", False, True)
     psqr, pns = emit("fe_sqr_asm_p", True, True)
+    # the layout-generic generator must reproduce the 10x26 serial blocks exactly
+    assert emit_layout(L26, "fe_mul_asm", False)[0] == mul and emit_layout(L26, "fe_sqr_asm", True)[0] == sqr
     text = ("// GENERATED by tools/gen_fe_asm.py -- do not edit; regenerate and commit both.\n"
             "// Serial schedule (variant 3): fe_mul %d instructions, fe_sqr %d, temporaries v%d..v%d.\n"
             "// Pipelined schedule (variant 4): fe_mul %d, fe_sqr %d, temporaries v%d..v%d.\n"
@@ -248,6 +370,14 @@ def main():
     with open(OUT, "w") as f:
         f.write(text)
     print("wrote %s: serial mul %d / sqr %d, pipelined mul %d / sqr %d instructions" % (OUT, nm, ns, pnm, pns))
+    m29, n29m, t29 = emit_layout(L29, "fe_mul_asm", False)
+    s29, n29s, _ = emit_layout(L29, "fe_sqr_asm", True)
+    text = ("// GENERATED by tools/gen_fe_asm.py -- do not edit; regenerate and commit both.\n"
+            "// 9 x 29-bit limbs: fe_mul %d instructions, fe_sqr %d (+8 doublings outside the block),\n"
+            "// temporaries v%d..v%d and vcc (clobbered).\n\n" % (n29m, n29s, BASE, BASE + t29 - 1)) + m29 + "\n" + s29
+    with open(OUT29, "w") as f:
+        f.write(text)
+    print("wrote %s: mul %d / sqr %d instructions" % (OUT29, n29m, n29s))
 
 
 if __name__ == "__main__":

@@ -6,11 +6,11 @@ using namespace cudasp;
 
 __device__ __forceinline__ void ld(fe& a, const uint32_t* p) {
 #pragma unroll
-  for (int i = 0; i < 10; i++) a.n[i] = p[i * 65536 + threadIdx.x];
+  for (int i = 0; i < FE_LIMBS; i++) a.n[i] = p[i * 65536 + threadIdx.x];
 }
 __device__ __forceinline__ void st(uint32_t* p, const fe& a) {
 #pragma unroll
-  for (int i = 0; i < 10; i++) p[i * 65536 + threadIdx.x] = a.n[i];
+  for (int i = 0; i < FE_LIMBS; i++) p[i * 65536 + threadIdx.x] = a.n[i];
 }
 extern "C" __global__ __launch_bounds__(256, 2) void probe_mul(const uint32_t* in, uint32_t* out) {
   fe a, b, r; ld(a, in); ld(b, in + 655360); fe_mul(r, a, b); st(out, r);
