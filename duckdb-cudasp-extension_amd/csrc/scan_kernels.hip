@@ -54,10 +54,10 @@ constexpr int BLOCK = 256;
 // Minimum waves per SIMD requested for the two hot kernels (register budget:
 // 2 -> 256 VGPRs, 3 -> 168, 4 -> 128).  Tuned on MI355X; see DESIGN.md.
 #ifndef CUDASP_WAVES_A
-#define CUDASP_WAVES_A 2
+#define CUDASP_WAVES_A 3
 #endif
 #ifndef CUDASP_WAVES_B
-#define CUDASP_WAVES_B 2
+#define CUDASP_WAVES_B 3
 #endif
 // Grid cap for the grid-stride kernels; also bounds the per-slot scratch.
 constexpr uint32_t MAX_BLOCKS = 4096;
