@@ -278,7 +278,7 @@ def main():
     ap.add_argument("--outputs-max", type=int, default=0,
                     help="variable outputs per row, uniform in [1, N] (15 -> mean 8, config 5); 0 = fixed")
     ap.add_argument("--streams", type=int, default=4)
-    ap.add_argument("--cpu-rows", type=int, default=300000)
+    ap.add_argument("--cpu-rows", type=int, default=1200000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_k_shared_secret.json"))
