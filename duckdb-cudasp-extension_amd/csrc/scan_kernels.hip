@@ -364,10 +364,28 @@ __global__ __launch_bounds__(BLOCK) void k_debug_field_ops(int op, const uint32_
     x.n[k] = a[(size_t)i * FE_LIMBS + k];
     y.n[k] = b[(size_t)i * FE_LIMBS + k];
   }
-  if (op == 0)
+  if (op == 0) {
     fe_mul(r, x, y);
-  else
+  } else if (op == 1) {
     fe_sqr(r, x);
+  } else {
+#if CUDASP_FE_LIMBS == 9
+    fe c, e;
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) {
+      c.n[k] = b[((size_t)n + i) * FE_LIMBS + k];
+      e.n[k] = b[((size_t)2 * n + i) * FE_LIMBS + k];
+    }
+    if (op == 2)
+      fe_mul2(r, x, y, c, e);
+    else if (op == 3)
+      fe_mulsqr(r, x, y, c);
+    else if (op == 4)
+      fe_mul_add(r, x, y, c);
+    else
+      fe_sqr_add(r, x, c);
+#endif
+  }
 #pragma unroll
   for (int k = 0; k < FE_LIMBS; k++) out[(size_t)i * FE_LIMBS + k] = r.n[k];
 }
@@ -819,7 +837,8 @@ int cudasp_field_layout(int* limbs, int* bits, int* mul_mag_max, int* sqr_mag_ma
 
 int cudasp_debug_field_ops(int op, const uint32_t* d_a, const uint32_t* d_b, uint32_t* d_out, uint32_t n) {
   if (n == 0) return CUDASP_OK;
-  if (op != 0 && op != 1) return set_error(CUDASP_ERR_INVALID_ARG, "op must be 0 (mul) or 1 (sqr)");
+  if (op < 0 || op > (CUDASP_FE_LIMBS == 9 ? 5 : 1))
+    return set_error(CUDASP_ERR_INVALID_ARG, "op must be 0 (mul) or 1 (sqr), or 2..5 (fused, 9 x 29 layout)");
   if (!d_a || !d_b || !d_out) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   hipLaunchKernelGGL(k_debug_field_ops, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, 0, op, d_a, d_b, d_out, n);
   HIP_TRY(hipGetLastError());

@@ -68,6 +68,11 @@ CUDASP_HD void fe_check_mul(const fe& a, const fe& b, const char* what) {
   if (mb > LIMB_MAG_MAX) fe_check_fail(what, -2, mb);
   if (ma * mb > MUL_MAG_MAX) fe_check_fail(what, -3, ma * mb);
 }
+CUDASP_HD void fe_check_mul2(const fe& a, const fe& b, const fe& c, const fe& e, const char* what) {
+  uint32_t ma = fe_mag_of(a), mb = fe_mag_of(b), mc = fe_mag_of(c), me = fe_mag_of(e);
+  if (ma > LIMB_MAG_MAX || mb > LIMB_MAG_MAX || mc > LIMB_MAG_MAX || me > LIMB_MAG_MAX) fe_check_fail(what, -1, ma);
+  if (ma * mb + mc * me > MUL_MAG_MAX) fe_check_fail(what, -3, ma * mb + mc * me);
+}
 CUDASP_HD void fe_check_sqr(const fe& a, const char* what) {
   uint32_t ma = fe_mag_of(a);
   if (ma > SQR_MAG_MAX) fe_check_fail(what, -4, ma);
@@ -78,11 +83,13 @@ CUDASP_HD void fe_check_sum(const fe& a, const char* what) {
 }
 #define FE_CHECK(a, m, what) fe_check_mag(a, m, what)
 #define FE_CHECK_MUL(a, b, what) fe_check_mul(a, b, what)
+#define FE_CHECK_MUL2(a, b, c, e, what) fe_check_mul2(a, b, c, e, what)
 #define FE_CHECK_SQR(a, what) fe_check_sqr(a, what)
 #define FE_CHECK_SUM(a, what) fe_check_sum(a, what)
 #else
 #define FE_CHECK(a, m, what) ((void)0)
 #define FE_CHECK_MUL(a, b, what) ((void)0)
+#define FE_CHECK_MUL2(a, b, c, e, what) ((void)0)
 #define FE_CHECK_SQR(a, what) ((void)0)
 #define FE_CHECK_SUM(a, what) ((void)0)
 #endif
@@ -248,37 +255,47 @@ CUDASP_HD void fe29_reduce_columns(fe& r, const uint64_t c[17]) {
   for (int k = 3; k < 9; k++) r.n[k] = o[k];
 }
 
-CUDASP_HD void fe_mul_c(fe& r, const fe& a, const fe& b) {
-  uint64_t c[17];
+// Product columns, accumulated into c[0..16].
+CUDASP_HD void fe29_mul_columns(uint64_t c[17], const fe& a, const fe& b) {
 #pragma unroll
   for (int k = 0; k < 17; k++) {
-    uint64_t s = 0;
 #pragma unroll
     for (int i = 0; i < 9; i++) {
       int j = k - i;
-      if (j >= 0 && j < 9) s += (uint64_t)a.n[i] * b.n[j];
+      if (j >= 0 && j < 9) c[k] += (uint64_t)a.n[i] * b.n[j];
     }
-    c[k] = s;
   }
+}
+
+CUDASP_HD void fe29_sqr_columns(uint64_t c[17], const fe& a) {
+  uint32_t a2[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) a2[i] = a.n[i] * 2;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      int j = k - i;
+      if (j > i && j < 9) c[k] += (uint64_t)a2[i] * a.n[j];
+      else if (j == i) c[k] += (uint64_t)a.n[i] * a.n[i];
+    }
+  }
+}
+
+CUDASP_HD void fe29_add_columns(uint64_t c[17], const fe& a) {
+#pragma unroll
+  for (int k = 0; k < 9; k++) c[k] += a.n[k];
+}
+
+CUDASP_HD void fe_mul_c(fe& r, const fe& a, const fe& b) {
+  uint64_t c[17] = {};
+  fe29_mul_columns(c, a, b);
   fe29_reduce_columns(r, c);
 }
 
 CUDASP_HD void fe_sqr_c(fe& r, const fe& a) {
-  uint32_t a2[9];
-#pragma unroll
-  for (int i = 0; i < 9; i++) a2[i] = a.n[i] * 2;
-  uint64_t c[17];
-#pragma unroll
-  for (int k = 0; k < 17; k++) {
-    uint64_t s = 0;
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-      int j = k - i;
-      if (j > i && j < 9) s += (uint64_t)a2[i] * a.n[j];
-      else if (j == i) s += (uint64_t)a.n[i] * a.n[i];
-    }
-    c[k] = s;
-  }
+  uint64_t c[17] = {};
+  fe29_sqr_columns(c, a);
   fe29_reduce_columns(r, c);
 }
 
@@ -301,6 +318,68 @@ CUDASP_HD void fe_sqr(fe& r, const fe& a) {
   fe_sqr_asm(r, a);
 #else
   fe_sqr_c(r, a);
+#endif
+}
+
+// ------------------------------------------------------------ fused forms
+// One reduction for a sum of products (+ an addend): the columns of every
+// term are summed before the fold, so the reduction (37 of a mul's 118 mads)
+// and the carry chain are paid once, and the result has magnitude 1 without
+// a separate normalization.  The column budget is shared: the operands'
+// magnitude products sum to <= 7 (an addend of magnitude <= 7 adds < 2^32 to
+// a low column, well inside the slack).
+
+// r = a b + c e
+CUDASP_HD void fe_mul2(fe& r, const fe& a, const fe& b, const fe& c, const fe& e) {
+  FE_CHECK_MUL2(a, b, c, e, "mul2");
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_mul2_asm(r, a, b, c, e);
+#else
+  uint64_t col[17] = {};
+  fe29_mul_columns(col, a, b);
+  fe29_mul_columns(col, c, e);
+  fe29_reduce_columns(r, col);
+#endif
+}
+
+// r = a b + c^2
+CUDASP_HD void fe_mulsqr(fe& r, const fe& a, const fe& b, const fe& c) {
+  FE_CHECK_MUL2(a, b, c, c, "mulsqr");
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_mulsqr_asm(r, a, b, c);
+#else
+  uint64_t col[17] = {};
+  fe29_mul_columns(col, a, b);
+  fe29_sqr_columns(col, c);
+  fe29_reduce_columns(r, col);
+#endif
+}
+
+// r = a b + c
+CUDASP_HD void fe_mul_add(fe& r, const fe& a, const fe& b, const fe& c) {
+  FE_CHECK_MUL(a, b, "mul_add");
+  FE_CHECK_SUM(c, "mul_add addend");
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_mul_add_asm(r, a, b, c);
+#else
+  uint64_t col[17] = {};
+  fe29_mul_columns(col, a, b);
+  fe29_add_columns(col, c);
+  fe29_reduce_columns(r, col);
+#endif
+}
+
+// r = a^2 + c
+CUDASP_HD void fe_sqr_add(fe& r, const fe& a, const fe& c) {
+  FE_CHECK_SQR(a, "sqr_add");
+  FE_CHECK_SUM(c, "sqr_add addend");
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_sqr_add_asm(r, a, c);
+#else
+  uint64_t col[17] = {};
+  fe29_sqr_columns(col, a);
+  fe29_add_columns(col, c);
+  fe29_reduce_columns(r, col);
 #endif
 }
 

@@ -6,8 +6,9 @@
 //
 // Point contract shared by the main-loop operations: a Jacobian point fed to
 // gej_double / gej_add_ge has x <= 1, y <= 2, z <= 2 (y = 2: a point set from a
-// negated affine entry); both return points with x = y = z = 1.  Affine operands: x <= 1, y <= 2 (a normalized y, or its
-// negation).
+// negated affine entry, or a doubling's output); gej_add_ge returns
+// (1, 1, 1), gej_double (1, 2, 1).  Affine operands: x <= 1, y <= 2 (a
+// normalized y, or its negation).
 #pragma once
 
 namespace cudasp {
@@ -21,7 +22,9 @@ struct gej {
 };
 
 // r = 2a (3M + 4S, the halved form: Z3 = Y1 Z1, L = 3/2 X1^2,
-// X3 = L^2 - 2 X1 Y1^2, Y3 = -(L (X3 - X1 Y1^2) + Y1^4)).  r may alias a.
+// X3 = L^2 - 2 X1 Y1^2, Y3 = -(L (X3 - X1 Y1^2) + Y1^4)).  X3 and Y3 each come
+// out of one fused reduction (fe_sqr_add, fe_mulsqr).  r may alias a.
+// Output: x = z = 1, y = 2.
 CUDASP_HD void gej_double(gej& r, const gej& a) {
   fe S, L, T, U;
   FE_CHECK(a.x, 1, "dbl x");
@@ -35,50 +38,41 @@ CUDASP_HD void gej_double(gej& r, const gej& a) {
   fe_normalize_weak(L);    //                                    (1)
   fe_mul(T, S, a.x);       //                                    (1)
   fe_negate<1>(T, T);      // T = -X1 S                          (2)
-  fe_sqr(r.x, L);          //                                    (1)
-  fe_add_to(r.x, T);       //                                    (3)
-  fe_add_to(r.x, T);       // X3 = L^2 + 2T                      (5)
-  fe_normalize_weak(r.x);  //                                    (1)
+  fe_add(U, T, T);         // 2T                                 (4)
+  fe_sqr_add(r.x, L, U);   // X3 = L^2 + 2T                      (1)
   fe_add(U, r.x, T);       // X3 + T                             (3)
-  fe_sqr(S, S);            // S^2                                (1)
-  fe_mul(r.y, L, U);       //                                    (1)
-  fe_add_to(r.y, S);       //                                    (2)
-  fe_negate<2>(r.y, r.y);  // Y3 = -(L (X3 + T) + S^2)           (3)
-  fe_normalize_weak(r.y);  //                                    (1)
+  fe_mulsqr(r.y, L, U, S); // L (X3 + T) + S^2                   1 * 3 + 1 -> (1)
+  fe_negate<1>(r.y, r.y);  // Y3                                 (2)
 }
 
 // Mixed addition r = a + b (b affine), 8M + 3S (madd-2004-hmv).  r may alias a.
-// If zr != nullptr it receives Z3 / Z1 (= H, mag 1).
+// If zr != nullptr it receives Z3 / Z1 (= H, mag 1).  H, R and X3 each take
+// their subtrahends inside the product's reduction (fe_mul_add, fe_sqr_add)
+// and Y3 = R (V - X3) + (-Y1) HHH is one fused reduction (fe_mul2).
 CUDASP_HD void gej_add_ge(gej& r, const gej& a, const ge& b, fe* zr = nullptr) {
-  fe z1z1, z1z1z1, u2, s2, h, rr, hh, hhh, v, t;
+  fe z1z1, z1z1z1, u2, h, rr, hh, hhh, v, ny, w;
   FE_CHECK(a.x, 1, "add a.x");
   FE_CHECK(a.y, 2, "add a.y");
   FE_CHECK(a.z, 2, "add a.z");
   FE_CHECK(b.x, 1, "add b.x");
   FE_CHECK(b.y, 2, "add b.y");
-  fe_sqr(z1z1, a.z);              // Z1^2                             (1)
-  fe_mul(z1z1z1, z1z1, a.z);      // Z1^3                             (1)
-  fe_mul(u2, b.x, z1z1);          // U2 = X2 Z1^2                     (1)
-  fe_mul(s2, b.y, z1z1z1);        // S2 = Y2 Z1^3                     (1)
-  fe_sub<1>(h, u2, a.x);          // H = U2 - X1                      (3)
-  fe_normalize_weak(h);           //                                  (1)
-  fe_sub<2>(rr, s2, a.y);         // R = S2 - Y1                      (4)
-  fe_normalize_weak(rr);          //                                  (1)
-  fe_mul(r.z, a.z, h);            // Z3 = Z1 H                        (1)
+  fe_sqr(z1z1, a.z);               // Z1^2                            (1)
+  fe_mul(z1z1z1, z1z1, a.z);       // Z1^3                            (1)
+  fe_negate<1>(u2, a.x);           // -X1                             (2)
+  fe_mul_add(h, b.x, z1z1, u2);    // H = X2 Z1^2 - X1                (1)
+  fe_negate<2>(ny, a.y);           // -Y1                             (3)
+  fe_mul_add(rr, b.y, z1z1z1, ny); // R = Y2 Z1^3 - Y1                2 * 1 -> (1)
+  fe_mul(r.z, a.z, h);             // Z3 = Z1 H                       (1)
   if (zr) *zr = h;
-  fe_sqr(hh, h);                  // HH                               (1)
-  fe_mul(hhh, h, hh);             // HHH                              (1)
-  fe_mul(v, a.x, hh);             // V = X1 HH                        (1)
-  fe_mul(t, a.y, hhh);            // Y1 HHH                           2 * 1 -> (1)
-  fe_sqr(r.x, rr);                // R^2                              (1)
-  fe_sub<1>(r.x, r.x, hhh);       //                                  (3)
-  fe_sub<1>(r.x, r.x, v);         //                                  (5)
-  fe_sub<1>(r.x, r.x, v);         // X3 = R^2 - HHH - 2V              (7)
-  fe_normalize_weak(r.x);         //                                  (1)
-  fe_sub<1>(v, v, r.x);           // V - X3                           (3)
-  fe_mul(v, rr, v);               //                                  (1)
-  fe_sub<1>(r.y, v, t);           // Y3 = R (V - X3) - Y1 HHH         (3)
-  fe_normalize_weak(r.y);         //                                  (1)
+  fe_sqr(hh, h);                   // HH                              (1)
+  fe_mul(hhh, h, hh);              // HHH                             (1)
+  fe_mul(v, a.x, hh);              // V = X1 HH                       (1)
+  fe_add(w, v, v);
+  fe_add_to(w, hhh);               // HHH + 2V                        (3)
+  fe_negate<3>(w, w);              //                                 (4)
+  fe_sqr_add(r.x, rr, w);          // X3 = R^2 - HHH - 2V             (1)
+  fe_sub<1>(v, v, r.x);            // V - X3                          (3)
+  fe_mul2(r.y, rr, v, ny, hhh);    // Y3 = R (V - X3) - Y1 HHH        1 * 3 + 3 * 1 -> (1)
 }
 
 // Co-Z initial doubling with update: for an affine, normalized T, d = 2T and

@@ -119,6 +119,34 @@ int emu_fe_sqr(const uint8_t a[32], uint8_t out[32]) {
   return 0;
 }
 
+int emu_fe_limbs(void) { return FE_LIMBS; }
+
+// Raw-limb field ops (magnitude preconditions checked): op 0 a*b, 1 a^2; the
+// 9 x 29 layout's fused forms 2 a*b + c*e, 3 a*b + c^2, 4 a*b + c, 5 a^2 + c.
+int emu_fe_raw_op(int op, const uint32_t* a, const uint32_t* b, const uint32_t* c, const uint32_t* e,
+                  uint32_t* out) {
+  fe x, y, z, w, r;
+  for (int k = 0; k < FE_LIMBS; k++) {
+    x.n[k] = a[k];
+    y.n[k] = b[k];
+    z.n[k] = c[k];
+    w.n[k] = e[k];
+  }
+  switch (op) {
+    case 0: fe_mul(r, x, y); break;
+    case 1: fe_sqr(r, x); break;
+#if CUDASP_FE_LIMBS == 9
+    case 2: fe_mul2(r, x, y, z, w); break;
+    case 3: fe_mulsqr(r, x, y, z); break;
+    case 4: fe_mul_add(r, x, y, z); break;
+    case 5: fe_sqr_add(r, x, z); break;
+#endif
+    default: return -1;
+  }
+  for (int k = 0; k < FE_LIMBS; k++) out[k] = r.n[k];
+  return 0;
+}
+
 int emu_fe_inv(const uint8_t a[32], uint8_t out[32]) {
   fe x, r;
   fe_from_bytes(x, a);

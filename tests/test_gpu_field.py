@@ -2,8 +2,10 @@
 secp256k1_fe29.hpp; on gfx950 the generated asm blocks) against Python
 integers, over the whole input range the group formulas rely on: every operand
 magnitude pair the build's layout allows (cudasp_field_layout: 10 x 26 limbs
-take mag(a) * mag(b) <= 400, 9 x 29 limbs <= 9), random limbs and every limb at
-its maximum.  The result must be congruent mod p and of magnitude 1."""
+take mag(a) * mag(b) <= 400, 9 x 29 limbs <= 7), random limbs and every limb at
+its maximum.  The 9 x 29 layout's fused forms (a b + c e, a b + c^2, a b + c,
+a^2 + c) are swept over every split of the shared budget.  The result must be
+congruent mod p and of magnitude 1."""
 import ctypes
 
 import numpy as np
@@ -53,14 +55,44 @@ def value(lay, limbs):
     return sum(int(v) << (lay["bits"] * k) for k, v in enumerate(limbs))
 
 
-def run(torch, op, a, b):
+def run(torch, op, a, b, c=None, e=None):
     from cudasp_amd import _native
     lib = _native.load()
+    if c is not None:
+        b = np.concatenate([b, c, e if e is not None else c])
     da = torch.from_numpy(a.view(np.int32).copy()).cuda()
     db = torch.from_numpy(b.view(np.int32).copy()).cuda()
     out = torch.zeros_like(da)
     _native.check(lib.cudasp_debug_field_ops(op, da.data_ptr(), db.data_ptr(), out.data_ptr(), a.shape[0]))
     return out.cpu().numpy().view(np.uint32)
+
+
+FUSED = {2: lambda a, b, c, e: a * b + c * e, 3: lambda a, b, c, e: a * b + c * c,
+         4: lambda a, b, c, e: a * b + c, 5: lambda a, b, c, e: a * a + c}
+
+
+def fused_cases(lay):
+    """(op, mag a, mag b, mag c, mag e) at the edge of the shared budget."""
+    top, lim = lay["mul_max"], lay["limb_max"]
+    cases = []
+    for s in range(1, top):
+        for ma in range(1, s + 1):
+            if s % ma:
+                continue
+            mb = s // ma
+            rest = top - s
+            for mc in range(1, rest + 1):
+                if rest % mc == 0:
+                    cases.append((2, ma, mb, mc, rest // mc))
+            for mc in range(1, lay["sqr_max"] + 1):
+                if mc * mc <= rest:
+                    cases.append((3, ma, mb, mc, 1))
+    for ma in range(1, lim + 1):
+        mb = min(lim, top // ma)
+        cases.append((4, ma, mb, lim, 1))
+    for ma in range(1, lay["sqr_max"] + 1):
+        cases.append((5, ma, 1, lim, 1))
+    return cases
 
 
 def check(lay, a, b, r, sqr):
@@ -104,3 +136,18 @@ def test_mul_reduced_edge_values(torch, layout):
     b = np.array([y for _ in rows for y in rows], dtype=np.uint32)
     check(layout, a, b, run(torch, 0, a, b), sqr=False)
     check(layout, a, a, run(torch, 1, a, a), sqr=True)
+
+
+def test_fused_magnitudes(torch, layout):
+    if layout["limbs"] != 9:
+        pytest.skip("fused forms exist in the 9 x 29 layout only")
+    for op, ma, mb, mc, me in fused_cases(layout):
+        rng = np.random.default_rng(10007 * op + 1000 * ma + 100 * mb + 10 * mc + me)
+        a, b = operands(layout, rng, ma, 512), operands(layout, rng, mb, 512)
+        c, e = operands(layout, rng, mc, 512), operands(layout, rng, me, 512)
+        r = run(torch, op, a, b, c, e)
+        assert (r.astype(np.uint64) <= limb_bounds(layout, 1)).all(), ("magnitude", op, ma, mb, mc, me)
+        f = FUSED[op]
+        for i in range(a.shape[0]):
+            want = f(value(layout, a[i]), value(layout, b[i]), value(layout, c[i]), value(layout, e[i])) % P
+            assert value(layout, r[i]) % P == want, (op, ma, mb, mc, me, i)

@@ -26,8 +26,7 @@ LAMBDA = 0x5363ad4cc05c30e0a5261c028812645a122e22ea20816678df02967c1b23bd72
 def emu(request):
     """The kernel math host-compiled once per field layout (tests/native)."""
     path = os.path.join(HERE, "native", request.param)
-    if not os.path.exists(path):
-        subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])  # rebuilds when csrc changed
     lib = ctypes.CDLL(path)
     V = ctypes.c_void_p
     lib.emu_row_values.argtypes = [V, V, V, ctypes.c_uint32, V, ctypes.c_uint32, V, V, V, V, V, V]
@@ -35,6 +34,7 @@ def emu(request):
     lib.emu_fb_layout.argtypes = [V, V, V]
     lib.emu_pend_invert.argtypes = [ctypes.c_char_p, ctypes.c_int, V]
     lib.emu_wnaf.argtypes = [V, ctypes.c_int, V, ctypes.c_int]
+    lib.emu_fe_raw_op.argtypes = [ctypes.c_int, V, V, V, V, V]
     return lib
 
 
@@ -91,6 +91,36 @@ def test_field_ops(emu):
             continue
         emu.emu_fe_inv_fermat(a.to_bytes(32, "little"), out)
         assert int.from_bytes(out.raw, "little") == pow(a, -1, P)
+
+
+def test_field_magnitude_edges(emu):
+    """The host build of the field ops at the edges of the magnitude rules
+    (same cases as tests/test_gpu_field.py), preconditions checked."""
+    import test_gpu_field as g
+    n = emu.emu_fe_limbs()
+    lay = (dict(limbs=9, bits=29, top=24, mul_max=7, sqr_max=2, limb_max=7, slack=(1 << 16, 1 << 11)) if n == 9 else
+           dict(limbs=10, bits=26, top=22, mul_max=400, sqr_max=20, limb_max=31, slack=(1 << 23, 1 << 13)))
+    out = np.zeros(n, dtype=np.uint32)
+
+    def run(op, a, b, c, e):
+        for i in range(a.shape[0]):
+            args = [np.ascontiguousarray(x[i]) for x in (a, b, c, e)]
+            assert emu.emu_fe_raw_op(op, *[x.ctypes.data for x in args], out.ctypes.data) == 0
+            assert (out.astype(np.uint64) <= g.limb_bounds(lay, 1)).all(), op
+            va, vb, vc, ve = (g.value(lay, x) for x in args)
+            want = g.FUSED[op](va, vb, vc, ve) if op >= 2 else (va * vb if op == 0 else va * va)
+            assert g.value(lay, out) % P == want % P, (op, i)
+
+    rng = np.random.default_rng(5)
+    for ma, mb in g.mag_pairs(lay):
+        a, b = g.operands(lay, rng, ma, 16), g.operands(lay, rng, mb, 16)
+        run(0, a, b, a, a)
+    for m in range(1, lay["sqr_max"] + 1):
+        a = g.operands(lay, rng, m, 16)
+        run(1, a, a, a, a)
+    if n == 9:
+        for op, ma, mb, mc, me in g.fused_cases(lay):
+            run(op, *(g.operands(lay, rng, m, 8) for m in (ma, mb, mc, me)))
 
 
 def test_glv_split(emu):

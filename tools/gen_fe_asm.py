@@ -157,6 +157,31 @@ def product_terms_l(lay, k, sqr):
 
 def gen_layout(lay, sqr):
     """gen() for any Layout (serial schedule)."""
+    return gen_layout_terms(lay, lambda k: product_terms_l(lay, k, sqr))
+
+
+def spec_terms(lay, k, spec):
+    """Column k's terms of a sum of products: spec = [("mul", x, y) |
+    ("sqr", x, d)] with operand prefixes (d = the doubled limbs of x)."""
+    t = []
+    for kind, x, y in spec:
+        for i in range(lay.n):
+            j = k - i
+            if j < 0 or j >= lay.n:
+                continue
+            if kind == "mul":
+                t.append(("%%[%s%d]" % (x, i), "%%[%s%d]" % (y, j)))
+            elif j > i:
+                t.append(("%%[%s%d]" % (y, i), "%%[%s%d]" % (x, j)))
+            elif j == i:
+                t.append(("%%[%s%d]" % (x, i), "%%[%s%d]" % (x, i)))
+    return t
+
+
+def gen_layout_terms(lay, col_terms, addend=None):
+    """Serial schedule of one reduced sum of products: col_terms(k) gives
+    product column k's (x, y) operand pairs; addend (an operand prefix) is a
+    field element added into the low columns (one mad by 1 per limb)."""
     n = lay.n
     ins = []
     H = [2 * m for m in range(n - 1)]
@@ -165,7 +190,7 @@ def gen_layout(lay, sqr):
     def mad(dst, x, y, acc):
         ins.append("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (dst, x, y, acc))
 
-    cols = [product_terms_l(lay, n + m, sqr) for m in range(n - 1)]
+    cols = [col_terms(n + m) for m in range(n - 1)]
     depth = max(len(c) for c in cols)
     for d in range(depth):
         for m in range(n - 1):
@@ -189,7 +214,9 @@ def gen_layout(lay, sqr):
             terms.append((hi(H[k - 2]), "%[r1s]"))
         if k == 2 and lay.top_has_hi:
             terms.append((hi(W), "%[r1s]"))
-        terms += product_terms_l(lay, k, sqr)
+        terms += col_terms(k)
+        if addend is not None:
+            terms.append(("%%[%s%d]" % (addend, k), "1"))
         for m_, (x, y) in enumerate(terms):
             mad(pair(ACC), x, y, "0" if (k == 0 and m_ == 0) else pair(ACC))
         if k == 0:
@@ -240,6 +267,48 @@ def emit_layout(lay, name, sqr):
             "  const uint32_t c_f0 = opaque_const(F0), c_f0s = opaque_const(F0 << %d);\n"
             "  asm(\n%s\n      : %s\n      : %s\n      : %s);\n}\n"
             % (name, sig, pre, lay.s, lay.s, lay.s, body, outs, ",\n        ".join(inl), clob)), len(ins), ntmp
+
+
+def emit_fused(lay, name, spec, addend=None):
+    """One asm block for a reduced sum of products (+ an addend): spec as in
+    spec_terms with single-letter operand names that are also the C
+    parameter names; a "sqr" entry's doubled limbs are formed outside the
+    block."""
+    n = lay.n
+    ins, ntmp = gen_layout_terms(lay, lambda k: spec_terms(lay, k, spec), addend)
+    body = "\n".join('      "%s\\n"' % s for s in ins)
+    outs = ", ".join('[o%d] "=&v"(r.n[%d])' % (k, k) for k in range(n))
+    params, inl, pre = [], [], ""
+    for kind, x, y in spec:
+        for v in (x,) if kind == "sqr" else (x, y):
+            if v not in params:
+                params.append(v)
+        if kind == "sqr":
+            pre += "  uint32_t %s[%d];\n#pragma unroll\n  for (int i = 0; i < %d; i++) %s[i] = %s.n[i] << 1;\n" % (
+                y, n - 1, n - 1, y, x)
+            inl += ['[%s%d] "v"(%s[%d])' % (y, i, y, i) for i in range(n - 1)]
+    if addend is not None:
+        params.append(addend)
+    inl = ['[%s%d] "v"(%s.n[%d])' % (v, i, v, i) for v in params for i in range(n)] + inl
+    inl += ['[r0] "s"(c_r0)', '[r1] "s"(c_r1)', '[r0s] "s"(c_r0s)', '[r1s] "s"(c_r1s)', '[f0] "s"(c_f0)',
+            '[f0s] "s"(c_f0s)']
+    clob = ", ".join(['"vcc"'] + ['"v%d"' % (BASE + i) for i in range(ntmp)])
+    sig = "fe& r, " + ", ".join("const fe& %s" % v for v in params)
+    return ("__device__ __forceinline__ void %s(%s) {\n%s"
+            "  const uint32_t c_r0 = opaque_const(R0), c_r1 = opaque_const(R1);\n"
+            "  const uint32_t c_r0s = opaque_const(R0 << %d), c_r1s = opaque_const(R1 << %d);\n"
+            "  const uint32_t c_f0 = opaque_const(F0), c_f0s = opaque_const(F0 << %d);\n"
+            "  asm(\n%s\n      : %s\n      : %s\n      : %s);\n}\n"
+            % (name, sig, pre, lay.s, lay.s, lay.s, body, outs, ",\n        ".join(inl), clob)), len(ins)
+
+
+# Fused 9 x 29 operations (secp256k1_fe29.hpp): name, products, addend.
+FUSED29 = [
+    ("fe_mul2_asm", [("mul", "a", "b"), ("mul", "c", "e")], None),   # a b + c e
+    ("fe_mulsqr_asm", [("mul", "a", "b"), ("sqr", "c", "g")], None),  # a b + c^2
+    ("fe_mul_add_asm", [("mul", "a", "b")], "c"),                     # a b + c
+    ("fe_sqr_add_asm", [("sqr", "a", "d")], "c"),                     # a^2 + c
+]
 
 
 def interleave(a, b):
@@ -372,9 +441,13 @@ def main():
     print("wrote %s: serial mul %d / sqr %d, pipelined mul %d / sqr %d instructions" % (OUT, nm, ns, pnm, pns))
     m29, n29m, t29 = emit_layout(L29, "fe_mul_asm", False)
     s29, n29s, _ = emit_layout(L29, "fe_sqr_asm", True)
+    fused = [emit_fused(L29, name, spec, add) for name, spec, add in FUSED29]
     text = ("// GENERATED by tools/gen_fe_asm.py -- do not edit; regenerate and commit both.\n"
             "// 9 x 29-bit limbs: fe_mul %d instructions, fe_sqr %d (+8 doublings outside the block),\n"
-            "// temporaries v%d..v%d and vcc (clobbered).\n\n" % (n29m, n29s, BASE, BASE + t29 - 1)) + m29 + "\n" + s29
+            "// fused: %s;\n"
+            "// temporaries v%d..v%d and vcc (clobbered).\n\n"
+            % (n29m, n29s, ", ".join("%s %d" % (f[0], c) for f, (_, c) in zip(FUSED29, fused)), BASE,
+               BASE + t29 - 1)) + m29 + "\n" + s29 + "".join("\n" + t for t, _ in fused)
     with open(OUT29, "w") as f:
         f.write(text)
     print("wrote %s: mul %d / sqr %d instructions" % (OUT29, n29m, n29s))
