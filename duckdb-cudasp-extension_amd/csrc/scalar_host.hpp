@@ -7,6 +7,7 @@
 // (GLV): d = k1 + k2 * lambda (mod n) with |k1|, |k2| < 2^129, and each half is
 // recoded to width-5 NAF.  The kernel then does ~129 doublings instead of 256.
 #pragma once
+#include <vector>
 #include <stdint.h>
 #include <string.h>
 
@@ -137,9 +138,9 @@ struct SignedHalf {
   bool neg;
 };
 
-// d = k1 + k2 * lambda (mod n).  Exact integer arithmetic on 288-bit two's
-// complement values; |k1|, |k2| come out below 2^129.
-static inline void glv_split(const Big<8>& d_in, SignedHalf& k1, SignedHalf& k2) {
+// d = k1 + k2 * lambda (mod n) by Babai rounding against the reduced lattice
+// basis, as two's complement 288-bit values r1 = k1, r2 = k2 (|k_i| < 2^129).
+static inline void glv_split_raw(const Big<8>& d_in, Big<9>& r1, Big<9>& r2) {
   GlvConsts c;
   Big<8> d = scalar_reduce(d_in);
   Big<8> c1 = mul_shift_384(d, c.g1);
@@ -149,21 +150,38 @@ static inline void glv_split(const Big<8>& d_in, SignedHalf& k1, SignedHalf& k2)
   Big<9> c2a2 = big_resize<9>(big_mul(big_resize<4>(c2), big_resize<5>(c.a2)));
   Big<9> c1b1 = big_resize<9>(big_mul(big_resize<4>(c1), big_resize<5>(c.minus_b1)));
   Big<9> c2b2 = big_resize<9>(big_mul(big_resize<4>(c2), big_resize<5>(c.b2)));
-  Big<9> r1 = big_resize<9>(d), r2;
+  r1 = big_resize<9>(d);
   big_sub(r1, r1, c1a1);
   big_sub(r1, r1, c2a2);   // k1 = d - c1 a1 - c2 a2
   big_sub(r2, c1b1, c2b2); // k2 = -c1 b1 - c2 b2 = c1 (-b1) - c2 b2
-  auto to_signed = [](const Big<9>& v, SignedHalf& out) {
-    out.neg = (v.w[8] >> 31) != 0;
-    Big<9> m = v;
-    if (out.neg) {
-      Big<9> z = big_zero<9>();
-      big_sub(m, z, v);
-    }
-    out.mag = big_resize<8>(m);
-  };
-  to_signed(r1, k1);
-  to_signed(r2, k2);
+}
+
+static inline void to_signed_half(const Big<9>& v, SignedHalf& out) {
+  out.neg = (v.w[8] >> 31) != 0;
+  Big<9> m = v;
+  if (out.neg) {
+    Big<9> z = big_zero<9>();
+    big_sub(m, z, v);
+  }
+  out.mag = big_resize<8>(m);
+}
+
+static inline void glv_split(const Big<8>& d_in, SignedHalf& k1, SignedHalf& k2) {
+  Big<9> r1, r2;
+  glv_split_raw(d_in, r1, r2);
+  to_signed_half(r1, k1);
+  to_signed_half(r2, k2);
+}
+
+// r += m * v for a small signed m.
+static inline void big_add_small_multiple(Big<9>& r, const Big<8>& v, int m) {
+  Big<9> w = big_resize<9>(v);
+  for (int i = 0; i < (m < 0 ? -m : m); i++) {
+    if (m > 0)
+      big_add(r, r, w);
+    else
+      big_sub(r, r, w);
+  }
 }
 
 // Width-w NAF of a non-negative integer (< 2^256); digits[i] is the digit of
@@ -196,6 +214,64 @@ static inline int wnaf(int8_t* digits, int max_digits, const Big<8>& k_in, int w
     i++;
   }
   return len;
+}
+
+// Stage-A ladder cost of one operation (VALU instructions per doubling and per
+// mixed addition incl. its table load, gfx950 build of secp256k1_group29.hpp);
+// used to rank decompositions of the scan key.
+constexpr int LADDER_DBL_COST = 962;
+constexpr int LADDER_ADD_COST = 1560;
+
+// The uniform signed digits of the stage-A ladder for scan key d: d = k1 +
+// k2 lambda (mod n), k1 and k2 each as a width-5 NAF (digits of k_i in
+// naf[i * naf_max ..], signs applied), naf_len = the longer length.  Every
+// lattice point (k1, k2) + i (a1, b1) + j (a2, b2) with |i|, |j| <= search
+// represents the same d; the kernels pay (naf_len - 1) doublings and
+// (weight - 1) additions, so the cheapest of those is taken (the Babai
+// point (0, 0) on ties).  The choice is per query and costs ~300 wNAF
+// recodings on the host.  Returns 0, or -1 if no candidate fits naf_max.
+static inline int scan_digits(const Big<8>& d, int8_t* naf, int naf_max, uint32_t* naf_len, int search = 8) {
+  GlvConsts c;
+  Big<9> r1, r2;
+  glv_split_raw(d, r1, r2);
+  std::vector<int8_t> t(2 * (size_t)naf_max);
+  long best = -1;
+  int order[2 * 64 + 1];
+  int m = 0;
+  order[m++] = 0;
+  for (int k = 1; k <= search && k <= 64; k++) {
+    order[m++] = k;
+    order[m++] = -k;
+  }
+  for (int ii = 0; ii < m; ii++) {
+    for (int jj = 0; jj < m; jj++) {
+      int i = order[ii], j = order[jj];
+      Big<9> v1 = r1, v2 = r2;
+      big_add_small_multiple(v1, c.a1, i);
+      big_add_small_multiple(v1, c.a2, j);
+      big_add_small_multiple(v2, c.minus_b1, -i);
+      big_add_small_multiple(v2, c.b2, j);
+      SignedHalf k1, k2;
+      to_signed_half(v1, k1);
+      to_signed_half(v2, k2);
+      int l1 = wnaf(t.data(), naf_max, k1.mag, 5);
+      int l2 = wnaf(t.data() + naf_max, naf_max, k2.mag, 5);
+      if (l1 < 0 || l2 < 0) continue;
+      int weight = 0;
+      for (int q = 0; q < 2 * naf_max; q++) weight += t[q] != 0;
+      int len = l1 > l2 ? l1 : l2;
+      if (weight == 0) continue;
+      long cost = (long)(len - 1) * LADDER_DBL_COST + (long)(weight - 1) * LADDER_ADD_COST;
+      if (best >= 0 && cost >= best) continue;
+      best = cost;
+      for (int q = 0; q < naf_max; q++) {
+        naf[q] = k1.neg ? (int8_t)-t[q] : t[q];
+        naf[naf_max + q] = k2.neg ? (int8_t)-t[naf_max + q] : t[naf_max + q];
+      }
+      *naf_len = (uint32_t)len;
+    }
+  }
+  return best >= 0 ? 0 : -1;
 }
 
 }  // namespace host

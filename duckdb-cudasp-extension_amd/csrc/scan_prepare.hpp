@@ -171,22 +171,15 @@ inline int prepare_scan(const uint8_t scan_private_key[32], const uint8_t spend_
     err = "scan_private_key is 0 mod n";
     return CUDASP_ERR_INVALID_ARG;
   }
-  host::SignedHalf k1, k2;
-  host::glv_split(d, k1, k2);
   naf.assign(2 * NAF_MAX, 0);
-  int len1 = host::wnaf(naf.data(), NAF_MAX, k1.mag, 5);
-  int len2 = host::wnaf(naf.data() + NAF_MAX, NAF_MAX, k2.mag, 5);
-  if (len1 < 0 || len2 < 0) {
+  uint32_t naf_len = 0;
+  if (host::scan_digits(d, naf.data(), NAF_MAX, &naf_len) != 0) {
     err = "GLV split out of range";
     return CUDASP_ERR_INVALID_ARG;
   }
-  for (int i = 0; i < NAF_MAX; i++) {
-    if (k1.neg) naf[i] = (int8_t)-naf[i];
-    if (k2.neg) naf[NAF_MAX + i] = (int8_t)-naf[NAF_MAX + i];
-  }
   memset(&k, 0, sizeof(k));
   bip352_midstate(k.mid);
-  k.naf_len = (uint32_t)(len1 > len2 ? len1 : len2);
+  k.naf_len = naf_len;
   k.label_count = label_count;
   const GenPowers& gp = gen_powers();
   HPoint co = gp.q[FB_WINDOWS];

@@ -160,10 +160,49 @@ CUDASP_HD void fe_sub(fe& r, const fe& a, const fe& b) {
   FE_CHECK_SUM(r, "sub");
 }
 
+#ifndef CUDASP_NORM_PAR
+#define CUDASP_NORM_PAR 0
+#endif
+
 // Carry-propagate and fold the bits above 2^256 once (inputs of magnitude
-// <= 7).  Output magnitude 1 with limbs 0..7 < 2^29.
+// <= 7).  Output magnitude 1.  Serial form: limbs 0..7 < 2^29.  Parallel form
+// (CUDASP_NORM_PAR): every limb keeps its low bits plus the carry of the limb
+// below (<= 7, or 7 * 0x3D1 into limb 0), so the result is within magnitude
+// 1's slack (limbs <= 2^29 + 2^13) and the nine carries are independent.
 CUDASP_HD void fe_normalize_weak(fe& r) {
   FE_CHECK_SUM(r, "normalize_weak");
+#if CUDASP_NORM_PAR
+  {
+    uint32_t c[9];
+#pragma unroll
+    for (int i = 0; i < 8; i++) c[i] = r.n[i] >> 29;
+    c[8] = r.n[8] >> 24;
+    r.n[0] = (r.n[0] & M29) + c[8] * F0;
+    r.n[1] = (r.n[1] & M29) + c[0] + (c[8] << 3);
+#pragma unroll
+    for (int i = 2; i < 8; i++) r.n[i] = (r.n[i] & M29) + c[i - 1];
+    r.n[8] = (r.n[8] & M24) + c[7];
+    return;
+  }
+#endif
+  uint32_t t[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) t[i] = r.n[i];
+  uint32_t x = t[8] >> 24;
+  t[8] &= M24;
+  t[0] += x * F0;
+  t[1] += x << 3;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    t[i + 1] += t[i] >> 29;
+    t[i] &= M29;
+  }
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.n[i] = t[i];
+}
+
+// Serial carry propagation (limbs 0..7 < 2^29 afterwards).
+CUDASP_HD void fe_normalize_weak_serial(fe& r) {
   uint32_t t[9];
 #pragma unroll
   for (int i = 0; i < 9; i++) t[i] = r.n[i];
@@ -182,8 +221,9 @@ CUDASP_HD void fe_normalize_weak(fe& r) {
 
 // Full normalization to the canonical representative in [0, p).
 CUDASP_HD void fe_normalize(fe& r) {
-  fe_normalize_weak(r);
-  fe_normalize_weak(r);
+  FE_CHECK_SUM(r, "normalize");
+  fe_normalize_weak_serial(r);
+  fe_normalize_weak_serial(r);
   // r >= p  <=>  r + 0x1000003D1 >= 2^256.
   uint32_t t[9];
   uint32_t c = 0;

@@ -184,6 +184,14 @@ int emu_glv_split(const uint8_t k[32], uint8_t k1[32], int* neg1, uint8_t k2[32]
   return 0;
 }
 
+// The ladder digits of scan key k (host::scan_digits): naf[2 * max_digits].
+int emu_scan_digits(const uint8_t k[32], int search, int8_t* naf, int max_digits, uint32_t* naf_len) {
+  host::Big<8> d = host::big_zero<8>();
+  for (int i = 0; i < 32; i++) d.w[i / 4] |= (uint32_t)k[i] << (8 * (i % 4));
+  d = host::scalar_reduce(d);
+  return host::scan_digits(d, naf, max_digits, naf_len, search);
+}
+
 int emu_wnaf(const uint8_t k[32], int w, int8_t* digits, int max_digits) {
   host::Big<8> d = host::big_zero<8>();
   for (int i = 0; i < 32; i++) d.w[i / 4] |= (uint32_t)k[i] << (8 * (i % 4));
@@ -247,18 +255,11 @@ int emu_shared_secret(const uint8_t scan[32], const uint8_t* tweaks, uint32_t n,
   for (int i = 0; i < 32; i++) d.w[i / 4] |= (uint32_t)scan[i] << (8 * (i % 4));
   d = host::scalar_reduce(d);
   if (host::big_is_zero(d)) return CUDASP_ERR_INVALID_ARG;
-  host::SignedHalf k1, k2;
-  host::glv_split(d, k1, k2);
   naf.assign(2 * NAF_MAX, 0);
-  int len1 = host::wnaf(naf.data(), NAF_MAX, k1.mag, 5);
-  int len2 = host::wnaf(naf.data() + NAF_MAX, NAF_MAX, k2.mag, 5);
-  for (int i = 0; i < NAF_MAX; i++) {
-    if (k1.neg) naf[i] = (int8_t)-naf[i];
-    if (k2.neg) naf[NAF_MAX + i] = (int8_t)-naf[NAF_MAX + i];
-  }
+  uint32_t naf_len = 0;
+  if (host::scan_digits(d, naf.data(), NAF_MAX, &naf_len) != 0) return CUDASP_ERR_INVALID_ARG;
   uint32_t mid[8];
   bip352_midstate(mid);
-  uint32_t naf_len = (uint32_t)(len1 > len2 ? len1 : len2);
   std::vector<uint32_t> scratch(VB_SCRATCH_WORDS);
   Scratch sc{scratch.data(), 1, 0};
   for (uint32_t r = 0; r < n; r++) {

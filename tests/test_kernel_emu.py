@@ -148,6 +148,40 @@ def test_wnaf(emu):
         assert ln == (nz[-1] + 1 if nz else 0)
 
 
+def test_scan_digits(emu):
+    """The ladder digits (scalar_host.hpp scan_digits): any lattice point
+    searched must still represent d = k1 + k2 lambda (mod n) as two width-5
+    NAFs, and the chosen one costs no more than the Babai split (search 0)."""
+    rng = random.Random(21)
+    M = 136
+    naf = (ctypes.c_int8 * (2 * M))()
+    ln = ctypes.c_uint32()
+    emu.emu_scan_digits.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    sc = golden_io.load("sql_cases.json")
+    keys = [int.from_bytes(bytes.fromhex(sc["queries"][0]["scan_key"]), "little"), 1, 2, N - 1, LAMBDA]
+    keys += [rng.randrange(1, N) for _ in range(60)]
+    saved = 0
+    for d in keys:
+        costs = []
+        for search in (0, 8):
+            assert emu.emu_scan_digits(d.to_bytes(32, "little"), search, naf, M, ctypes.byref(ln)) == 0
+            dg = list(naf)
+            k1 = sum(x << i for i, x in enumerate(dg[:M]))
+            k2 = sum(x << i for i, x in enumerate(dg[M:]))
+            assert (k1 + k2 * LAMBDA - d) % N == 0
+            for half in (dg[:M], dg[M:]):
+                nz = [i for i, x in enumerate(half) if x]
+                assert all(half[i] % 2 and -16 < half[i] < 16 for i in nz)
+                assert all(b - a >= 5 for a, b in zip(nz, nz[1:]))
+            top = max([i + 1 for i, x in enumerate(dg[:M]) if x] + [i + 1 for i, x in enumerate(dg[M:]) if x])
+            assert ln.value == top
+            weight = sum(1 for x in dg if x)
+            costs.append((ln.value - 1) * 962 + (weight - 1) * 1560)
+        assert costs[1] <= costs[0]
+        saved += costs[0] - costs[1]
+    assert saved > 0
+
+
 def fb_layout(emu):
     bits, windows, entries = ctypes.c_int(), ctypes.c_int(), ctypes.c_uint32()
     emu.emu_fb_layout(ctypes.byref(bits), ctypes.byref(windows), ctypes.byref(entries))
