@@ -102,6 +102,10 @@ CUDASP_HD void scr_load(fe& a, const Scratch& sc, int base) {
 // Scratch layout of stage A (u32 words per row).
 // (FE_LIMBS words per field element)
 constexpr int FW = FE_LIMBS;
+// Stage-A ladder in the doubled-Y form (secp256k1_group29.hpp, 9 x 29 only).
+#ifndef LADDER_YH
+#define LADDER_YH (CUDASP_FE_LIMBS == 9)
+#endif
 constexpr int VB_ENTRY_X(int e) { return e * 2 * FW; }
 constexpr int VB_ENTRY_Y(int e) { return e * 2 * FW + FW; }
 constexpr int VB_ZR(int i) { return VB_ENTRIES * 2 * FW + i * FW; }
@@ -153,6 +157,9 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
       if (e == VB_ENTRIES - 1) {  // the only entry not rescaled below
         fe_normalize_weak(acc.x);
         fe_normalize_weak(acc.y);
+#if LADDER_YH
+        fe_add(acc.y, acc.y, acc.y);
+#endif
 #if CUDASP_PHI_TABLE
         fe xb;
         fe_mul(xb, acc.x, beta);
@@ -175,6 +182,9 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
       fe_sqr(r2, ratio);
       fe_mul(r3, r2, ratio);
       fe_mul(x, x, r2);
+#if LADDER_YH
+      fe_add(r3, r3, r3);  // entries hold 2y (the ladder's Yh form)
+#endif
       fe_mul(y, y, r3);
       scr_store(sc, VB_ENTRY_X(e), x);
       scr_store(sc, VB_ENTRY_Y(e), y);
@@ -191,9 +201,20 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
   }
 
   // --- S'' = k1*T'' + k2*phi(T'') with uniform NAF digits -------------------
+  // LADDER_YH: R holds (X, 2Y, Z) of sgn * R_true; the doubling returns the
+  // negated double, so sgn flips with every doubling and an addition adds the
+  // entry with its digit's sign times sgn (wave-uniform, like the digits).
   bool inf = true;
+  bool sgn_neg = false;
   for (int i = (int)naf_len - 1; i >= 0; --i) {
+#if LADDER_YH
+    if (!inf) {
+      gej_double_neg_yh(R, R);
+      sgn_neg = !sgn_neg;
+    }
+#else
     if (!inf) gej_double(R, R);
+#endif
 #pragma unroll
     for (int half = 0; half < 2; half++) {
       int d = uniform_digit(naf, half * NAF_MAX + i);
@@ -207,6 +228,16 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
         if (half) fe_mul(P.x, P.x, beta);
 #endif
         scr_load(P.y, sc, VB_ENTRY_Y(e));
+#if LADDER_YH
+        if ((d < 0) != sgn_neg) fe_negate<2>(P.y, P.y);
+        if (inf) {
+          gej_set_ge(R, P);
+          fe_normalize_weak(R.y);
+          inf = false;
+        } else {
+          gej_add_ge_yh(R, R, P);
+        }
+#else
         if (d < 0) ge_neg(P, P);
         if (inf) {
           gej_set_ge(R, P);
@@ -214,9 +245,14 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
         } else {
           gej_add_ge(R, R, P);
         }
+#endif
       }
     }
   }
+#if LADDER_YH
+  fe_half(R.y, R.y);                              // Y = Yh / 2
+  if (sgn_neg) fe_negate<2>(R.y, R.y);            // R_true
+#endif
 
 
   // --- back to the original curve: Z times the common table Z -------------

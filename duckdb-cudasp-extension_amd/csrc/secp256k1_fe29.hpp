@@ -250,8 +250,10 @@ CUDASP_HD void fe_half(fe& r, const fe& a) {
 #pragma unroll
   for (int i = 2; i < 8; i++) t[i] = a.n[i] + (M29 & odd);
   t[8] = a.n[8] + (M24 & odd);
+  // (t_i + (t_(i+1) mod 2) 2^29) / 2: and, shift-add, shift per limb
+  // (t_i <= 2^30 + 2^15, so the sum stays below 2^32).
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.n[i] = (t[i] >> 1) + ((t[i + 1] & 1u) << 28);
+  for (int i = 0; i < 8; i++) r.n[i] = (t[i] + ((t[i + 1] & 1u) << 29)) >> 1;
   r.n[8] = t[8] >> 1;
 }
 
@@ -391,6 +393,21 @@ CUDASP_HD void fe_mulsqr(fe& r, const fe& a, const fe& b, const fe& c) {
   uint64_t col[17] = {};
   fe29_mul_columns(col, a, b);
   fe29_sqr_columns(col, c);
+  fe29_reduce_columns(r, col);
+#endif
+}
+
+// r = 3 a^2 (mag(a) <= 1: the columns of 3 a^2 fit like a product of
+// magnitude 3); the squares' operand is 3 a, the cross products' 6 a.
+CUDASP_HD void fe_sqr3(fe& r, const fe& a) {
+  FE_CHECK_MUL2(a, a, a, a, "sqr3");  // 2 m^2 <= 7 <=> m = 1 (3 m^2 <= 7)
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_sqr3_asm(r, a);
+#else
+  uint64_t col[17] = {};
+  fe29_sqr_columns(col, a);
+#pragma unroll
+  for (int k = 0; k < 17; k++) col[k] *= 3;
   fe29_reduce_columns(r, col);
 #endif
 }

@@ -32,16 +32,14 @@ CUDASP_HD void gej_double(gej& r, const gej& a) {
   FE_CHECK(a.z, 2, "dbl z");
   fe_mul(r.z, a.z, a.y);   // Z3 = Y1 Z1                         2 * 2 -> (1)
   fe_sqr(S, a.y);          // S = Y1^2                           (1)
-  fe_sqr(L, a.x);          //                                    (1)
-  fe_mul_int(L, L, 3);     //                                    (3)
-  fe_half(L, L);           // L = 3/2 X1^2                       (2.5)
-  fe_normalize_weak(L);    //                                    (1)
+  fe_sqr3(L, a.x);         // 3 X1^2                             (1)
+  fe_half(L, L);           // L = 3/2 X1^2                       (2)
   fe_mul(T, S, a.x);       //                                    (1)
   fe_negate<1>(T, T);      // T = -X1 S                          (2)
   fe_add(U, T, T);         // 2T                                 (4)
   fe_sqr_add(r.x, L, U);   // X3 = L^2 + 2T                      (1)
   fe_add(U, r.x, T);       // X3 + T                             (3)
-  fe_mulsqr(r.y, L, U, S); // L (X3 + T) + S^2                   1 * 3 + 1 -> (1)
+  fe_mulsqr(r.y, L, U, S); // L (X3 + T) + S^2                   2 * 3 + 1 -> (1)
   fe_negate<1>(r.y, r.y);  // Y3                                 (2)
 }
 
@@ -73,6 +71,61 @@ CUDASP_HD void gej_add_ge(gej& r, const gej& a, const ge& b, fe* zr = nullptr) {
   fe_sqr_add(r.x, rr, w);          // X3 = R^2 - HHH - 2V             (1)
   fe_sub<1>(v, v, r.x);            // V - X3                          (3)
   fe_mul2(r.y, rr, v, ny, hhh);    // Y3 = R (V - X3) - Y1 HHH        1 * 3 + 3 * 1 -> (1)
+}
+
+// ---- Stage-A ladder forms: Y kept doubled ("Yh" = 2Y), sign tracked outside.
+// The doubling then needs no halving (M = 3 X^2 instead of 3/2 X^2) and no
+// final negation: it returns -2Q.  The mixed addition halves R once instead.
+// A stored triple (X, Yh, Z) stands for the Jacobian point Q = (X, Yh / 2, Z).
+
+// r = -2a (Yh form).  Input: x <= 1, yh <= 2, z <= 2.  Output: (1, 1, 1).
+// Z3 = Yh Z (= 2 Y Z), A = Yh^2 (= 4 Y^2), B = X A (= 4 X Y^2), M = 3 X^2,
+// X3 = M^2 - 2 B, Yh3 = 2 M (X3 - B) + A^2 (= -2 Y3).  r may alias a.
+CUDASP_HD void gej_double_neg_yh(gej& r, const gej& a) {
+  fe A, M, B, w;
+  FE_CHECK(a.x, 1, "dblh x");
+  FE_CHECK(a.y, 2, "dblh y");
+  FE_CHECK(a.z, 2, "dblh z");
+  fe_mul(r.z, a.z, a.y);    // Z3 = Yh Z                          (1)
+  fe_sqr(A, a.y);           // A = Yh^2                           (1)
+  fe_sqr3(M, a.x);          // M = 3 X^2                          (1)
+  fe_mul(B, a.x, A);        // B = X A                            (1)
+  fe_negate<1>(w, B);
+  fe_add(w, w, w);          // -2B                                (4)
+  fe_sqr_add(r.x, M, w);    // X3 = M^2 - 2B                      (1)
+  fe_sub<1>(w, r.x, B);     // X3 - B                             (3)
+  fe_add(M, M, M);          // 2M                                 (2)
+  fe_mulsqr(r.y, M, w, A);  // Yh3' = 2M (X3 - B) + A^2           2 * 3 + 1 -> (1)
+}
+
+// r = a + b (Yh form, b affine with yh = 2y, possibly negated).  Input:
+// a = (1, 1, 2), b = (1, 3).  Output (1, 1, 1).  H = X2 Z1^2 - X1,
+// R' = Yh2 Z1^3 - Yh1 (= 2R), R = R' / 2, X3 = R^2 - HHH - 2V,
+// Yh3 = R' (V - X3) - Yh1 HHH, Z3 = Z1 H.  r may alias a.
+CUDASP_HD void gej_add_ge_yh(gej& r, const gej& a, const ge& b) {
+  fe z1z1, z1z1z1, t, h, rr, r1, hh, hhh, v, ny, w;
+  FE_CHECK(a.x, 1, "addh a.x");
+  FE_CHECK(a.y, 1, "addh a.y");
+  FE_CHECK(a.z, 2, "addh a.z");
+  FE_CHECK(b.x, 1, "addh b.x");
+  FE_CHECK(b.y, 3, "addh b.y");
+  fe_sqr(z1z1, a.z);               // Z1^2                            (1)
+  fe_mul(z1z1z1, z1z1, a.z);       // Z1^3                            (1)
+  fe_negate<1>(t, a.x);            // -X1                             (2)
+  fe_mul_add(h, b.x, z1z1, t);     // H = X2 Z1^2 - X1                (1)
+  fe_negate<1>(ny, a.y);           // -Yh1                            (2)
+  fe_mul_add(rr, b.y, z1z1z1, ny); // R' = Yh2 Z1^3 - Yh1             3 * 1 -> (1)
+  fe_half(r1, rr);                 // R                               (2)
+  fe_mul(r.z, a.z, h);             // Z3 = Z1 H                       (1)
+  fe_sqr(hh, h);                   // HH                              (1)
+  fe_mul(hhh, h, hh);              // HHH                             (1)
+  fe_mul(v, a.x, hh);              // V = X1 HH                       (1)
+  fe_add(w, v, v);
+  fe_add_to(w, hhh);               // HHH + 2V                        (3)
+  fe_negate<3>(w, w);              //                                 (4)
+  fe_sqr_add(r.x, r1, w);          // X3 = R^2 - HHH - 2V             (1)
+  fe_sub<1>(v, v, r.x);            // V - X3                          (3)
+  fe_mul2(r.y, rr, v, ny, hhh);    // Yh3 = R' (V - X3) - Yh1 HHH     1 * 3 + 2 * 1 -> (1)
 }
 
 // Co-Z initial doubling with update: for an affine, normalized T, d = 2T and

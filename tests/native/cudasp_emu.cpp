@@ -122,7 +122,8 @@ int emu_fe_sqr(const uint8_t a[32], uint8_t out[32]) {
 int emu_fe_limbs(void) { return FE_LIMBS; }
 
 // Raw-limb field ops (magnitude preconditions checked): op 0 a*b, 1 a^2; the
-// 9 x 29 layout's fused forms 2 a*b + c*e, 3 a*b + c^2, 4 a*b + c, 5 a^2 + c.
+// 9 x 29 layout's fused forms 2 a*b + c*e, 3 a*b + c^2, 4 a*b + c, 5 a^2 + c,
+// 6 3 a^2.
 int emu_fe_raw_op(int op, const uint32_t* a, const uint32_t* b, const uint32_t* c, const uint32_t* e,
                   uint32_t* out) {
   fe x, y, z, w, r;
@@ -140,6 +141,7 @@ int emu_fe_raw_op(int op, const uint32_t* a, const uint32_t* b, const uint32_t* 
     case 3: fe_mulsqr(r, x, y, z); break;
     case 4: fe_mul_add(r, x, y, z); break;
     case 5: fe_sqr_add(r, x, z); break;
+    case 6: fe_sqr3(r, x); break;
 #endif
     default: return -1;
   }

@@ -4,7 +4,7 @@ integers, over the whole input range the group formulas rely on: every operand
 magnitude pair the build's layout allows (cudasp_field_layout: 10 x 26 limbs
 take mag(a) * mag(b) <= 400, 9 x 29 limbs <= 7), random limbs and every limb at
 its maximum.  The 9 x 29 layout's fused forms (a b + c e, a b + c^2, a b + c,
-a^2 + c) are swept over every split of the shared budget.  The result must be
+a^2 + c, 3 a^2) are swept over every split of the shared budget.  The result must be
 congruent mod p and of magnitude 1."""
 import ctypes
 
@@ -68,7 +68,7 @@ def run(torch, op, a, b, c=None, e=None):
 
 
 FUSED = {2: lambda a, b, c, e: a * b + c * e, 3: lambda a, b, c, e: a * b + c * c,
-         4: lambda a, b, c, e: a * b + c, 5: lambda a, b, c, e: a * a + c}
+         4: lambda a, b, c, e: a * b + c, 5: lambda a, b, c, e: a * a + c, 6: lambda a, b, c, e: 3 * a * a}
 
 
 def fused_cases(lay):
@@ -92,6 +92,7 @@ def fused_cases(lay):
         cases.append((4, ma, mb, lim, 1))
     for ma in range(1, lay["sqr_max"] + 1):
         cases.append((5, ma, 1, lim, 1))
+    cases.append((6, 1, 1, 1, 1))
     return cases
 
 

@@ -162,7 +162,10 @@ def gen_layout(lay, sqr):
 
 def spec_terms(lay, k, spec):
     """Column k's terms of a sum of products: spec = [("mul", x, y) |
-    ("sqr", x, d)] with operand prefixes (d = the doubled limbs of x)."""
+    ("sqr", x, d) | ("sqr3", x, q)] with operand prefixes: d = the doubled
+    limbs of x; for 3 x^2, q = 6 x for the cross products and q + "h" = 3 x
+    for the squares.  (Prefixes must not collide with the constants' names
+    r0, r1, r0s, r1s, f0, f0s or the outputs o0...)"""
     t = []
     for kind, x, y in spec:
         for i in range(lay.n):
@@ -174,7 +177,8 @@ def spec_terms(lay, k, spec):
             elif j > i:
                 t.append(("%%[%s%d]" % (y, i), "%%[%s%d]" % (x, j)))
             elif j == i:
-                t.append(("%%[%s%d]" % (x, i), "%%[%s%d]" % (x, i)))
+                diag = x if kind == "sqr" else y + "h"
+                t.append(("%%[%s%d]" % (diag, i), "%%[%s%d]" % (x, i)))
     return t
 
 
@@ -280,13 +284,19 @@ def emit_fused(lay, name, spec, addend=None):
     outs = ", ".join('[o%d] "=&v"(r.n[%d])' % (k, k) for k in range(n))
     params, inl, pre = [], [], ""
     for kind, x, y in spec:
-        for v in (x,) if kind == "sqr" else (x, y):
+        for v in (x,) if kind in ("sqr", "sqr3") else (x, y):
             if v not in params:
                 params.append(v)
         if kind == "sqr":
             pre += "  uint32_t %s[%d];\n#pragma unroll\n  for (int i = 0; i < %d; i++) %s[i] = %s.n[i] << 1;\n" % (
                 y, n - 1, n - 1, y, x)
             inl += ['[%s%d] "v"(%s[%d])' % (y, i, y, i) for i in range(n - 1)]
+        if kind == "sqr3":
+            pre += ("  uint32_t %sh[%d], %s[%d];\n#pragma unroll\n  for (int i = 0; i < %d; i++) %sh[i] = %s.n[i] * 3;\n"
+                    "#pragma unroll\n  for (int i = 0; i < %d; i++) %s[i] = %sh[i] << 1;\n"
+                    % (y, n, y, n - 1, n, y, x, n - 1, y, y))
+            inl += ['[%s%d] "v"(%s[%d])' % (y, i, y, i) for i in range(n - 1)]
+            inl += ['[%sh%d] "v"(%sh[%d])' % (y, i, y, i) for i in range(n)]
     if addend is not None:
         params.append(addend)
     inl = ['[%s%d] "v"(%s.n[%d])' % (v, i, v, i) for v in params for i in range(n)] + inl
@@ -308,6 +318,7 @@ FUSED29 = [
     ("fe_mulsqr_asm", [("mul", "a", "b"), ("sqr", "c", "g")], None),  # a b + c^2
     ("fe_mul_add_asm", [("mul", "a", "b")], "c"),                     # a b + c
     ("fe_sqr_add_asm", [("sqr", "a", "d")], "c"),                     # a^2 + c
+    ("fe_sqr3_asm", [("sqr3", "a", "q")], None),                      # 3 a^2
 ]
 
 
