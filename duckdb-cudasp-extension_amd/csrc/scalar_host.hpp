@@ -219,8 +219,8 @@ static inline int wnaf(int8_t* digits, int max_digits, const Big<8>& k_in, int w
 // Stage-A ladder cost of one operation (VALU instructions per doubling and per
 // mixed addition incl. its table load, gfx950 build of secp256k1_group29.hpp);
 // used to rank decompositions of the scan key.
-constexpr int LADDER_DBL_COST = 962;
-constexpr int LADDER_ADD_COST = 1560;
+constexpr int LADDER_DBL_COST = 903;
+constexpr int LADDER_ADD_COST = 1600;
 
 // The uniform signed digits of the stage-A ladder for scan key d: d = k1 +
 // k2 lambda (mod n), k1 and k2 each as a width-5 NAF (digits of k_i in

@@ -176,7 +176,7 @@ def test_scan_digits(emu):
             top = max([i + 1 for i, x in enumerate(dg[:M]) if x] + [i + 1 for i, x in enumerate(dg[M:]) if x])
             assert ln.value == top
             weight = sum(1 for x in dg if x)
-            costs.append((ln.value - 1) * 962 + (weight - 1) * 1560)
+            costs.append((ln.value - 1) * 903 + (weight - 1) * 1600)
         assert costs[1] <= costs[0]
         saved += costs[0] - costs[1]
     assert saved > 0
