@@ -484,6 +484,17 @@ struct DeviceGuard {
   }
 };
 
+// Stream arguments (include/cudasp_abi.h): NULL = the scanner's own stream
+// (the stateless entry points: the null stream), CUDASP_STREAM_DEFAULT = the
+// device's null stream -- torch's default stream, whose handle is 0 and so
+// cannot be passed as itself.
+hipStream_t plain_stream(void* stream) {
+  return stream == CUDASP_STREAM_DEFAULT ? nullptr : (hipStream_t)stream;
+}
+hipStream_t scanner_stream(const cudasp_scanner* s, void* stream) {
+  return stream == nullptr ? s->stream : plain_stream(stream);
+}
+
 void free_scanner(cudasp_scanner* s) {
   if (!s) return;
   DeviceGuard g(s->device);
@@ -673,7 +684,7 @@ int cudasp_scan_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint3
   if (!d_tweak_x || !d_tweak_y || !d_output_offsets || !d_output_lengths || !d_match_flags)
     return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   DeviceGuard g(s->device);
-  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  hipStream_t st = scanner_stream(s, stream);
   return launch_pipeline(s, d_tweak_x, d_tweak_y, d_outputs, d_output_offsets, d_output_lengths, n, d_match_flags,
                          (d_match_rows && d_match_count) ? d_match_rows : nullptr,
                          (d_match_rows && d_match_count) ? d_match_count : nullptr, nullptr, nullptr, st);
@@ -685,7 +696,7 @@ int cudasp_row_values_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const
   if (n == 0) return CUDASP_OK;
   if (!d_tweak_x || !d_tweak_y || !d_values) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   DeviceGuard g(s->device);
-  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  hipStream_t st = scanner_stream(s, stream);
   return launch_pipeline(s, d_tweak_x, d_tweak_y, nullptr, nullptr, nullptr, n, nullptr, nullptr, nullptr, d_values,
                          d_t, st);
 }
@@ -694,7 +705,7 @@ int cudasp_tweaks_to_columns(const uint8_t* d_tweak_rows, uint32_t n, uint32_t* 
                              void* stream) {
   if (n == 0) return CUDASP_OK;
   if (!d_tweak_rows || !d_tweak_x || !d_tweak_y) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
-  hipLaunchKernelGGL(k_rows_to_cols, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, d_tweak_rows, n,
+  hipLaunchKernelGGL(k_rows_to_cols, dim3(grid_for(n)), dim3(BLOCK), 0, plain_stream(stream), d_tweak_rows, n,
                      d_tweak_x, d_tweak_y);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
@@ -749,7 +760,7 @@ int cudasp_stage_shared_secret_device(cudasp_scanner* s, const uint32_t* d_tweak
   if (!d_tweak_x || !d_tweak_y || !d_t) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
   DeviceGuard g(s->device);
-  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  hipStream_t st = scanner_stream(s, stream);
   hipLaunchKernelGGL(k_shared_secret, dim3(grid_a(s, n)), dim3(BLOCK), 0, st, d_tweak_x, d_tweak_y, n, s->d_naf,
                      s->consts, s->d_vscratch, d_t);
   HIP_TRY(hipGetLastError());
@@ -765,7 +776,7 @@ int cudasp_stage_match_device(cudasp_scanner* s, const uint32_t* d_t, const int6
     return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
   DeviceGuard g(s->device);
-  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  hipStream_t st = scanner_stream(s, stream);
   bool compact = d_match_rows && d_match_count;
   hipLaunchKernelGGL(k_match<false>, dim3(grid_b(s, n)), dim3(BLOCK), 0, st, d_t, n, s->d_fb, s->consts, s->d_labels,
                      d_outputs, d_output_offsets, d_output_lengths, s->d_lscratch, d_match_flags,
@@ -790,7 +801,7 @@ int cudasp_synth_tweak_columns(int device, const uint8_t s0_le[32], uint64_t fir
   const GenPowers& gp = gen_powers();
   hp_words(c.c_odd, gp.q[FB_WINDOWS]);
   hp_words(c.c_even, hp_add(gp.q[FB_WINDOWS], hp_neg(gp.q[0])));
-  hipLaunchKernelGGL(k_synth_tweaks, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, c, first_index, n, fb,
+  hipLaunchKernelGGL(k_synth_tweaks, dim3(grid_for(n)), dim3(BLOCK), 0, plain_stream(stream), c, first_index, n, fb,
                      d_x, d_y);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
@@ -800,7 +811,7 @@ int cudasp_synth_outputs(uint64_t seed, uint64_t first_index, uint32_t n, uint32
                          uint32_t* d_offsets, uint32_t* d_lengths, void* stream) {
   if (n == 0) return CUDASP_OK;
   if (!d_outputs || !d_offsets || !d_lengths) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
-  hipLaunchKernelGGL(k_synth_outputs, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, seed, first_index, n,
+  hipLaunchKernelGGL(k_synth_outputs, dim3(grid_for(n)), dim3(BLOCK), 0, plain_stream(stream), seed, first_index, n,
                      k, d_outputs, d_offsets, d_lengths);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
@@ -810,7 +821,7 @@ int cudasp_synth_output_lengths(uint64_t seed, uint64_t first_index, uint32_t n,
                                 void* stream) {
   if (n == 0) return CUDASP_OK;
   if (!d_lengths || kmax == 0) return set_error(CUDASP_ERR_INVALID_ARG, "invalid argument");
-  hipLaunchKernelGGL(k_synth_output_lengths, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, seed,
+  hipLaunchKernelGGL(k_synth_output_lengths, dim3(grid_for(n)), dim3(BLOCK), 0, plain_stream(stream), seed,
                      first_index, n, kmax, d_lengths);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
@@ -820,7 +831,7 @@ int cudasp_synth_output_values(uint64_t seed, uint64_t first_index, uint32_t n, 
                                const uint32_t* d_lengths, int64_t* d_outputs, void* stream) {
   if (n == 0) return CUDASP_OK;
   if (!d_offsets || !d_lengths || !d_outputs) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
-  hipLaunchKernelGGL(k_synth_output_values, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, seed,
+  hipLaunchKernelGGL(k_synth_output_values, dim3(grid_for(n)), dim3(BLOCK), 0, plain_stream(stream), seed,
                      first_index, n, d_offsets, d_lengths, d_outputs);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;

@@ -77,11 +77,20 @@ CUDASP_HD Scratch make_scratch(uint32_t* s, uint32_t stride, uint32_t slot) {
   return sc;
 }
 
+// Cache policy of the scratch loads / stores (gfx950 CPol bits: 1 = sc0,
+// 2 = nt, 16 = sc1).
+#ifndef CUDASP_SCR_LOAD_CPOL
+#define CUDASP_SCR_LOAD_CPOL 0
+#endif
+#ifndef CUDASP_SCR_STORE_CPOL
+#define CUDASP_SCR_STORE_CPOL 0
+#endif
+
 CUDASP_HD void scr_store(const Scratch& sc, int base, const fe& a) {
 #pragma unroll
   for (int l = 0; l < FE_LIMBS; l++) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_raw_buffer_store_b32(a.n[l], sc.rsrc, sc.slot * 4u, (uint32_t)(base + l) * sc.stride * 4u, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(a.n[l], sc.rsrc, sc.slot * 4u, (uint32_t)(base + l) * sc.stride * 4u, CUDASP_SCR_STORE_CPOL);
 #else
     sc.s[(size_t)(base + l) * sc.stride + sc.slot] = a.n[l];
 #endif
@@ -92,7 +101,8 @@ CUDASP_HD void scr_load(fe& a, const Scratch& sc, int base) {
 #pragma unroll
   for (int l = 0; l < FE_LIMBS; l++) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    a.n[l] = __builtin_amdgcn_raw_buffer_load_b32(sc.rsrc, sc.slot * 4u, (uint32_t)(base + l) * sc.stride * 4u, 0);
+    a.n[l] = __builtin_amdgcn_raw_buffer_load_b32(sc.rsrc, sc.slot * 4u, (uint32_t)(base + l) * sc.stride * 4u,
+                                                  CUDASP_SCR_LOAD_CPOL);
 #else
     a.n[l] = sc.s[(size_t)(base + l) * sc.stride + sc.slot];
 #endif

@@ -82,3 +82,15 @@ def check(rc):
         msg = load().cudasp_last_error()
         raise CudaspError(rc, msg.decode() if msg else "")
     return rc
+
+
+CUDASP_STREAM_DEFAULT = 1  # include/cudasp_abi.h: the device's null stream
+
+
+def stream_arg(stream):
+    """A torch stream as the ABI's `stream` argument.  torch's default stream
+    has handle 0, which the ABI reads as "the scanner's own stream"; it is
+    passed as CUDASP_STREAM_DEFAULT so the launch stays ordered with the work
+    torch queued on it."""
+    h = stream.cuda_stream
+    return ctypes.c_void_p(h if h else CUDASP_STREAM_DEFAULT)

@@ -83,7 +83,7 @@ class Scanner:
         import torch
         if stream is None:
             stream = torch.cuda.current_stream(torch.device("cuda", self.device))
-        return ctypes.c_void_p(stream.cuda_stream)
+        return _native.stream_arg(stream)
 
     def scan_device(self, tweak_x, tweak_y, outputs, offsets, lengths, flags, match_rows=None,
                     match_count=None, stream=None):

@@ -75,8 +75,14 @@ void cudasp_scanner_destroy(cudasp_scanner* s);
 int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32],
                             const uint8_t spend_public_key[64], const uint8_t* label_keys, uint32_t label_count);
 
-/* Device-resident batch, asynchronous on `stream` (a hipStream_t; NULL = the
- * scanner's own stream).  Inputs: tweak x and y columns (8 x n each,
+/* Stream arguments: a hipStream_t; NULL = the scanner's own stream (for the
+ * entry points without a scanner: the null stream); CUDASP_STREAM_DEFAULT =
+ * the device's null stream, for callers whose current stream is the default
+ * stream (its handle is 0, which would otherwise select the scanner's stream
+ * and lose the ordering with the caller's work). */
+#define CUDASP_STREAM_DEFAULT ((void*)1)
+
+/* Device-resident batch, asynchronous on `stream`.  Inputs: tweak x and y columns (8 x n each,
  * column-major), the outputs CSR (values, per-row u32 offset and length).
  * Outputs: d_match_flags[n] (0/1, required); if d_match_rows and
  * d_match_count are both non-NULL, *d_match_count (which the caller zeroes)

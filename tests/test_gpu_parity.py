@@ -123,3 +123,35 @@ def test_legacy_three_phase_abi(torch_cuda):
         lib.FreeBatchScanManaged(p)
     lib.FreeBatchScanState(st)
     assert [bool(v) for v in flags] == [r["match_all_labels"] for r in rows]
+
+
+def test_default_stream_ordering(torch_cuda):
+    """Launches without an explicit stream run on torch's current stream, also
+    when that is the default stream (handle 0, passed as CUDASP_STREAM_DEFAULT):
+    inputs written by a delayed copy on the default stream are the ones read.
+    (Before the fix the kernels ran on the scanner's own stream and raced the
+    copy; the bench's planting lost that race when another process shared the GPU.)"""
+    torch = torch_cuda
+    from cudasp_amd import Scanner
+    rr = golden_io.load("random_rows.json")
+    rows = rr["rows"][:64]
+    tw = golden_io.tweak_array([r["tweak"] for r in rows])
+    x, y = golden_io.tweak_columns(tw)
+    n = len(rows)
+    with torch.cuda.stream(torch.cuda.default_stream()):
+        assert torch.cuda.current_stream().cuda_stream == 0
+        with Scanner(bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [], max_rows=n) as s:
+            src_x = torch.from_numpy(x.view(np.int32)).cuda()
+            src_y = torch.from_numpy(y.view(np.int32)).cuda()
+            torch.cuda.synchronize()
+            dx = torch.zeros_like(src_x)
+            dy = torch.zeros_like(src_y)
+            dt = torch.zeros((8, n), dtype=torch.int32, device="cuda")
+            dv = torch.zeros((1, n), dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            torch.cuda._sleep(50_000_000)  # hold the default stream back
+            dx.copy_(src_x)
+            dy.copy_(src_y)
+            s.row_values_device(dx, dy, dt, dv)
+            s.sync()
+            assert [int(v) for v in dv.cpu().numpy()[0]] == [r["v"] for r in rows]
