@@ -81,6 +81,20 @@ inline uint32_t lscratch_words(uint32_t label_count) { return FW * label_count +
 
 // ----------------------------------------------------------------- kernels
 
+// t of output index kk of row `row`: virtual row kk * n + row of the 8 x (K n)
+// column-major t array (K = k.output_count, 1 in the reference's semantics).
+__device__ __forceinline__ void store_t(uint32_t* __restrict__ t_out, uint32_t n, uint32_t K, uint32_t row,
+                                        const uint32_t sx[8], uint32_t y_odd, const uint32_t mid[8]) {
+  const size_t N = (size_t)K * n;
+#pragma unroll 1
+  for (uint32_t kk = 0; kk < K; kk++) {
+    uint32_t t[8];
+    bip352_shared_secret_hash(t, mid, sx, y_odd, kk);
+#pragma unroll
+    for (int w = 0; w < 8; w++) t_out[(size_t)w * N + (size_t)kk * n + row] = t[w];
+  }
+}
+
 // Stage A: thread `slot` takes the rows g, g + G, ... (G = ceil(n / ROWS_A)) of
 // each of its groups g, so every row access stays coalesced.
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const uint32_t* __restrict__ tx,
@@ -93,15 +107,19 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
   const Scratch sc = make_scratch(vscr, stride, slot);
   if constexpr (ROWS_A == 1) {
     for (uint32_t row = slot; row < n; row += stride) {
-      uint32_t x[8], y[8], t[8];
+      uint32_t x[8], y[8];
 #pragma unroll
       for (int w = 0; w < 8; w++) {
         x[w] = tx[(size_t)w * n + row];
         y[w] = ty[(size_t)w * n + row];
       }
-      row_shared_secret(t, x, y, naf, k.naf_len, k.mid, sc);
-#pragma unroll
-      for (int w = 0; w < 8; w++) t_out[(size_t)w * n + row] = t[w];
+      gej R;
+      row_shared_secret_point(R, x, y, naf, k.naf_len, sc);
+      fe zi;
+      fe_inv(zi, R.z);
+      uint32_t sx[8];
+      const uint32_t y_odd = row_shared_secret_affine(sx, R, zi);
+      store_t(t_out, n, k.output_count, row, sx, y_odd, k.mid);
     }
     return;
   }
@@ -132,19 +150,21 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
       fe zi;
       pend_load(R, sc, PB, j);
       scr_load(zi, sc, PEND_ZI(PB, j));
-      uint32_t t[8];
-      row_shared_secret_finish(t, R, zi, k.mid);
-#pragma unroll
-      for (int w = 0; w < 8; w++) t_out[(size_t)w * n + row] = t[w];
+      uint32_t sx[8];
+      const uint32_t y_odd = row_shared_secret_affine(sx, R, zi);
+      store_t(t_out, n, k.output_count, row, sx, y_odd, k.mid);
     }
   }
 }
 
 // Stage B: rows g, g + G, ... (G = ceil(n / ROWS_B)) per thread as in stage A;
 // the block walks its groups together so that the compaction ballots see
-// consecutive rows of full waves.
+// consecutive rows of full waves.  n counts virtual rows kk * n_rows + row
+// (K output indices per input row; n == n_rows when K = 1): t, flags and
+// values are indexed by the virtual row, the outputs lists by the input row.
 template <bool VALUES>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t* __restrict__ t_in, uint32_t n,
+                                                 uint32_t n_rows,
                                                  const uint32_t* __restrict__ fb, ScanConsts k,
                                                  const uint32_t* __restrict__ labels,
                                                  const int64_t* __restrict__ outputs,
@@ -185,8 +205,9 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
         uint32_t t[8];
 #pragma unroll
         for (int w = 0; w < 8; w++) t[w] = t_in[(size_t)w * n + row];
-        uint32_t off = VALUES ? 0u : offs[row];
-        uint32_t len = VALUES ? 0u : lens[row];
+        const uint32_t orow = n == n_rows ? row : row % n_rows;
+        uint32_t off = VALUES ? 0u : offs[orow];
+        uint32_t len = VALUES ? 0u : lens[orow];
         hit = row_match(t, fb, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
         if (!VALUES) flags[row] = hit ? 1 : 0;
       } else if (j < count) {
@@ -194,8 +215,9 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
         fe zi;
         pend_load(R, sc, PB, j);
         scr_load(zi, sc, PEND_ZI(PB, j));
-        uint32_t off = VALUES ? 0u : offs[row];
-        uint32_t len = VALUES ? 0u : lens[row];
+        const uint32_t orow = n == n_rows ? row : row % n_rows;
+        uint32_t off = VALUES ? 0u : offs[orow];
+        uint32_t len = VALUES ? 0u : lens[orow];
         hit = row_match_finish(R, zi, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
         if (!VALUES) flags[row] = hit ? 1 : 0;
       }
@@ -208,6 +230,32 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
           base = __shfl(base, 0);
           if (hit) match_rows[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = row;
         }
+      }
+    }
+  }
+}
+
+// K > 1 output indices: a row matches when any of its K virtual rows does;
+// flags and the ballot compaction of k_match, over the input rows.
+__global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ vflags, uint32_t n, uint32_t K,
+                                                    uint8_t* __restrict__ flags, uint32_t* __restrict__ match_rows,
+                                                    uint32_t* __restrict__ match_count) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r0 = blockIdx.x * blockDim.x; r0 < n; r0 += stride) {
+    const uint32_t row = r0 + threadIdx.x;
+    bool hit = false;
+    if (row < n) {
+      for (uint32_t kk = 0; kk < K; kk++) hit = hit || vflags[(size_t)kk * n + row] != 0;
+      flags[row] = hit ? 1 : 0;
+    }
+    if (match_rows != nullptr) {
+      const uint64_t m = __ballot(hit);
+      if (m) {
+        const uint32_t lane = threadIdx.x & 63u;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(match_count, (uint32_t)__popcll(m));
+        base = __shfl(base, 0);
+        if (hit) match_rows[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = row;
       }
     }
   }
@@ -435,10 +483,15 @@ struct cudasp_scanner {
   const uint32_t* d_fb = nullptr;
   int8_t* d_naf = nullptr;
   uint32_t* d_labels = nullptr;
-  uint32_t label_count = 0;
+  uint32_t label_count = 0;  // label keys in d_labels (x2 with label_negation)
   uint32_t label_cap = 0;  // label keys the label buffers are sized for
   uint32_t capacity = 0;
-  uint32_t* d_t = nullptr;         // 8 x capacity
+  cudasp_scan_options opt{1, 0, 0};
+  uint32_t t_cap_k = 1;            // output indices d_t / d_vflags are sized for
+  std::vector<uint8_t> keys;       // scan key || spend key || label keys (set_options re-prepares)
+  uint32_t raw_label_count = 0;
+  uint32_t* d_t = nullptr;         // 8 x (t_cap_k capacity)
+  uint8_t* d_vflags = nullptr;     // t_cap_k x capacity (K > 1: per output index)
   uint32_t* d_vscratch = nullptr;  // VSCRATCH_WORDS x slots_a
   uint32_t* d_lscratch = nullptr;  // lscratch_words(L) x slots_b
   uint32_t slots_a = 0, slots_b = 0;
@@ -499,12 +552,37 @@ void free_scanner(cudasp_scanner* s) {
   if (!s) return;
   DeviceGuard g(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  void* ptrs[] = {s->d_naf, s->d_labels, s->d_t, s->d_vscratch, s->d_lscratch, s->d_rows,
-                  s->d_tx,  s->d_ty,     s->d_flags, s->d_offs, s->d_lens,    s->d_outputs};
+  void* ptrs[] = {s->d_naf, s->d_labels, s->d_t,    s->d_vscratch, s->d_lscratch, s->d_rows, s->d_tx,
+                  s->d_ty,  s->d_flags,  s->d_offs, s->d_lens,     s->d_outputs,   s->d_vflags};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
+}
+
+// Stage B over the K n virtual rows of n input rows (t: 8 x (K n)); with
+// K > 1 the per-index flags are ORed per input row before the compaction.
+int launch_match(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t* outputs, const uint32_t* offs,
+                 const uint32_t* lens, uint8_t* flags, uint32_t* match_rows, uint32_t* match_count, int64_t* values,
+                 hipStream_t st) {
+  const uint32_t K = s->consts.output_count;
+  const uint32_t N = K * n;
+  const uint32_t blocks_b = grid_b(s, N);
+  if (values) {
+    hipLaunchKernelGGL(k_match<true>, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels,
+                       nullptr, nullptr, nullptr, s->d_lscratch, nullptr, nullptr, nullptr, values);
+  } else if (K == 1) {
+    hipLaunchKernelGGL(k_match<false>, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels,
+                       outputs, offs, lens, s->d_lscratch, flags, match_rows, match_count, nullptr);
+  } else {
+    hipLaunchKernelGGL(k_match<false>, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels,
+                       outputs, offs, lens, s->d_lscratch, s->d_vflags, nullptr, nullptr, nullptr);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_or_flags, dim3(grid_for(n)), dim3(BLOCK), 0, st, s->d_vflags, n, K, flags, match_rows,
+                       match_count);
+  }
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
 }
 
 int launch_pipeline(cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, const int64_t* outputs,
@@ -512,20 +590,11 @@ int launch_pipeline(cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, c
                     uint32_t* match_count, int64_t* values, uint32_t* t_out, hipStream_t st) {
   if (n == 0) return CUDASP_OK;
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
-  const uint32_t blocks_a = grid_a(s, n), blocks_b = grid_b(s, n);
   uint32_t* t = t_out ? t_out : s->d_t;
-  hipLaunchKernelGGL(k_shared_secret, dim3(blocks_a), dim3(BLOCK), 0, st, tx, ty, n, s->d_naf, s->consts,
+  hipLaunchKernelGGL(k_shared_secret, dim3(grid_a(s, n)), dim3(BLOCK), 0, st, tx, ty, n, s->d_naf, s->consts,
                      s->d_vscratch, t);
   HIP_TRY(hipGetLastError());
-  if (values) {
-    hipLaunchKernelGGL(k_match<true>, dim3(blocks_b), dim3(BLOCK), 0, st, t, n, s->d_fb, s->consts, s->d_labels,
-                       nullptr, nullptr, nullptr, s->d_lscratch, nullptr, nullptr, nullptr, values);
-  } else {
-    hipLaunchKernelGGL(k_match<false>, dim3(blocks_b), dim3(BLOCK), 0, st, t, n, s->d_fb, s->consts, s->d_labels,
-                       outputs, offs, lens, s->d_lscratch, flags, match_rows, match_count, nullptr);
-  }
-  HIP_TRY(hipGetLastError());
-  return CUDASP_OK;
+  return launch_match(s, t, n, outputs, offs, lens, flags, match_rows, match_count, values, st);
 }
 
 }  // namespace
@@ -572,6 +641,10 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
   s->capacity = max_rows;
   s->label_count = label_count;
   s->label_cap = label_count;
+  s->keys.assign(scan_private_key, scan_private_key + 32);
+  s->keys.insert(s->keys.end(), spend_public_key, spend_public_key + 64);
+  if (label_count) s->keys.insert(s->keys.end(), label_keys, label_keys + 64 * (size_t)label_count);
+  s->raw_label_count = label_count;
 
   // --- device state --------------------------------------------------------
   DeviceGuard g(device);
@@ -635,8 +708,11 @@ int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32
   std::vector<int8_t> naf;
   std::vector<uint32_t> labels;
   std::string err;
-  int prc = prepare_scan(scan_private_key, spend_public_key, label_keys, label_count, consts, naf, labels, err);
+  int prc = prepare_scan(scan_private_key, spend_public_key, label_keys, label_count, consts, naf, labels, err,
+                         &s->opt);
   if (prc != CUDASP_OK) return set_error(prc, "%s", err.c_str());
+  const uint32_t raw_label_count = label_count;
+  label_count = consts.label_count;  // with the negated copies
   if ((uint64_t)lscratch_words(label_count) * 4 * BLOCK > (1ull << 32) - 1)
     return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys (%u)", label_count);
   DeviceGuard g(s->device);
@@ -665,7 +741,49 @@ int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32
   HIP_TRY(hipMemcpy(s->d_labels, labels.data(), labels.size() * 4, hipMemcpyHostToDevice));
   s->consts = consts;
   s->label_count = label_count;
+  if (s->keys.data() != scan_private_key) {
+    std::vector<uint8_t> keys(scan_private_key, scan_private_key + 32);
+    keys.insert(keys.end(), spend_public_key, spend_public_key + 64);
+    if (raw_label_count) keys.insert(keys.end(), label_keys, label_keys + 64 * (size_t)raw_label_count);
+    s->keys.swap(keys);
+    s->raw_label_count = raw_label_count;
+  }
   return CUDASP_OK;
+}
+
+int cudasp_scanner_set_options(cudasp_scanner* s, const cudasp_scan_options* options) {
+  g_last_error.clear();
+  if (!s || !options) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  const uint32_t K = options->output_count;
+  if (K < 1 || K > CUDASP_MAX_OUTPUT_COUNT)
+    return set_error(CUDASP_ERR_INVALID_ARG, "output_count must be between 1 and %d", CUDASP_MAX_OUTPUT_COUNT);
+  if ((uint64_t)K * s->capacity > 0xFFFFFFFFull)
+    return set_error(CUDASP_ERR_CAPACITY, "output_count %u x capacity %u exceeds 2^32 virtual rows", K, s->capacity);
+  DeviceGuard g(s->device);
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  if (K > s->t_cap_k) {
+    uint32_t* d_t = nullptr;
+    uint8_t* d_vflags = nullptr;
+    HIP_TRY(hipMalloc(&d_t, (size_t)8 * K * s->capacity * 4));
+    hipError_t e = hipMalloc(&d_vflags, (size_t)K * s->capacity);
+    if (e != hipSuccess) {
+      (void)hipFree(d_t);
+      return set_error(CUDASP_ERR_HIP, "hipMalloc failed: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(s->d_t);
+    (void)hipFree(s->d_vflags);
+    s->d_t = d_t;
+    s->d_vflags = d_vflags;
+    s->t_cap_k = K;
+  }
+  const cudasp_scan_options old = s->opt;
+  s->opt = *options;
+  s->opt.label_negation = options->label_negation ? 1u : 0u;
+  s->opt.full_x = options->full_x ? 1u : 0u;
+  const uint8_t* k = s->keys.data();
+  int rc = cudasp_scanner_set_keys(s, k, k + 32, s->raw_label_count ? k + 96 : nullptr, s->raw_label_count);
+  if (rc != CUDASP_OK) s->opt = old;
+  return rc;
 }
 
 int cudasp_scanner_sync(cudasp_scanner* s) {
@@ -732,17 +850,18 @@ int cudasp_scan_host(cudasp_scanner* s, const uint8_t* h_tweak_keys, const int64
     HIP_TRY(hipMalloc(&s->d_offs, (size_t)4 * s->capacity));
     HIP_TRY(hipMalloc(&s->d_lens, (size_t)4 * s->capacity));
   }
-  if (outputs_size > s->outputs_cap) {
+  const size_t out_bytes = outputs_size * (s->consts.full_x ? 32 : 8);  // one int64 or one 32-byte x
+  if (out_bytes > s->outputs_cap) {
     if (s->d_outputs) HIP_TRY(hipFree(s->d_outputs));
     s->d_outputs = nullptr;
-    HIP_TRY(hipMalloc(&s->d_outputs, outputs_size * 8));
-    s->outputs_cap = outputs_size;
+    HIP_TRY(hipMalloc(&s->d_outputs, out_bytes));
+    s->outputs_cap = out_bytes;
   }
   hipStream_t st = s->stream;
   HIP_TRY(hipMemcpyAsync(s->d_rows, h_tweak_keys, (size_t)64 * n, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(s->d_offs, h_output_offsets, (size_t)4 * n, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(s->d_lens, h_output_lengths, (size_t)4 * n, hipMemcpyHostToDevice, st));
-  if (outputs_size) HIP_TRY(hipMemcpyAsync(s->d_outputs, h_outputs, outputs_size * 8, hipMemcpyHostToDevice, st));
+  if (outputs_size) HIP_TRY(hipMemcpyAsync(s->d_outputs, h_outputs, out_bytes, hipMemcpyHostToDevice, st));
   int rc = cudasp_tweaks_to_columns(s->d_rows, n, s->d_tx, s->d_ty, st);
   if (rc != CUDASP_OK) return rc;
   rc = launch_pipeline(s, s->d_tx, s->d_ty, s->d_outputs, s->d_offs, s->d_lens, n, s->d_flags, nullptr, nullptr,
@@ -778,11 +897,8 @@ int cudasp_stage_match_device(cudasp_scanner* s, const uint32_t* d_t, const int6
   DeviceGuard g(s->device);
   hipStream_t st = scanner_stream(s, stream);
   bool compact = d_match_rows && d_match_count;
-  hipLaunchKernelGGL(k_match<false>, dim3(grid_b(s, n)), dim3(BLOCK), 0, st, d_t, n, s->d_fb, s->consts, s->d_labels,
-                     d_outputs, d_output_offsets, d_output_lengths, s->d_lscratch, d_match_flags,
-                     compact ? d_match_rows : nullptr, compact ? d_match_count : nullptr, nullptr);
-  HIP_TRY(hipGetLastError());
-  return CUDASP_OK;
+  return launch_match(s, d_t, n, d_outputs, d_output_offsets, d_output_lengths, d_match_flags,
+                      compact ? d_match_rows : nullptr, compact ? d_match_count : nullptr, nullptr, st);
 }
 
 int cudasp_synth_tweak_columns(int device, const uint8_t s0_le[32], uint64_t first_index, uint32_t n,

@@ -161,9 +161,18 @@ inline std::vector<uint32_t> fb_window_bases() {
   return bases;
 }
 
+// opt (may be NULL = the reference's semantics): K and full_x go to the
+// constants; with label_negation the label buffer holds L_0..L_(L-1) then
+// -L_0..-L_(L-1) and k.label_count = 2 L.
 inline int prepare_scan(const uint8_t scan_private_key[32], const uint8_t spend_public_key[64],
                         const uint8_t* label_keys, uint32_t label_count, ScanConsts& k, std::vector<int8_t>& naf,
-                        std::vector<uint32_t>& labels, std::string& err) {
+                        std::vector<uint32_t>& labels, std::string& err, const cudasp_scan_options* opt = nullptr) {
+  const uint32_t K = opt ? opt->output_count : 1u;
+  if (K < 1 || K > CUDASP_MAX_OUTPUT_COUNT) {
+    err = "output_count must be between 1 and " + std::to_string(CUDASP_MAX_OUTPUT_COUNT);
+    return CUDASP_ERR_INVALID_ARG;
+  }
+  const bool negate = opt && opt->label_negation;
   host::Big<8> d = host::big_zero<8>();
   for (int i = 0; i < 32; i++) d.w[i / 4] |= (uint32_t)scan_private_key[i] << (8 * (i % 4));
   d = host::scalar_reduce(d);
@@ -180,15 +189,21 @@ inline int prepare_scan(const uint8_t scan_private_key[32], const uint8_t spend_
   memset(&k, 0, sizeof(k));
   bip352_midstate(k.mid);
   k.naf_len = naf_len;
-  k.label_count = label_count;
+  k.label_count = negate ? 2 * label_count : label_count;
+  k.output_count = K;
+  k.full_x = opt && opt->full_x ? 1u : 0u;
   const GenPowers& gp = gen_powers();
   HPoint co = gp.q[FB_WINDOWS];
   HPoint ce = hp_add(co, hp_neg(gp.q[0]));
   hp_words(k.c_odd, co);
   hp_words(k.c_even, ce);
   hp_words(k.spend, hp_from_bytes(spend_public_key));
-  labels.assign(16 * (size_t)(label_count ? label_count : 1), 0);
-  for (uint32_t j = 0; j < label_count; j++) hp_words(&labels[16 * j], hp_from_bytes(label_keys + 64 * (size_t)j));
+  labels.assign(16 * (size_t)(k.label_count ? k.label_count : 1), 0);
+  for (uint32_t j = 0; j < label_count; j++) {
+    HPoint Lj = hp_from_bytes(label_keys + 64 * (size_t)j);
+    hp_words(&labels[16 * j], Lj);
+    if (negate) hp_words(&labels[16 * ((size_t)label_count + j)], hp_neg(Lj));
+  }
   return CUDASP_OK;
 }
 

@@ -39,7 +39,11 @@ struct ScanConsts {
   uint32_t c_even[16];  // 2^(FB_BITS FB_WINDOWS) G - G  (used when the hash t is even)
   uint32_t spend[16];   // B, the spend public key (normalized)
   uint32_t naf_len;     // digits in each GLV half
-  uint32_t label_count;
+  uint32_t label_count; // label keys in the label buffer (negated copies included)
+  // Protocol variants (cudasp_scan_options, include/cudasp_abi.h; the reference
+  // is output_count 1, full_x 0):
+  uint32_t output_count;  // K: output indices k = 0..K-1 hashed per row
+  uint32_t full_x;        // outputs are 32-byte big-endian x-only keys
 };
 
 // beta, a primitive cube root of unity mod p: (beta*x, y) = lambda*(x, y).
@@ -271,15 +275,23 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
   fe_mul(R.z, R.z, cz);
 }
 
-// Stage A, second half: from S (Jacobian) and 1/Z, serialize and hash.
-// Writes t (8 LE words of the BE digest read as an integer).
-CUDASP_HD void row_shared_secret_finish(uint32_t t_out[8], const gej& R, const fe& zi, const uint32_t mid[8]) {
+// Stage A, second half: from S (Jacobian) and 1/Z, the affine x (8 LE words)
+// and the parity of y.
+CUDASP_HD uint32_t row_shared_secret_affine(uint32_t sx[8], const gej& R, const fe& zi) {
   ge S;
   gej_to_ge_zinv(S, R, zi);
-  uint32_t sx[8], sy[8];
+  uint32_t sy[8];
   fe_to_u32x8(sx, S.x);
   fe_to_u32x8(sy, S.y);
-  bip352_shared_secret_hash(t_out, mid, sx, sy[0] & 1u);
+  return sy[0] & 1u;
+}
+
+// Serialize and hash (output index 0, the reference's).  Writes t (8 LE words
+// of the BE digest read as an integer).
+CUDASP_HD void row_shared_secret_finish(uint32_t t_out[8], const gej& R, const fe& zi, const uint32_t mid[8]) {
+  uint32_t sx[8];
+  uint32_t y_odd = row_shared_secret_affine(sx, R, zi);
+  bip352_shared_secret_hash(t_out, mid, sx, y_odd);
 }
 
 // Stage A for one row (one inversion per row).
@@ -377,6 +389,31 @@ CUDASP_HD bool outputs_contain(const int64_t* outputs, uint32_t off, uint32_t le
   return false;
 }
 
+// Full-x compare (cudasp_scan_options.full_x): outputs are 32-byte big-endian
+// x-only keys, 8 u32 words each; x is a fully normalized field element.
+CUDASP_HD uint32_t bswap32(uint32_t v) {
+  return (v >> 24) | ((v >> 8) & 0xff00u) | ((v << 8) & 0xff0000u) | (v << 24);
+}
+
+CUDASP_HD bool outputs_contain_x(const uint32_t* outputs_x, uint32_t off, uint32_t len, const fe& x) {
+  uint32_t w[8];
+  fe_to_u32x8(w, x);
+  for (uint32_t k = 0; k < len; k++) {
+    const uint32_t* o = outputs_x + ((size_t)off + k) * 8;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) diff |= bswap32(o[q]) ^ w[7 - q];
+    if (diff == 0) return true;
+  }
+  return false;
+}
+
+CUDASP_HD bool outputs_match(const ScanConsts& k, const int64_t* outputs, uint32_t off, uint32_t len, const fe& x,
+                             int64_t v) {
+  return k.full_x ? outputs_contain_x(reinterpret_cast<const uint32_t*>(outputs), off, len, x)
+                  : outputs_contain(outputs, off, len, v);
+}
+
 // Value reported for a label whose sum F + L is the point at infinity (F = -L):
 // no x coordinate exists, the row cannot match through it.
 constexpr int64_t LABEL_INFINITY = (int64_t)0x8000000000000000ull;
@@ -461,9 +498,9 @@ CUDASP_HD bool row_match_finish(const gej& R, const fe& zi, const ScanConsts& k,
                                 int64_t* values, uint32_t vstride) {
   ge F;
   gej_to_ge_zinv(F, R, zi);
-  int64_t v = fe_upper64(F.x);
+  int64_t v = fe_upper64(F.x);  // F is normalized by gej_to_ge_zinv
   if (values) values[0] = v;
-  bool hit = outputs_contain(outputs, off, len, v);
+  bool hit = outputs_match(k, outputs, off, len, F.x, v);
 
   uint32_t L = k.label_count;
   if (L == 0) return hit;
@@ -520,7 +557,7 @@ CUDASP_HD bool row_match_finish(const gej& R, const fe& zi, const ScanConsts& k,
     fe_normalize(x3);
     int64_t vj = infinity ? LABEL_INFINITY : fe_upper64(x3);
     if (values) values[(size_t)(1 + j) * vstride] = vj;
-    if (!infinity) hit = hit || outputs_contain(outputs, off, len, vj);
+    if (!infinity) hit = hit || outputs_match(k, outputs, off, len, x3, vj);
   }
   return hit;
 }

@@ -66,17 +66,19 @@ CUDASP_SHA_HD void sha256_init(uint32_t s[8]) {
 // of y.  Output t as 8 little-endian u32 limbs of the big-endian digest read as
 // an integer (the reference's host conversion, src/cudasp_gpu.cu:862-877:
 // limb j = digest bytes [31-4j-3 .. 31-4j] big-endian = digest word 7-j).
+// k: the output index serialized after x as ser32(k) (BIP-352); the reference
+// always hashes k = 0 (src/cudasp_gpu.cu:278-282).
 CUDASP_SHA_HD void bip352_shared_secret_hash(uint32_t t[8], const uint32_t mid[8], const uint32_t x[8],
-                                             uint32_t y_odd) {
-  // ser = (0x02 | y_odd) || BE(x) || 00 00 00 00   (src/cudasp_gpu.cu:261-282)
+                                             uint32_t y_odd, uint32_t k = 0) {
+  // ser = (0x02 | y_odd) || BE(x) || ser32(k)   (src/cudasp_gpu.cu:261-282, k = 0 there)
   // x BE bytes: word k of BE(x) = x limb (7-k).  The message starts one byte in.
   uint32_t w[16];
   uint32_t prefix = 0x02u | (y_odd & 1u);
   w[0] = (prefix << 24) | (x[7] >> 8);
 #pragma unroll
   for (int k = 1; k < 8; k++) w[k] = (x[8 - k] << 24) | (x[7 - k] >> 8);
-  w[8] = x[0] << 24;  // last x byte, then ser[33..35] = 0
-  w[9] = 0x00800000u; // ser[36] = 0, then the 0x80 pad byte
+  w[8] = (x[0] << 24) | (k >> 8);       // last x byte, then ser32(k) bytes 0..2
+  w[9] = (k << 24) | 0x00800000u;       // ser32(k) byte 3, then the 0x80 pad byte
   w[10] = 0; w[11] = 0; w[12] = 0; w[13] = 0; w[14] = 0;
   w[15] = (64u + 37u) * 8u;
   uint32_t s[8];

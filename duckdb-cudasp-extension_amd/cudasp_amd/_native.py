@@ -28,6 +28,7 @@ SIGNATURES = {
     "cudasp_scanner_create": (_I32, [_I32, _P, _P, _P, _U32, _U32, ctypes.POINTER(_P)]),
     "cudasp_scanner_destroy": (None, [_P]),
     "cudasp_scanner_set_keys": (_I32, [_P, _P, _P, _P, _U32]),
+    "cudasp_scanner_set_options": (_I32, [_P, _P]),
     "cudasp_scan_device": (_I32, [_P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "cudasp_scan_host": (_I32, [_P, _P, _P, ctypes.c_size_t, _P, _P, _U32, _P]),
     "cudasp_row_values_device": (_I32, [_P, _P, _P, _U32, _P, _P, _P]),
@@ -85,6 +86,13 @@ def check(rc):
 
 
 CUDASP_STREAM_DEFAULT = 1  # include/cudasp_abi.h: the device's null stream
+CUDASP_MAX_OUTPUT_COUNT = 64
+
+
+class ScanOptions(ctypes.Structure):
+    """cudasp_scan_options (include/cudasp_abi.h)."""
+    _fields_ = [("output_count", ctypes.c_uint32), ("label_negation", ctypes.c_uint32),
+                ("full_x", ctypes.c_uint32)]
 
 
 def stream_arg(stream):

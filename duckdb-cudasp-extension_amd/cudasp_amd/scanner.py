@@ -50,6 +50,27 @@ class Scanner:
                                                 self.max_rows, ctypes.byref(h)))
         self._h = h
         self._lib = lib
+        self.output_count = 1
+        self.label_negation = False
+        self.full_x = False
+
+    def set_options(self, output_count=1, label_negation=False, full_x=False):
+        """Protocol variants (cudasp_scanner_set_options):
+        output indices k = 0..output_count-1, labels also negated, outputs as
+        32-byte big-endian x-only keys compared in full.  The defaults are the
+        reference's semantics."""
+        opt = _native.ScanOptions(int(output_count), int(bool(label_negation)), int(bool(full_x)))
+        _native.check(self._lib.cudasp_scanner_set_options(self._h, ctypes.byref(opt)))
+        self.output_count = int(output_count)
+        self.label_negation = bool(label_negation)
+        self.full_x = bool(full_x)
+        self._t = None
+
+    @property
+    def value_rows(self):
+        """Compare values per virtual row: the base value and one per label
+        (labels twice with label_negation)."""
+        return 1 + (2 if self.label_negation else 1) * self.label_count
 
     def set_keys(self, scan_private_key, spend_public_key, label_keys=()):
         """Rebind to another query's keys, keeping the device buffers
@@ -106,7 +127,7 @@ class Scanner:
         if t_out is None:
             import torch
             if getattr(self, "_t", None) is None:
-                self._t = torch.empty((8 * self.max_rows,), dtype=torch.int32,
+                self._t = torch.empty((8 * self.max_rows * self.output_count,), dtype=torch.int32,
                                       device=torch.device("cuda", self.device))
             t_out = self._t
         self._t_last = t_out
@@ -131,11 +152,15 @@ class Scanner:
     # ------------------------------------------------------------- host path
     def scan_host(self, tweak_keys, outputs, offsets, lengths):
         """Synchronous scan from host memory.  tweak_keys: uint8 [n, 64];
-        outputs: int64 CSR values; offsets/lengths: uint32 [n].  Returns a
+        outputs: int64 CSR values (with full_x: uint8 [total, 32] big-endian
+        x-only keys); offsets/lengths: uint32 [n], counting outputs.  Returns a
         uint8 [n] array of match flags."""
         tk = np.ascontiguousarray(tweak_keys, dtype=np.uint8).reshape(-1, 64)
         n = tk.shape[0]
-        outs = np.ascontiguousarray(outputs, dtype=np.int64)
+        if self.full_x:
+            outs = np.ascontiguousarray(outputs, dtype=np.uint8).reshape(-1, 32)
+        else:
+            outs = np.ascontiguousarray(outputs, dtype=np.int64)
         offs = np.ascontiguousarray(offsets, dtype=np.uint32)
         lens = np.ascontiguousarray(lengths, dtype=np.uint32)
         if offs.shape[0] != n or lens.shape[0] != n:
@@ -144,6 +169,6 @@ class Scanner:
         if n == 0:
             return flags
         _native.check(self._lib.cudasp_scan_host(
-            self._h, _ptr(tk), _ptr(outs) if outs.size else None, outs.size, _ptr(offs), _ptr(lens), n,
+            self._h, _ptr(tk), _ptr(outs) if outs.size else None, outs.shape[0], _ptr(offs), _ptr(lens), n,
             _ptr(flags)))
         return flags

@@ -75,6 +75,35 @@ void cudasp_scanner_destroy(cudasp_scanner* s);
 int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32],
                             const uint8_t spend_public_key[64], const uint8_t* label_keys, uint32_t label_count);
 
+/* Protocol variants, off by default.  With the
+ * defaults a scanner computes exactly the reference's flags.
+ *   output_count   K >= 1: each row is tested for the output indices
+ *                  k = 0 .. K-1, t_k = SHA256(H(tag)||H(tag)||ser(S)||ser32(k))
+ *                  (BIP-352); the reference hashes k = 0 only
+ *                  (src/cudasp_gpu.cu:278-282).  A row matches if any k does.
+ *   label_negation nonzero: every label is also tested negated, F - L_j after
+ *                  the F + L_j of all labels (the "(and negated)" of
+ *                  src/cudasp_gpu.cu:938-939, which the reference kernel does
+ *                  not do).
+ *   full_x         nonzero: outputs are 32-byte big-endian x-only keys (on-chain
+ *                  taproot output keys), compared with all of F.x instead of
+ *                  the signed int64 of its upper 64 bits.  Device and host
+ *                  output arrays then hold 32 bytes per output (an int64_t*
+ *                  argument points at them; offsets and lengths count outputs).
+ * Device-path buffer sizes scale with K: stage t arrays are 8 x (K n) words
+ * and the diagnostic values (1 + L') x (K n), virtual row k * n + row, where
+ * L' = label_count (x2 with label_negation). */
+#define CUDASP_MAX_OUTPUT_COUNT 64
+typedef struct {
+  uint32_t output_count;
+  uint32_t label_negation;
+  uint32_t full_x;
+} cudasp_scan_options;
+
+/* Set a scanner's options (the keys are kept; buffers grow as needed).
+ * Not concurrent with work in flight on the scanner. */
+int cudasp_scanner_set_options(cudasp_scanner* s, const cudasp_scan_options* options);
+
 /* Stream arguments: a hipStream_t; NULL = the scanner's own stream (for the
  * entry points without a scanner: the null stream); CUDASP_STREAM_DEFAULT =
  * the device's null stream, for callers whose current stream is the default

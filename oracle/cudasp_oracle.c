@@ -407,37 +407,71 @@ static apt apt_from_le64(const uint8_t* b) {
   return p;
 }
 
-int cudasp_oracle_row(const uint8_t scan_key_le[32], const uint8_t spend_key_le[64], const uint8_t* label_keys_le,
-                      uint32_t label_count, const uint8_t tweak_le[64], uint8_t t_be_out[32], int64_t* values_out) {
+/* One row for output indices k = 0..K-1 (cudasp_oracle_options; the
+ * reference is K = 1, no negation, int64 compare).  Per k: t_k from
+ * ser(S) || ser32(k) (src/cudasp_gpu.cu:261-284 with k instead of the fixed
+ * zero), F = t_k G + B (:318-354, :44-71), the base value, then F + L_j for
+ * the labels in order (:133-172), then F - L_j when label_negation (the
+ * "(and negated)" of :938-939).  values_out[k * (1 + L') + c]; xs_out (may be
+ * NULL) the matching 32-byte BE x (zeros for infinity); t_be_out (may be NULL)
+ * K digests. */
+int cudasp_oracle_row_ex(const uint8_t scan_key_le[32], const uint8_t spend_key_le[64], const uint8_t* label_keys_le,
+                         uint32_t label_count, const uint8_t tweak_le[64], const cudasp_oracle_options* opt,
+                         uint8_t* t_be_out, uint8_t* xs_out, int64_t* values_out) {
+  const uint32_t K = opt ? opt->output_count : 1;
+  const int neg = opt && opt->label_negation;
+  const uint32_t Lp = neg ? 2 * label_count : label_count;
   fe4 d;
   u256_from_le(&d, scan_key_le);
   apt T = apt_from_le64(tweak_le);
   apt S = pt_mul(&d, &T);
   if (S.inf) return -1;
-  uint8_t ser[37];
-  ser[0] = (uint8_t)(0x02 | (S.y.v[0] & 1));
-  u256_to_be(ser + 1, &S.x);
-  memset(ser + 33, 0, 4);
-  uint8_t h[32];
-  tagged_hash(h, "BIP0352/SharedSecret", ser, 37);
-  if (t_be_out) memcpy(t_be_out, h, 32);
-  fe4 t;
-  u256_from_be(&t, h);
   apt G;
   G.x = GX;
   G.y = GY;
   G.inf = 0;
-  apt P0 = pt_mul(&t, &G);
   apt B = apt_from_le64(spend_key_le);
-  apt F = pt_add(&P0, &B);
-  if (F.inf) return -1;
-  values_out[0] = upper64(&F.x);
-  for (uint32_t j = 0; j < label_count; j++) {
-    apt Lj = apt_from_le64(label_keys_le + 64 * (size_t)j);
-    apt FL = pt_add(&F, &Lj);
-    values_out[1 + j] = FL.inf ? CUDASP_ORACLE_LABEL_INFINITY : upper64(&FL.x);
+  for (uint32_t k = 0; k < K; k++) {
+    uint8_t ser[37];
+    ser[0] = (uint8_t)(0x02 | (S.y.v[0] & 1));
+    u256_to_be(ser + 1, &S.x);
+    ser[33] = (uint8_t)(k >> 24); /* ser32(k), big-endian */
+    ser[34] = (uint8_t)(k >> 16);
+    ser[35] = (uint8_t)(k >> 8);
+    ser[36] = (uint8_t)k;
+    uint8_t h[32];
+    tagged_hash(h, "BIP0352/SharedSecret", ser, 37);
+    if (t_be_out) memcpy(t_be_out + 32 * (size_t)k, h, 32);
+    fe4 t;
+    u256_from_be(&t, h);
+    apt P0 = pt_mul(&t, &G);
+    apt F = pt_add(&P0, &B);
+    if (F.inf) return -1;
+    int64_t* v = values_out + (size_t)k * (1 + Lp);
+    uint8_t* xs = xs_out ? xs_out + (size_t)k * (1 + Lp) * 32 : NULL;
+    v[0] = upper64(&F.x);
+    if (xs) u256_to_be(xs, &F.x);
+    for (uint32_t c = 0; c < Lp; c++) {
+      uint32_t j = c < label_count ? c : c - label_count;
+      apt Lj = apt_from_le64(label_keys_le + 64 * (size_t)j);
+      if (c >= label_count) fp_sub(&Lj.y, &(fe4){{0, 0, 0, 0}}, &Lj.y); /* -L_j */
+      apt FL = pt_add(&F, &Lj);
+      v[1 + c] = FL.inf ? CUDASP_ORACLE_LABEL_INFINITY : upper64(&FL.x);
+      if (xs) {
+        if (FL.inf)
+          memset(xs + 32 * (size_t)(1 + c), 0, 32);
+        else
+          u256_to_be(xs + 32 * (size_t)(1 + c), &FL.x);
+      }
+    }
   }
   return 0;
+}
+
+int cudasp_oracle_row(const uint8_t scan_key_le[32], const uint8_t spend_key_le[64], const uint8_t* label_keys_le,
+                      uint32_t label_count, const uint8_t tweak_le[64], uint8_t t_be_out[32], int64_t* values_out) {
+  return cudasp_oracle_row_ex(scan_key_le, spend_key_le, label_keys_le, label_count, tweak_le, NULL, t_be_out, NULL,
+                              values_out);
 }
 
 static int contains(const int64_t* outs, uint32_t off, uint32_t len, int64_t v) {
@@ -446,10 +480,17 @@ static int contains(const int64_t* outs, uint32_t off, uint32_t len, int64_t v) 
   return 0;
 }
 
+static int contains_x(const uint8_t* outs_x, uint32_t off, uint32_t len, const uint8_t x[32]) {
+  for (uint32_t k = 0; k < len; k++)
+    if (memcmp(outs_x + 32 * ((size_t)off + k), x, 32) == 0) return 1;
+  return 0;
+}
+
 typedef struct {
   const uint8_t *scan, *spend, *labels, *tweaks;
   uint32_t label_count, begin, end;
-  const int64_t* outputs;
+  cudasp_oracle_options opt;
+  const void* outputs;
   const uint32_t *offs, *lens;
   uint8_t* flags;
   int64_t* values;
@@ -458,31 +499,43 @@ typedef struct {
 
 static void* run_job(void* arg) {
   job_t* j = (job_t*)arg;
-  int64_t* v = (int64_t*)malloc(sizeof(int64_t) * (1 + j->label_count));
+  const uint32_t K = j->opt.output_count;
+  const uint32_t W = 1 + (j->opt.label_negation ? 2 : 1) * j->label_count; /* values per output index */
+  int64_t* v = (int64_t*)malloc(sizeof(int64_t) * K * W);
+  uint8_t* xs = (uint8_t*)malloc(32 * (size_t)K * W);
   j->rc = 0;
   for (uint32_t r = j->begin; r < j->end; r++) {
-    if (cudasp_oracle_row(j->scan, j->spend, j->labels, j->label_count, j->tweaks + 64 * (size_t)r, NULL, v) != 0) {
+    if (cudasp_oracle_row_ex(j->scan, j->spend, j->labels, j->label_count, j->tweaks + 64 * (size_t)r, &j->opt,
+                             NULL, xs, v) != 0) {
       j->rc = -1;
       if (j->flags) j->flags[r] = 0;
       continue;
     }
-    if (j->values) memcpy(j->values + (size_t)r * (1 + j->label_count), v, sizeof(int64_t) * (1 + j->label_count));
+    if (j->values) memcpy(j->values + (size_t)r * K * W, v, sizeof(int64_t) * K * W);
     if (j->flags) {
-      /* CheckMatchesWithLabelsKernel: base value first, then labels in order */
-      int hit = contains(j->outputs, j->offs[r], j->lens[r], v[0]);
-      for (uint32_t k = 0; !hit && k < j->label_count; k++)
-        if (v[1 + k] != CUDASP_ORACLE_LABEL_INFINITY) hit = contains(j->outputs, j->offs[r], j->lens[r], v[1 + k]);
+      /* CheckMatchesWithLabelsKernel: base value first, then labels in order;
+       * a row matches if any output index does */
+      int hit = 0;
+      for (uint32_t q = 0; !hit && q < K * W; q++) {
+        if (q % W != 0 && v[q] == CUDASP_ORACLE_LABEL_INFINITY) continue;
+        hit = j->opt.full_x ? contains_x((const uint8_t*)j->outputs, j->offs[r], j->lens[r], xs + 32 * (size_t)q)
+                            : contains((const int64_t*)j->outputs, j->offs[r], j->lens[r], v[q]);
+      }
       j->flags[r] = (uint8_t)hit;
     }
   }
   free(v);
+  free(xs);
   return NULL;
 }
 
-int cudasp_oracle_scan(const uint8_t scan_key_le[32], const uint8_t spend_key_le[64], const uint8_t* label_keys_le,
-                       uint32_t label_count, const uint8_t* tweaks_le, uint32_t n, const int64_t* outputs,
-                       const uint32_t* offsets, const uint32_t* lengths, uint8_t* flags_out, int64_t* values_out,
-                       int threads) {
+int cudasp_oracle_scan_ex(const uint8_t scan_key_le[32], const uint8_t spend_key_le[64], const uint8_t* label_keys_le,
+                          uint32_t label_count, const uint8_t* tweaks_le, uint32_t n, const cudasp_oracle_options* opt,
+                          const void* outputs, const uint32_t* offsets, const uint32_t* lengths, uint8_t* flags_out,
+                          int64_t* values_out, int threads) {
+  cudasp_oracle_options o = {1, 0, 0};
+  if (opt) o = *opt;
+  if (o.output_count < 1) return -2;
   if (threads < 1) threads = 1;
   if ((uint32_t)threads > n) threads = n ? (int)n : 1;
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
@@ -491,6 +544,7 @@ int cudasp_oracle_scan(const uint8_t scan_key_le[32], const uint8_t spend_key_le
     job_t* j = &jobs[i];
     j->scan = scan_key_le; j->spend = spend_key_le; j->labels = label_keys_le; j->tweaks = tweaks_le;
     j->label_count = label_count;
+    j->opt = o;
     j->begin = (uint32_t)((uint64_t)n * i / threads);
     j->end = (uint32_t)((uint64_t)n * (i + 1) / threads);
     j->outputs = outputs; j->offs = offsets; j->lens = lengths;
@@ -505,6 +559,14 @@ int cudasp_oracle_scan(const uint8_t scan_key_le[32], const uint8_t spend_key_le
   free(th);
   free(jobs);
   return rc;
+}
+
+int cudasp_oracle_scan(const uint8_t scan_key_le[32], const uint8_t spend_key_le[64], const uint8_t* label_keys_le,
+                       uint32_t label_count, const uint8_t* tweaks_le, uint32_t n, const int64_t* outputs,
+                       const uint32_t* offsets, const uint32_t* lengths, uint8_t* flags_out, int64_t* values_out,
+                       int threads) {
+  return cudasp_oracle_scan_ex(scan_key_le, spend_key_le, label_keys_le, label_count, tweaks_le, n, NULL, outputs,
+                               offsets, lengths, flags_out, values_out, threads);
 }
 
 /* Synthetic tweak of bench/test tables: T_i = (s0 + i) * G,

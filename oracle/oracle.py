@@ -31,6 +31,11 @@ def load():
         lib.cudasp_oracle_row.restype = ctypes.c_int
         lib.cudasp_oracle_scan.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint32, P, P, P, P, P, ctypes.c_int]
         lib.cudasp_oracle_scan.restype = ctypes.c_int
+        lib.cudasp_oracle_row_ex.argtypes = [P, P, P, ctypes.c_uint32, P, P, P, P, P]
+        lib.cudasp_oracle_row_ex.restype = ctypes.c_int
+        lib.cudasp_oracle_scan_ex.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint32, P, P, P, P, P, P,
+                                              ctypes.c_int]
+        lib.cudasp_oracle_scan_ex.restype = ctypes.c_int
         lib.cudasp_oracle_synth_tweak.argtypes = [P, ctypes.c_uint64, P]
         lib.cudasp_oracle_synth_tweak.restype = ctypes.c_int
         lib.cudasp_oracle_sha256.argtypes = [P, P, ctypes.c_size_t]
@@ -72,6 +77,57 @@ def scan(scan_key, spend_key, labels, tweaks, outputs=None, offsets=None, length
     outs_ptr = ptr(outputs) if (outputs is not None and outputs.size) else None
     lib.cudasp_oracle_scan(scan_key, spend_key, lab, L, ptr(tw), n, outs_ptr, ptr(offsets), ptr(lengths),
                            ptr(flags), ptr(values), int(threads))
+    return flags, values
+
+
+class _Options(ctypes.Structure):
+    _fields_ = [("output_count", ctypes.c_uint32), ("label_negation", ctypes.c_uint32),
+                ("full_x", ctypes.c_uint32)]
+
+
+def row_ex(scan, spend, labels, tweak, output_count=1, label_negation=False):
+    """-> (K digests (32 BE bytes each), values [K][1 + L'], xs [K][1 + L'] as
+    32-byte BE x or None at infinity) for the protocol variants."""
+    lib = load()
+    L = len(labels)
+    W = 1 + (2 if label_negation else 1) * L
+    K = output_count
+    opt = _Options(K, int(bool(label_negation)), 0)
+    t = ctypes.create_string_buffer(32 * K)
+    xs = ctypes.create_string_buffer(32 * K * W)
+    vals = (ctypes.c_int64 * (K * W))()
+    lab = b"".join(labels) if labels else None
+    if lib.cudasp_oracle_row_ex(scan, spend, lab, L, tweak, ctypes.byref(opt), t, xs, vals) != 0:
+        raise ValueError("degenerate row (point at infinity)")
+    v = [list(vals[k * W:(k + 1) * W]) for k in range(K)]
+    x = [[None if v[k][c] == LABEL_INFINITY and c else xs.raw[32 * (k * W + c):32 * (k * W + c + 1)]
+          for c in range(W)] for k in range(K)]
+    return [t.raw[32 * k:32 * (k + 1)] for k in range(K)], v, x
+
+
+def scan_ex(scan_key, spend_key, labels, tweaks, outputs=None, offsets=None, lengths=None, output_count=1,
+            label_negation=False, full_x=False, threads=1, want_values=False):
+    """scan() for the protocol variants: outputs are int64 values, or with
+    full_x a uint8 [total, 32] array of BE x-only keys.  values: int64
+    [n, K, 1 + L']."""
+    lib = load()
+    tw = np.ascontiguousarray(tweaks, dtype=np.uint8).reshape(-1, 64)
+    n = tw.shape[0]
+    L = len(labels)
+    W = 1 + (2 if label_negation else 1) * L
+    lab = b"".join(labels) if labels else None
+    opt = _Options(output_count, int(bool(label_negation)), int(bool(full_x)))
+    flags = None
+    if outputs is not None:
+        outputs = np.ascontiguousarray(outputs, dtype=np.uint8 if full_x else np.int64)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        flags = np.zeros(n, dtype=np.uint8)
+    values = np.zeros((n, output_count, W), dtype=np.int64) if want_values else None
+    ptr = lambda a: None if a is None else a.ctypes.data
+    outs_ptr = ptr(outputs) if (outputs is not None and outputs.size) else None
+    lib.cudasp_oracle_scan_ex(scan_key, spend_key, lab, L, ptr(tw), n, ctypes.byref(opt), outs_ptr, ptr(offsets),
+                              ptr(lengths), ptr(flags), ptr(values), int(threads))
     return flags, values
 
 

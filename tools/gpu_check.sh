@@ -1,11 +1,7 @@
-# Usage (on the GPU box): bash tools/gpu_check.sh [tag]
-# pytest -m gpu, then stage timings at 300k rows for 0/1/16 labels.
+# GPU tests (one process, per-test time limit), then a short bench.
 set -o pipefail
-mkdir -p gpurun_out
-TAG=${1:-check}
-timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/${TAG}_pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
-tail -1 gpurun_out/${TAG}_pytest.log
-for L in 0 1 16; do
-  timeout -k 10 120 python tools/quick_timing.py 300000 $L >> gpurun_out/${TAG}_timing.log 2>&1 || { echo "timing failed"; tail -20 gpurun_out/${TAG}_timing.log; exit 1; }
-done
-grep "rows/s" gpurun_out/${TAG}_timing.log
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O; cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/check_pytest.log 2>&1 || { grep -E "PASS|FAIL|Error|error" $O/check_pytest.log | tail -30; tail -30 $O/check_pytest.log; exit 1; }
+tail -1 $O/check_pytest.log
+timeout -k 10 300 python bench.py --steps 3 --no-cpu-baseline > $O/check_bench.log 2>&1 || { tail -20 $O/check_bench.log; exit 1; }
+python -c "import json,sys; d=json.loads(open('$O/check_bench.log').read().strip().splitlines()[-1]); print(d['value']/1e6, d['matches'])"
