@@ -39,6 +39,9 @@ namespace {
 
 constexpr uint64_t TWEAK_KEY_SIZE = 64;  // CudaspScanBindData::TWEAK_KEY_SIZE
 constexpr uint64_t SCALAR_SIZE = 32;     // CudaspScanBindData::SCALAR_SIZE
+constexpr uint32_t XONLY_SIZE = 32;      // full_x outputs: x-only keys
+// int64 words per output in the host/device outputs buffers.
+inline size_t out_words(const cudasp_tf_bind_data& b);
 
 void write_err(char* err, size_t cap, const char* fmt, ...) {
   if (!err || cap == 0) return;
@@ -54,11 +57,16 @@ extern "C" void cudasp_internal_set_error(const char* msg);
 
 struct cudasp_tf_bind_data {
   uint64_t batch_size = CUDASP_TF_DEFAULT_BATCH;
+  cudasp_scan_options opt{1, 0, 0};  // named parameters output_count / label_negation / full_x
   std::string scan_private_key_data;
   std::string spend_public_key_data;
   std::vector<std::string> label_keys_data;
   std::string label_keys_flat;  // label_count x 64, back to back
 };
+
+namespace {
+inline size_t out_words(const cudasp_tf_bind_data& b) { return b.opt.full_x ? XONLY_SIZE / 8 : 1; }
+}  // namespace
 
 struct cudasp_tf_global {
   std::atomic<uint64_t> currently_adding{0};
@@ -147,13 +155,14 @@ struct DeviceSet {
   }
 };
 
-int ensure_outputs_cap(HostSlot& s, size_t need) {
+// need: int64 words; ow: words per output already held (n_outputs * ow used).
+int ensure_outputs_cap(HostSlot& s, size_t need, size_t ow = 1) {
   if (need <= s.outputs_cap) return CUDASP_OK;
   size_t cap = s.outputs_cap ? s.outputs_cap : 4096;
   while (cap < need) cap *= 2;
   int64_t* p = nullptr;
   HOST_HIP(hipHostMalloc((void**)&p, cap * sizeof(int64_t), hipHostMallocDefault));
-  if (s.n_outputs) memcpy(p, s.h_outputs, s.n_outputs * sizeof(int64_t));
+  if (s.n_outputs) memcpy(p, s.h_outputs, s.n_outputs * ow * sizeof(int64_t));
   if (s.h_outputs) (void)hipHostFree(s.h_outputs);
   s.h_outputs = p;
   s.outputs_cap = cap;
@@ -255,6 +264,7 @@ int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
   const auto nlabels = (uint32_t)b.label_keys_data.size();
   if (GpuCtx* c = pool_take(l.assigned_gpu, cap_rows)) {
     int rc = cudasp_scanner_set_keys(c->scanner, scan, spend, labels, nlabels);
+    if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(c->scanner, &b.opt);
     if (rc != CUDASP_OK) {
       pool_put(c);
       return host_fail(rc, "Failed to bind scanner on GPU %d: %s", l.assigned_gpu, cudasp_last_error());
@@ -264,6 +274,7 @@ int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
   }
   l.cap_rows = cap_rows;
   int rc = cudasp_scanner_create(l.assigned_gpu, scan, spend, labels, nlabels, l.cap_rows, &l.scanner);
+  if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(l.scanner, &b.opt);
   if (rc != CUDASP_OK)
     return host_fail(rc, "Failed to create scanner on GPU %d: %s", l.assigned_gpu, cudasp_last_error());
   HOST_HIP(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
@@ -316,6 +327,9 @@ int accumulate(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const cudasp_tf
   int rc = ensure_local_gpu(b, l);
   if (rc != CUDASP_OK) return rc;
   HostSlot& s = l.slots[l.cur];
+  const size_t ow = out_words(b);
+  if (b.opt.full_x && c.count > 0 && (!c.child_blob_data || !c.child_blob_size))
+    return host_fail(CUDASP_ERR_INVALID_ARG, "full_x needs the outputs column as BLOB[] (child_blob_data)");
   for (uint32_t i = 0; i < c.count; i++) {
     // Only rows with valid txid, height and tweak_key (:195-197).
     if (!(valid(c.txid_valid, i) && valid(c.height_valid, i) && valid(c.tweak_valid, i))) continue;
@@ -331,14 +345,21 @@ int accumulate(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const cudasp_tf
     s.h_offs[r] = (uint32_t)s.n_outputs;
     uint32_t len = 0;
     if (valid(c.list_valid, i)) {
-      rc = ensure_outputs_cap(s, s.n_outputs + c.list_length[i]);
+      rc = ensure_outputs_cap(s, (s.n_outputs + c.list_length[i]) * ow, ow);
       if (rc != CUDASP_OK) return rc;
       for (uint64_t k = 0; k < c.list_length[i]; k++) {
         uint64_t ci = c.list_offset[i] + k;
-        if (valid(c.child_valid, (uint32_t)ci)) {
+        if (!valid(c.child_valid, (uint32_t)ci)) continue;
+        if (b.opt.full_x) {
+          if (c.child_blob_size[ci] != XONLY_SIZE)
+            return host_fail(CUDASP_ERR_INVALID_ARG, "full_x outputs must be 32-byte x-only keys, got %u bytes",
+                             c.child_blob_size[ci]);
+          memcpy(s.h_outputs + s.n_outputs * ow, c.child_blob_data[ci], XONLY_SIZE);
+          s.n_outputs++;
+        } else {
           s.h_outputs[s.n_outputs++] = c.child_values[ci];
-          len++;
         }
+        len++;
       }
     }
     s.h_lens[r] = len;
@@ -358,6 +379,31 @@ int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const c
   if (rc != CUDASP_OK) return rc;
   HostSlot& s = l.slots[l.cur];
   const uint64_t n = r1 - r0;
+  const size_t ow = out_words(b);
+  // full_x: the outputs child is binary (child_blob_offsets) or
+  // fixed_size_binary(child_blob_fixed_width) of 32-byte x-only keys.
+  auto child_blob = [&](uint64_t k, uint32_t* size) -> const uint8_t* {
+    const uint64_t ck = c.child_offset + k;
+    if (c.child_blob_offsets) {
+      *size = (uint32_t)(c.child_blob_offsets[ck + 1] - c.child_blob_offsets[ck]);
+      return c.child_blob_data + c.child_blob_offsets[ck];
+    }
+    *size = (uint32_t)c.child_blob_fixed_width;
+    return c.child_blob_data + ck * (uint64_t)c.child_blob_fixed_width;
+  };
+  auto push_output = [&](uint64_t k) -> int {
+    if (!b.opt.full_x) {
+      s.h_outputs[s.n_outputs++] = c.child_values[c.child_offset + k];
+      return CUDASP_OK;
+    }
+    uint32_t sz;
+    const uint8_t* p = child_blob(k, &sz);
+    if (sz != XONLY_SIZE)
+      return host_fail(CUDASP_ERR_INVALID_ARG, "full_x outputs must be 32-byte x-only keys, got %u bytes", sz);
+    memcpy(s.h_outputs + s.n_outputs * ow, p, XONLY_SIZE);
+    s.n_outputs++;
+    return CUDASP_OK;
+  };
   const int32_t* txo = c.txid_offsets + c.txid_offset;
   const int32_t* lo = c.list_offsets + c.list_offset;
   auto tweak_ptr = [&](uint64_t i, uint32_t* size) -> const uint8_t* {
@@ -376,6 +422,9 @@ int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const c
   } else if (fast) {
     fast = c.tweak_fixed_width == (int32_t)TWEAK_KEY_SIZE;
   }
+  if (fast && b.opt.full_x) {  // bulk copy only for fixed 32-byte keys
+    fast = !c.child_blob_offsets && c.child_blob_fixed_width == (int32_t)XONLY_SIZE;
+  }
   if (fast) {
     const uint32_t r = s.rows;
     uint32_t sz;
@@ -384,9 +433,13 @@ int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const c
     const size_t tbase = s.txid_bytes.size();
     s.txid_bytes.insert(s.txid_bytes.end(), c.txid_data + txo[r0], c.txid_data + txo[r1]);
     const uint64_t first = (uint64_t)lo[r0], total = (uint64_t)lo[r1] - first;
-    rc = ensure_outputs_cap(s, s.n_outputs + total);
+    rc = ensure_outputs_cap(s, (s.n_outputs + total) * ow, ow);
     if (rc != CUDASP_OK) return rc;
-    memcpy(s.h_outputs + s.n_outputs, c.child_values + c.child_offset + first, total * sizeof(int64_t));
+    if (b.opt.full_x)
+      memcpy(s.h_outputs + s.n_outputs * ow, c.child_blob_data + (c.child_offset + first) * XONLY_SIZE,
+             total * XONLY_SIZE);
+    else
+      memcpy(s.h_outputs + s.n_outputs, c.child_values + c.child_offset + first, total * sizeof(int64_t));
     for (uint64_t i = r0; i < r1; i++) {
       const uint32_t row = r + (uint32_t)(i - r0);
       s.txid_offset.push_back(tbase + (size_t)(txo[i] - txo[r0]));
@@ -415,11 +468,12 @@ int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const c
     s.h_offs[r] = (uint32_t)s.n_outputs;
     uint32_t len = 0;
     if (bit(c.list_validity, c.list_offset + i)) {
-      rc = ensure_outputs_cap(s, s.n_outputs + (uint64_t)(lo[i + 1] - lo[i]));
+      rc = ensure_outputs_cap(s, (s.n_outputs + (uint64_t)(lo[i + 1] - lo[i])) * ow, ow);
       if (rc != CUDASP_OK) return rc;
       for (int64_t k = lo[i]; k < lo[i + 1]; k++) {
         if (bit(c.child_validity, c.child_offset + (uint64_t)k)) {
-          s.h_outputs[s.n_outputs++] = c.child_values[c.child_offset + (uint64_t)k];
+          rc = push_output((uint64_t)k);
+          if (rc != CUDASP_OK) return rc;
           len++;
         }
       }
@@ -462,13 +516,13 @@ int harvest(cudasp_tf_global& g, cudasp_tf_local& l, HostSlot& s) {
 // current slot on the thread's stream and switch to the other slot, first
 // harvesting it if its previous batch is still outstanding.
 int launch_batch(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l) {
-  (void)b;
   HostSlot& s = l.slots[l.cur];
   uint32_t n = s.rows;
   if (n > 0) {
     DeviceSet dg(l.assigned_gpu);
     hipStream_t st = l.stream;
-    if (s.n_outputs > s.d_outputs_cap) {
+    const size_t words = s.n_outputs * out_words(b);
+    if (words > s.d_outputs_cap) {
       if (s.d_outputs) HOST_HIP(hipFree(s.d_outputs));
       s.d_outputs = nullptr;
       size_t cap = s.outputs_cap;
@@ -478,8 +532,7 @@ int launch_batch(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_lo
     HOST_HIP(hipMemcpyAsync(s.d_rows, s.h_tweaks, (size_t)n * 64, hipMemcpyHostToDevice, st));
     HOST_HIP(hipMemcpyAsync(s.d_offs, s.h_offs, (size_t)n * 4, hipMemcpyHostToDevice, st));
     HOST_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, st));
-    if (s.n_outputs)
-      HOST_HIP(hipMemcpyAsync(s.d_outputs, s.h_outputs, s.n_outputs * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    if (words) HOST_HIP(hipMemcpyAsync(s.d_outputs, s.h_outputs, words * sizeof(int64_t), hipMemcpyHostToDevice, st));
     int rc = cudasp_tweaks_to_columns(s.d_rows, n, s.d_tx, s.d_ty, st);
     if (rc == CUDASP_OK)
       rc = cudasp_scan_device(l.scanner, s.d_tx, s.d_ty, s.d_outputs, s.d_offs, s.d_lens, n, s.d_flags, nullptr,
@@ -567,6 +620,28 @@ int cudasp_tf_bind(uint32_t arg_count, cudasp_tf_blob_arg scan_private_key, cuda
     b->label_keys_flat.append((const char*)label_keys[i].data, TWEAK_KEY_SIZE);
   }
   *out = b;
+  return CUDASP_OK;
+}
+
+int cudasp_tf_bind_options(cudasp_tf_bind_data* b, int has_output_count, int64_t output_count,
+                           int has_label_negation, int label_negation, int has_full_x, int full_x, char* err,
+                           size_t err_cap) {
+  if (!b) {
+    write_err(err, err_cap, "null bind data");
+    return CUDASP_ERR_INVALID_ARG;
+  }
+  cudasp_scan_options o = b->opt;
+  if (has_output_count) {
+    if (output_count < 1 || output_count > CUDASP_MAX_OUTPUT_COUNT) {
+      write_err(err, err_cap, "output_count must be between 1 and %d, got %lld", CUDASP_MAX_OUTPUT_COUNT,
+                (long long)output_count);
+      return CUDASP_ERR_INVALID_ARG;
+    }
+    o.output_count = (uint32_t)output_count;
+  }
+  if (has_label_negation) o.label_negation = label_negation ? 1u : 0u;
+  if (has_full_x) o.full_x = full_x ? 1u : 0u;
+  b->opt = o;
   return CUDASP_OK;
 }
 

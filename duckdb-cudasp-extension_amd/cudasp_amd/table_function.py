@@ -45,6 +45,8 @@ class _Chunk(ctypes.Structure):
         ("list_valid", ctypes.POINTER(ctypes.c_uint8)),
         ("child_values", ctypes.POINTER(ctypes.c_int64)),
         ("child_valid", ctypes.POINTER(ctypes.c_uint8)),
+        ("child_blob_data", ctypes.POINTER(ctypes.c_void_p)),
+        ("child_blob_size", ctypes.POINTER(ctypes.c_uint32)),
     ]
 
 
@@ -80,6 +82,9 @@ class _Columns(ctypes.Structure):
         ("child_values", ctypes.c_void_p),
         ("child_validity", ctypes.c_void_p),
         ("child_offset", ctypes.c_uint64),
+        ("child_blob_offsets", ctypes.c_void_p),
+        ("child_blob_data", ctypes.c_void_p),
+        ("child_blob_fixed_width", ctypes.c_int32),
     ]
 
 
@@ -88,6 +93,8 @@ _HOST_SIGNATURES = {
     "cudasp_tf_bind": (ctypes.c_int, [ctypes.c_uint32, _BlobArg, _BlobArg, ctypes.c_int, ctypes.POINTER(_BlobArg),
                                       ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                       ctypes.POINTER(_P), ctypes.c_char_p, ctypes.c_size_t]),
+    "cudasp_tf_bind_options": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
     "cudasp_tf_bind_free": (None, [_P]),
     "cudasp_tf_bind_batch_size": (ctypes.c_uint64, [_P]),
     "cudasp_tf_init": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
@@ -129,7 +136,8 @@ def _blob(value):
 class BoundScan:
     """Bind data of one cudasp_scan call (CudaspScanBindData)."""
 
-    def __init__(self, scan_private_key, spend_public_key, label_keys, batch_size=None, arg_count=4):
+    def __init__(self, scan_private_key, spend_public_key, label_keys, batch_size=None, arg_count=4,
+                 output_count=None, label_negation=None, full_x=None):
         lib = _lib()
         keep = []
         k1, a1 = _blob(scan_private_key)
@@ -151,6 +159,13 @@ class BoundScan:
             raise InvalidInputException(err.value.decode())
         self._h = h
         self.batch_size = lib.cudasp_tf_bind_batch_size(h)
+        # named parameters of the protocol variants (None = not given)
+        rc = lib.cudasp_tf_bind_options(h, output_count is not None, int(output_count or 0),
+                                        label_negation is not None, bool(label_negation), full_x is not None,
+                                        bool(full_x), err, 512)
+        if rc != 0:
+            raise InvalidInputException(err.value.decode())
+        self.full_x = bool(full_x)
 
     def __del__(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -158,8 +173,9 @@ class BoundScan:
             self._h = None
 
 
-def _make_chunk(rows):
-    """Build a DuckDB-like unified chunk from Python rows; returns (keep, chunk)."""
+def _make_chunk(rows, full_x=False):
+    """Build a DuckDB-like unified chunk from Python rows; returns (keep, chunk).
+    With full_x the outputs are BLOB lists (32-byte x-only keys)."""
     n = len(rows)
     keep = []
     txid_ptrs = (ctypes.c_void_p * n)()
@@ -196,14 +212,27 @@ def _make_chunk(rows):
             list_valid[i] = 1
             list_length[i] = len(outs)
             for o in outs:
-                child.append(0 if o is None else o)
+                child.append(o if full_x else (0 if o is None else o))
                 child_ok.append(0 if o is None else 1)
-    cv = (ctypes.c_int64 * max(1, len(child)))(*child)
     cvalid = (ctypes.c_uint8 * max(1, len(child_ok)))(*child_ok)
+    if full_x:
+        cv = None
+        bdata = (ctypes.c_void_p * max(1, len(child)))()
+        bsize = (ctypes.c_uint32 * max(1, len(child)))()
+        for i, o in enumerate(child):
+            if o is not None:
+                b = ctypes.create_string_buffer(bytes(o), max(1, len(o)))
+                keep.append(b)
+                bdata[i] = ctypes.cast(b, ctypes.c_void_p)
+                bsize[i] = len(o)
+        keep += [bdata, bsize]
+    else:
+        cv = (ctypes.c_int64 * max(1, len(child)))(*child)
+        bdata, bsize = None, None
     keep += [txid_ptrs, txid_size, txid_valid, height, height_valid, tweak_ptrs, tweak_size, tweak_valid,
              list_offset, list_length, list_valid, cv, cvalid]
     c = _Chunk(n, txid_ptrs, txid_size, txid_valid, height, height_valid, tweak_ptrs, tweak_size, tweak_valid,
-               list_offset, list_length, list_valid, cv, cvalid)
+               list_offset, list_length, list_valid, cv, cvalid, bdata, bsize)
     return keep, c
 
 
@@ -218,13 +247,17 @@ def release_pool():
 
 
 def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size=None, threads=1,
-                chunk_rows=VECTOR_SIZE):
+                chunk_rows=VECTOR_SIZE, output_count=None, label_negation=None, full_x=None):
     """Run the table function over `rows` with `threads` executor threads.
     Chunks are dealt round-robin to the threads, as DuckDB's parallel scan
     would hand out morsels; each thread gets its own local state (and GPU,
-    round-robin, CudaspScanLocalInit :523-529)."""
+    round-robin, CudaspScanLocalInit :523-529).  output_count /
+    label_negation / full_x: the protocol-variant named parameters
+    (cudasp_tf_bind_options); with full_x the outputs are lists of 32-byte
+    x-only keys."""
     lib = _lib()
-    bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size)
+    bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size, output_count=output_count,
+                      label_negation=label_negation, full_x=full_x)
     g = _P()
     _native.check(lib.cudasp_tf_init(bound._h, ctypes.byref(g)))
     locals_ = []
@@ -241,7 +274,7 @@ def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size
         def worker(t):
             try:
                 for ci in range(t, len(chunks), threads):
-                    keep, c = _make_chunk(chunks[ci])
+                    keep, c = _make_chunk(chunks[ci], bound.full_x)
                     rc = lib.cudasp_tf_function(bound._h, g, locals_[t], ctypes.byref(c))
                     if rc < 0:
                         _native.check(rc)
@@ -280,7 +313,7 @@ def _addr(buf):
     return None if buf is None else buf.address
 
 
-def _arrow_pieces(data, piece_rows):
+def _arrow_pieces(data, piece_rows, full_x=False):
     """Record batches of `data` (pa.Table, pa.RecordBatch or an iterable of
     record batches), columns cast to the layouts cudasp_tf_columns takes,
     sliced into pieces of at most piece_rows rows."""
@@ -302,7 +335,11 @@ def _arrow_pieces(data, piece_rows):
             height = height.cast(pa.int32())
         if not (pa.types.is_binary(tweak.type) or pa.types.is_fixed_size_binary(tweak.type)):
             tweak = tweak.cast(pa.binary())
-        if not (pa.types.is_list(outs.type) and pa.types.is_int64(outs.type.value_type)):
+        if full_x:
+            vt = outs.type.value_type if pa.types.is_list(outs.type) else None
+            if not (vt is not None and (pa.types.is_binary(vt) or pa.types.is_fixed_size_binary(vt))):
+                outs = outs.cast(pa.list_(pa.binary()))
+        elif not (pa.types.is_list(outs.type) and pa.types.is_int64(outs.type.value_type)):
             outs = outs.cast(pa.list_(pa.int64()))
         for start in range(0, len(txid), piece_rows):
             m = min(piece_rows, len(txid) - start)
@@ -333,24 +370,32 @@ def _columns(txid, height, tweak, outs):
     c.list_offset = outs.offset
     child = outs.values
     cb = child.buffers()
-    c.child_validity, c.child_values = _addr(cb[0]) if child.null_count else None, _addr(cb[1])
+    c.child_validity = _addr(cb[0]) if child.null_count else None
     c.child_offset = child.offset
+    if pa.types.is_fixed_size_binary(child.type):
+        c.child_blob_data, c.child_blob_fixed_width = _addr(cb[1]), child.type.byte_width
+    elif pa.types.is_binary(child.type):
+        c.child_blob_offsets, c.child_blob_data = _addr(cb[1]), _addr(cb[2])
+    else:
+        c.child_values = _addr(cb[1])
     return c
 
 
 def cudasp_scan_arrow(data, scan_private_key, spend_public_key, label_keys, batch_size=None, threads=1,
-                      piece_rows=65536):
+                      piece_rows=65536, output_count=None, label_negation=None, full_x=None):
     """cudasp_scan over Arrow data (a pyarrow Table / RecordBatch / iterable of
     record batches, e.g. pyarrow.parquet.read_table(...) or DuckDB's
     .arrow()), with the same four columns by position.  Rows reach the
     batch buffers through cudasp_tf_function_columns (bulk copies from the
     Arrow buffers); the semantics and batches equal cudasp_scan's.  Returns a
     pyarrow Table (txid binary, height int32, tweak_key binary) in unspecified
-    row order, like the reference."""
+    row order, like the reference.  output_count / label_negation / full_x as
+    for cudasp_scan (full_x: outputs list<binary> or list<fixed_size_binary(32)>)."""
     import pyarrow as pa
     lib = _lib()
-    bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size)
-    pieces = _arrow_pieces(data, piece_rows)
+    bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size, output_count=output_count,
+                      label_negation=label_negation, full_x=full_x)
+    pieces = _arrow_pieces(data, piece_rows, bound.full_x)
     g = _P()
     _native.check(lib.cudasp_tf_init(bound._h, ctypes.byref(g)))
     locals_ = []

@@ -24,6 +24,7 @@ namespace duckdb {
 
 struct CudaspScanBindData : public TableFunctionData {
 	cudasp_tf_bind_data *handle = nullptr;
+	bool full_x = false; // outputs column is BLOB[] of x-only keys
 	~CudaspScanBindData() override {
 		cudasp_tf_bind_free(handle);
 	}
@@ -91,6 +92,22 @@ static unique_ptr<FunctionData> CudaspScanBind(ClientContext &context, TableFunc
 	                   has_bs, bs_int, bs, &result->handle, err, sizeof(err)) != 0) {
 		throw InvalidInputException(err);
 	}
+	// Protocol variants: output_count := INTEGER,
+	// label_negation := BOOLEAN, full_x := BOOLEAN.
+	auto param = [&](const char *name, int &has, int64_t &v) {
+		auto it = input.named_parameters.find(name);
+		has = it != input.named_parameters.end() && !it->second.IsNull();
+		v = has ? it->second.GetValue<int64_t>() : 0;
+	};
+	int has_k, has_neg, has_fx;
+	int64_t k, neg, fx;
+	param("output_count", has_k, k);
+	param("label_negation", has_neg, neg);
+	param("full_x", has_fx, fx);
+	if (cudasp_tf_bind_options(result->handle, has_k, k, has_neg, neg != 0, has_fx, fx != 0, err, sizeof(err)) != 0) {
+		throw InvalidInputException(err);
+	}
+	result->full_x = has_fx && fx != 0;
 	return_types = {LogicalType::BLOB, LogicalType::INTEGER, LogicalType::BLOB};
 	names = {"txid", "height", "tweak_key"};
 	return std::move(result);
@@ -137,7 +154,9 @@ static OperatorResultType CudaspScanFunction(ExecutionContext &context, TableFun
 	auto &child = ListVector::GetEntry(input.data[3]);
 	UnifiedVectorFormat child_fmt;
 	child.ToUnifiedFormat(ListVector::GetListSize(input.data[3]), child_fmt);
-	auto child_ptr = UnifiedVectorFormat::GetData<int64_t>(child_fmt);
+	// BIGINT[] values, or with full_x BLOB[] x-only keys
+	auto child_ptr = bind.full_x ? nullptr : UnifiedVectorFormat::GetData<int64_t>(child_fmt);
+	auto child_blob_ptr = bind.full_x ? UnifiedVectorFormat::GetData<string_t>(child_fmt) : nullptr;
 
 	vector<const uint8_t *> txid_data(count), tweak_data(count);
 	vector<uint32_t> txid_size(count), tweak_size(count);
@@ -146,6 +165,8 @@ static OperatorResultType CudaspScanFunction(ExecutionContext &context, TableFun
 	vector<uint64_t> list_offset(count), list_length(count);
 	vector<int64_t> child_values;
 	vector<uint8_t> child_valid;
+	vector<const uint8_t *> child_blob_data;
+	vector<uint32_t> child_blob_size;
 	for (idx_t i = 0; i < count; i++) {
 		auto ti = txid.sel->get_index(i), hi = height.sel->get_index(i), wi = tweak.sel->get_index(i),
 		     oi = outs.sel->get_index(i);
@@ -164,18 +185,25 @@ static OperatorResultType CudaspScanFunction(ExecutionContext &context, TableFun
 			tweak_data[i] = reinterpret_cast<const uint8_t *>(tweak_ptr[wi].GetData());
 			tweak_size[i] = static_cast<uint32_t>(tweak_ptr[wi].GetSize());
 		}
-		list_offset[i] = child_values.size();
+		list_offset[i] = child_valid.size();
 		if (list_valid[i]) {
 			auto &e = list_ptr[oi];
 			for (idx_t k = 0; k < e.length; k++) {
 				auto ci = child_fmt.sel->get_index(e.offset + k);
 				child_valid.push_back(child_fmt.validity.RowIsValid(ci));
-				child_values.push_back(child_valid.back() ? child_ptr[ci] : 0);
+				if (bind.full_x) {
+					bool ok = child_valid.back();
+					child_blob_data.push_back(ok ? reinterpret_cast<const uint8_t *>(child_blob_ptr[ci].GetData())
+					                             : nullptr);
+					child_blob_size.push_back(ok ? static_cast<uint32_t>(child_blob_ptr[ci].GetSize()) : 0);
+				} else {
+					child_values.push_back(child_valid.back() ? child_ptr[ci] : 0);
+				}
 			}
 			list_length[i] = e.length;
 		}
 	}
-	cudasp_tf_chunk c;
+	cudasp_tf_chunk c {};
 	c.count = static_cast<uint32_t>(count);
 	c.txid_data = txid_data.data();
 	c.txid_size = txid_size.data();
@@ -190,6 +218,8 @@ static OperatorResultType CudaspScanFunction(ExecutionContext &context, TableFun
 	c.list_valid = list_valid.data();
 	c.child_values = child_values.data();
 	c.child_valid = child_valid.data();
+	c.child_blob_data = child_blob_data.data();
+	c.child_blob_size = child_blob_size.data();
 	if (cudasp_tf_function(bind.handle, g.handle, l.handle, &c) < 0) {
 		throw IOException("cudasp_scan: %s", cudasp_last_error());
 	}
@@ -228,6 +258,9 @@ static void LoadInternal(ExtensionLoader &loader) {
 	func.in_out_function = CudaspScanFunction;
 	func.in_out_function_final = CudaspScanFinalFunction;
 	func.named_parameters["batch_size"] = LogicalType::INTEGER;
+	func.named_parameters["output_count"] = LogicalType::INTEGER;
+	func.named_parameters["label_negation"] = LogicalType::BOOLEAN;
+	func.named_parameters["full_x"] = LogicalType::BOOLEAN;
 	loader.RegisterFunction(func);
 }
 

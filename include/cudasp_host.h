@@ -58,6 +58,18 @@ int cudasp_tf_bind(uint32_t arg_count, cudasp_tf_blob_arg scan_private_key, cuda
                    int label_keys_is_list, const cudasp_tf_blob_arg* label_keys, uint32_t label_count,
                    int has_batch_size, int batch_size_is_integer, int64_t batch_size, cudasp_tf_bind_data** out,
                    char* err, size_t err_cap);
+/* Named parameters of the protocol variants (SURVEY.md 8(f) row 4;
+ * cudasp_scan_options of cudasp_abi.h), applied after cudasp_tf_bind:
+ *   output_count := INTEGER    (1 .. CUDASP_MAX_OUTPUT_COUNT, default 1)
+ *   label_negation := BOOLEAN  (default false)
+ *   full_x := BOOLEAN          (default false; the outputs column is then
+ *                               BLOB[] of 32-byte big-endian x-only keys, fed
+ *                               through the child_blob_* members below)
+ * has_* = 0 keeps the default.  The defaults are the reference's semantics.
+ * On failure returns a negative code and writes the message into err. */
+int cudasp_tf_bind_options(cudasp_tf_bind_data* b, int has_output_count, int64_t output_count,
+                           int has_label_negation, int label_negation, int has_full_x, int full_x, char* err,
+                           size_t err_cap);
 void cudasp_tf_bind_free(cudasp_tf_bind_data* b);
 uint64_t cudasp_tf_bind_batch_size(const cudasp_tf_bind_data* b);
 
@@ -98,6 +110,9 @@ typedef struct {
   const uint8_t* list_valid;
   const int64_t* child_values;
   const uint8_t* child_valid;
+  /* full_x: the outputs child vector as BLOBs (32 bytes each) */
+  const uint8_t* const* child_blob_data;
+  const uint32_t* child_blob_size;
 } cudasp_tf_chunk;
 
 /* in_out_function: accumulate, run a batch once batch_size rows are held.
@@ -142,6 +157,11 @@ typedef struct {
   const int64_t* child_values;
   const uint8_t* child_validity;
   uint64_t child_offset;
+  /* full_x: the child array as binary (int32 child_blob_offsets) or, when
+   * child_blob_offsets is NULL, fixed_size_binary(child_blob_fixed_width) */
+  const int32_t* child_blob_offsets;
+  const uint8_t* child_blob_data;
+  int32_t child_blob_fixed_width;
 } cudasp_tf_columns;
 
 int cudasp_tf_function_columns(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,

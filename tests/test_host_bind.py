@@ -37,3 +37,16 @@ def test_bind_errors(args, kw, msg):
     with pytest.raises(InvalidInputException) as e:
         bind(*args, **kw)
     assert str(e.value) == msg
+
+
+@pytest.mark.parametrize("k,msg", [
+    (0, "output_count must be between 1 and 64, got 0"),
+    (65, "output_count must be between 1 and 64, got 65"),
+    (-3, "output_count must be between 1 and 64, got -3"),
+])
+def test_variant_parameter_errors(k, msg):
+    """Named parameters of the protocol variants (cudasp_tf_bind_options)."""
+    with pytest.raises(InvalidInputException) as e:
+        bind(SCAN, SPEND, [], output_count=k)
+    assert str(e.value) == msg
+    assert bind(SCAN, SPEND, [], output_count=64, label_negation=True, full_x=True).full_x

@@ -171,3 +171,54 @@ def test_synthetic_batch_against_oracle(torch_cuda):
         s.sync()
         got = dv.cpu().numpy().reshape(s.value_rows, 2, n).transpose(2, 1, 0)
     assert (got == vals).all()
+
+
+def _tf_rows(rows, outs, offs, lens, full_x):
+    out = []
+    for i, r in enumerate(rows):
+        o = [bytes(outs[k]) if full_x else int(outs[k]) for k in range(offs[i], offs[i] + lens[i])]
+        out.append((i.to_bytes(32, "big"), 1000 + i, bytes.fromhex(r["tweak"]), o))
+    return out
+
+
+@pytest.mark.parametrize("K,neg,full_x", [(2, True, False), (2, True, True), (3, False, True)])
+def test_table_function_variants(torch_cuda, K, neg, full_x):
+    """The named parameters through the C++ table-function host (row chunks
+    and Arrow columns), against the oracle's flags."""
+    import pyarrow as pa
+    from cudasp_amd import cudasp_scan, cudasp_scan_arrow
+    scan, spend, labels, rows = _case()
+    tw = golden_io.tweak_array([r["tweak"] for r in rows])
+    outs, offs, lens = _outputs(scan, spend, labels, rows, K, neg, full_x)
+    want, _ = oracle.scan_ex(scan, spend, labels, tw, outs, offs, lens, output_count=K, label_negation=neg,
+                             full_x=full_x)
+    expect = sorted(1000 + i for i in np.flatnonzero(want))
+    trows = _tf_rows(rows, outs, offs, lens, full_x)
+    got = cudasp_scan(trows, scan, spend, labels, batch_size=20, threads=2, chunk_rows=16, output_count=K,
+                      label_negation=neg, full_x=full_x)
+    assert sorted(h for _, h, _ in got) == expect
+    # without the parameters: the reference semantics (a subset of the hits)
+    if not full_x:
+        base = cudasp_scan(trows, scan, spend, labels, batch_size=20)
+        ref, _ = oracle.scan(scan, spend, labels, tw, outs, offs, lens)
+        assert sorted(h for _, h, _ in base) == sorted(1000 + i for i in np.flatnonzero(ref))
+    vt = pa.binary(32) if full_x else pa.int64()
+    for child_type in ([vt, pa.binary()] if full_x else [vt]):
+        table = pa.table({
+            "txid": pa.array([r[0] for r in trows], pa.binary()),
+            "height": pa.array([r[1] for r in trows], pa.int32()),
+            "tweak_key": pa.array([r[2] for r in trows], pa.binary(64)),
+            "outputs": pa.array([r[3] for r in trows], pa.list_(child_type)),
+        })
+        res = cudasp_scan_arrow(table, scan, spend, labels, batch_size=20, threads=2, piece_rows=24,
+                                output_count=K, label_negation=neg, full_x=full_x)
+        assert sorted(res.column("height").to_pylist()) == expect
+
+
+def test_table_function_full_x_rejects_short_keys(torch_cuda):
+    from cudasp_amd import cudasp_scan, _native
+    scan, spend, labels, rows = _case(4)
+    trows = [(b"t", 1, bytes.fromhex(r["tweak"]), [b"\x01" * 31]) for r in rows]
+    with pytest.raises(_native.CudaspError) as e:
+        cudasp_scan(trows, scan, spend, labels, full_x=True)
+    assert "full_x outputs must be 32-byte x-only keys, got 31 bytes" in str(e.value)
