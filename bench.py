@@ -247,7 +247,7 @@ def run_step(tab, scanners, streams, events=None):
                 events.append((e0, e1, e2))
 
 
-def cpu_baseline(tab, labels, sample_rows, threads):
+def cpu_baseline(tab, labels, sample_rows, threads, output_count=1, label_negation=False):
     sys.path.insert(0, ROOT)
     from oracle import oracle  # the C restatement: baseline + checker only
     m = min(sample_rows, tab.sizes[0])
@@ -258,7 +258,8 @@ def cpu_baseline(tab, labels, sample_rows, threads):
     offs = tab.offs[0][:m].cpu().numpy().view(np.uint32)
     lens = tab.lens[0][:m].cpu().numpy().view(np.uint32)
     t0 = time.perf_counter()
-    flags, _ = oracle.scan(SCAN_KEY, SPEND_KEY, labels, tweaks, outs, offs, lens, threads=threads)
+    flags, _ = oracle.scan_ex(SCAN_KEY, SPEND_KEY, labels, tweaks, outs, offs, lens, output_count=output_count,
+                              label_negation=label_negation, threads=threads)
     dt = time.perf_counter() - t0
     gpu_flags = tab.flags[0][:m].cpu().numpy()
     return dict(value=m / dt, unit="tx/s", cores=threads, kind="port",
@@ -276,6 +277,9 @@ def main():
     ap.add_argument("--rows", type=int, default=32_700_000, help="rows per rank")
     ap.add_argument("--batch-size", type=int, default=300_000)
     ap.add_argument("--labels", type=int, default=0)
+    ap.add_argument("--output-count", type=int, default=1,
+                    help="protocol variant: output indices k = 0..K-1 per row (1 = the reference)")
+    ap.add_argument("--label-negation", action="store_true", help="protocol variant: labels also negated")
     ap.add_argument("--outputs-per-row", type=int, default=2)
     ap.add_argument("--outputs-max", type=int, default=0,
                     help="variable outputs per row, uniform in [1, N] (15 -> mean 8, config 5); 0 = fixed")
@@ -309,6 +313,9 @@ def main():
     streams = [torch.cuda.Stream(device) for _ in range(args.streams)]
     scanners = [Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=args.batch_size, device=device)
                 for _ in range(args.streams)]
+    if args.output_count != 1 or args.label_negation:
+        for s in scanners:
+            s.set_options(args.output_count, args.label_negation)
     setup_s = time.perf_counter() - t_setup
 
     def barrier():
@@ -404,6 +411,7 @@ def main():
                                                        if args.outputs_max else str(args.outputs_per_row),
                                                        args.batch_size),
                     rows_per_rank=args.rows, batch_size=args.batch_size, labels=args.labels,
+                    output_count=args.output_count, label_negation=args.label_negation,
                     outputs_per_row=round(mean_k, 3), streams=args.streams, parallelism="dp%d" % world),
         roofline=dict(bound="hbm", achieved=achieved_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                       frac=achieved_gbs / HBM_PEAK_GBS, traffic=traffic,
@@ -415,7 +423,8 @@ def main():
         setup_s=round(setup_s, 2),
     )
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(tab, labels, args.cpu_rows, args.cpu_threads)
+        result["cpu_baseline"] = cpu_baseline(tab, labels, args.cpu_rows, args.cpu_threads, args.output_count,
+                                              args.label_negation)
     if rank == 0:
         print(json.dumps(result), flush=True)
     for s in scanners:
