@@ -133,3 +133,36 @@ def test_full_batch_properties(torch):
         s2.scan_device(x, y, outs, offs, lens, flags)
         s2.sync()
         assert (flags.cpu().numpy() == f1).all()
+
+
+def test_max_batch_size(torch):
+    """The reference's largest batch_size (10,000,000 rows, bind limit
+    src/cudasp_extension.cu:483-486) in one launch: the stage-A scratch is capped
+    below 4 GiB, so the grid is capped and threads take several row groups.
+    Every planted value is found, exactly, and the flags equal those of the
+    same rows scanned as 300000-row batches."""
+    from cudasp_amd import Scanner
+    n = 10_000_000
+    x, y, outs, offs, lens = synth(torch, 5_000_000, n)
+    planted = _plant(torch, x, y, outs, [], every=10007)
+    flags = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    rows = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    with Scanner(SCAN, SPEND, [], max_rows=n) as s:
+        s.scan_device(x, y, outs, offs, lens, flags, rows, cnt)
+        s.sync()
+        c = int(cnt.item())
+        assert c == len(planted)
+        assert sorted(rows[:c].cpu().tolist()) == planted.cpu().tolist()
+        f1 = flags.cpu().numpy()
+    step = 300000
+    parts = []
+    with Scanner(SCAN, SPEND, [], max_rows=step) as s:
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            fl = torch.zeros(b - a, dtype=torch.uint8, device="cuda")
+            s.scan_device(x[:, a:b].contiguous(), y[:, a:b].contiguous(), outs[2 * a:2 * b].contiguous(),
+                          (offs[a:b] - 2 * a).contiguous(), lens[a:b].contiguous(), fl)
+            parts.append(fl)
+        s.sync()
+    assert (torch.cat(parts).cpu().numpy() == f1).all()
