@@ -247,6 +247,52 @@ def run_step(tab, scanners, streams, events=None):
                 events.append((e0, e1, e2))
 
 
+def layout_probe(lib, tab, reps=5):
+    """HBM cost of the data layout alone: k_layout_probe (cudasp_layout_probe)
+    over the whole rank table as one column-major launch, reading exactly the
+    algorithmic bytes of every row with the kernels' thread
+    mapping and no arithmetic.  Timed with HIP events on the current stream,
+    after (and outside) the timed bench steps."""
+    m = tab.sizes
+    k = tab.kmax if tab.kmax else tab.k
+    x = torch.cat([tab.cols(tab.tx, b) for b in range(tab.nb)], dim=1).contiguous()
+    y = torch.cat([tab.cols(tab.ty, b) for b in range(tab.nb)], dim=1).contiguous()
+    lens = torch.cat([tab.lens[b][:m[b]] for b in range(tab.nb)]).contiguous()
+    per_batch_total = [int(tab.lens[b][:m[b]].to(torch.int64).sum().item()) for b in range(tab.nb)]
+    outs = torch.cat([tab.outs[b][:per_batch_total[b]] for b in range(tab.nb)]).contiguous()
+    base = 0
+    offs_parts = []
+    for b in range(tab.nb):
+        offs_parts.append(tab.offs[b][:m[b]] + base)
+        base += per_batch_total[b]
+    offs = torch.cat(offs_parts).contiguous()
+    n = x.shape[1]
+    flags = torch.zeros(n, dtype=torch.uint8, device=x.device)
+    st = _native.stream_arg(torch.cuda.current_stream())
+
+    def launch():
+        _native.check(lib.cudasp_layout_probe(x.data_ptr(), y.data_ptr(), n, outs.data_ptr(), offs.data_ptr(),
+                                              lens.data_ptr(), flags.data_ptr(), st))
+    launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = n * (64 + 8 + 1) + 8 * int(outs.numel())
+    del x, y, lens, outs, offs, flags
+    torch.cuda.empty_cache()
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return dict(kernel="k_layout_probe", rows=n, outputs_per_row=round(int(base) / n, 3),
+                algorithmic_bytes=nbytes, ms=ms, achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=gbs / HBM_PEAK_GBS,
+                note="the scan's algorithmic HBM bytes (73 + 8k per row) moved with the kernels' thread "
+                     "mapping and no arithmetic: the layout's own HBM roofline, one launch over the rank table")
+
+
 def cpu_baseline(tab, labels, sample_rows, threads, output_count=1, label_negation=False):
     sys.path.insert(0, ROOT)
     from oracle import oracle  # the C restatement: baseline + checker only
@@ -287,6 +333,7 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=1200000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-layout-probe", action="store_true")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_k_shared_secret.json"))
     ap.add_argument("--pmc-sq", default=os.path.join(ROOT, "profiles", "r01_pmc_sq_counters.json"))
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) for the barrier/max; gloo to rehearse "
@@ -422,6 +469,15 @@ def main():
         matches=dict(found=found, flagged=flagged, expected_planted=expected),
         setup_s=round(setup_s, 2),
     )
+    if not args.no_layout_probe:
+        result["layout_probe"] = layout_probe(lib, tab)
+        if os.path.exists(args.pmc_summary):
+            with open(args.pmc_summary) as f:
+                probe_traffic = json.load(f).get("probe_hbm_bytes_per_row")
+            if probe_traffic:
+                result["layout_probe"]["traffic_per_row"] = probe_traffic
+                result["layout_probe"]["traffic_ratio"] = probe_traffic / (result["layout_probe"]["algorithmic_bytes"]
+                                                                           / result["layout_probe"]["rows"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(tab, labels, args.cpu_rows, args.cpu_threads, args.output_count,
                                               args.label_negation)

@@ -294,6 +294,35 @@ __global__ __launch_bounds__(BLOCK) void k_rows_to_cols(const uint8_t* __restric
   }
 }
 
+// Layout probe (measurement only; never part of a scan): moves exactly the
+// algorithmic bytes of a row (tweak x and y columns 64 B,
+// offset + length 8 B, outputs 8k B, flag 1 B) with stage A's thread-to-row
+// mapping (ROWS_A rows per thread: g, g + G, ...), so its time and HBM
+// counters show what the column-major layout costs when the arithmetic is
+// free.  The flag is a function of every byte read (nothing is dead code).
+__global__ __launch_bounds__(BLOCK) void k_layout_probe(const uint32_t* __restrict__ tx,
+                                                        const uint32_t* __restrict__ ty, uint32_t n,
+                                                        const int64_t* __restrict__ outputs,
+                                                        const uint32_t* __restrict__ offs,
+                                                        const uint32_t* __restrict__ lens,
+                                                        uint8_t* __restrict__ flags) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t G = (n + ROWS_A - 1) / ROWS_A;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += stride) {
+#pragma unroll
+    for (int j = 0; j < ROWS_A; j++) {
+      const uint32_t row = g + (uint32_t)j * G;
+      if (row >= n) break;
+      uint32_t h = 0;
+#pragma unroll
+      for (int w = 0; w < 8; w++) h = (h ^ tx[(size_t)w * n + row]) + ty[(size_t)w * n + row];
+      const uint32_t off = offs[row], len = lens[row];
+      bool hit = false;
+      for (uint32_t k = 0; k < len; k++) hit |= (uint32_t)outputs[(size_t)off + k] == h;
+      flags[row] = hit ? 1 : 0;
+    }
+  }
+}
 
 // ------------------------------------------------------ synthetic tables
 // Deterministic benchmark/test inputs: tweak T_i = (s0 + i) G
@@ -825,6 +854,19 @@ int cudasp_tweaks_to_columns(const uint8_t* d_tweak_rows, uint32_t n, uint32_t* 
   if (!d_tweak_rows || !d_tweak_x || !d_tweak_y) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   hipLaunchKernelGGL(k_rows_to_cols, dim3(grid_for(n)), dim3(BLOCK), 0, plain_stream(stream), d_tweak_rows, n,
                      d_tweak_x, d_tweak_y);
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
+int cudasp_layout_probe(const uint32_t* d_tweak_x, const uint32_t* d_tweak_y, uint32_t n, const int64_t* d_outputs,
+                        const uint32_t* d_output_offsets, const uint32_t* d_output_lengths, uint8_t* d_flags,
+                        void* stream) {
+  if (n == 0) return CUDASP_OK;
+  if (!d_tweak_x || !d_tweak_y || !d_output_offsets || !d_output_lengths || !d_flags)
+    return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
+  const uint32_t groups = (n + ROWS_A - 1) / ROWS_A;
+  hipLaunchKernelGGL(k_layout_probe, dim3(grid_for(groups)), dim3(BLOCK), 0, plain_stream(stream), d_tweak_x,
+                     d_tweak_y, n, d_outputs, d_output_offsets, d_output_lengths, d_flags);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
 }

@@ -36,6 +36,7 @@ SIGNATURES = {
     "cudasp_tweaks_to_columns": (_I32, [_P, _U32, _P, _P, _P]),
     "cudasp_stage_shared_secret_device": (_I32, [_P, _P, _P, _U32, _P, _P]),
     "cudasp_stage_match_device": (_I32, [_P, _P, _P, _P, _P, _U32, _P, _P, _P, _P]),
+    "cudasp_layout_probe": (_I32, [_P, _P, _U32, _P, _P, _P, _P, _P]),
     "cudasp_synth_tweak_columns": (_I32, [_I32, _P, ctypes.c_uint64, _U32, _P, _P, _P]),
     "cudasp_synth_outputs": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _U32, _P, _P, _P, _P]),
     "cudasp_synth_output_lengths": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _U32, _P, _P]),

@@ -151,6 +151,15 @@ int cudasp_stage_match_device(cudasp_scanner* s, const uint32_t* d_t, const int6
                               const uint32_t* d_output_offsets, const uint32_t* d_output_lengths, uint32_t n,
                               uint8_t* d_match_flags, uint32_t* d_match_rows, uint32_t* d_match_count, void* stream);
 
+/* Layout probe (measurement only): reads the algorithmic bytes of n rows
+ * (tweak columns, offsets, lengths, outputs) and writes a flag per row, with
+ * stage A's thread-to-row mapping and no arithmetic, so rocprof / HIP events
+ * show the HBM cost of the column-major layout on its own.  Asynchronous on
+ * `stream` (NULL = the null stream).  The flags carry no meaning. */
+int cudasp_layout_probe(const uint32_t* d_tweak_x, const uint32_t* d_tweak_y, uint32_t n, const int64_t* d_outputs,
+                        const uint32_t* d_output_offsets, const uint32_t* d_output_lengths, uint8_t* d_flags,
+                        void* stream);
+
 /* Synthetic benchmark tables, generated on `device`:
  * tweak rows T_i = (s0 + first_index + i) G as x/y columns (8 x n each), and
  * k splitmix64 outputs per row: outputs[i*k + j] = splitmix64(seed ^ ((first_index + i)*k + j)),

@@ -166,3 +166,17 @@ def test_max_batch_size(torch):
             parts.append(fl)
         s.sync()
     assert (torch.cat(parts).cpu().numpy() == f1).all()
+
+
+def test_layout_probe_runs(torch):
+    """The measurement-only layout probe (cudasp_layout_probe) touches every
+    row: it writes a 0/1 flag for each, including a partial last row group."""
+    from cudasp_amd import _native
+    n = 300001
+    x, y, outs, offs, lens = synth(torch, 0, n)
+    flags = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    lib = _native.load()
+    _native.check(lib.cudasp_layout_probe(x.data_ptr(), y.data_ptr(), n, outs.data_ptr(), offs.data_ptr(),
+                                          lens.data_ptr(), flags.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert int((flags > 1).sum().item()) == 0

@@ -21,7 +21,7 @@ step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_writ
 cd $R
 python tools/prof_summary.py $O/prof_bench/bench_kernel_trace.csv --out $O/rocprof_bench_summary.json > /dev/null
 python tools/pmc_summary.py sq $O/pmc_sq_counters.json $O/pmc_sq/sq_counter_collection.csv $O/pmc_sq2/sq2_counter_collection.csv --source "rocprofv3 --pmc (two passes) of python3 tools/quick_timing.py 300000 0 (0 labels, 2 outputs/row), per-dispatch averages over full 300k-row dispatches, MI355X" > /dev/null
-python tools/pmc_summary.py hbm $O/pmc_k_shared_secret.json $O/pmc_fetch/fetch_counter_collection.csv $O/pmc_write/write_counter_collection.csv --source "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of python3 bench.py --rows 3000000 --steps 1 --warmup 0 --no-cpu-baseline, full 300k-row dispatches, MI355X" > /dev/null
+python tools/pmc_summary.py hbm $O/pmc_k_shared_secret.json $O/pmc_fetch/fetch_counter_collection.csv $O/pmc_write/write_counter_collection.csv --probe-rows 3000000 --source "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of python3 bench.py --rows 3000000 --steps 1 --warmup 0 --no-cpu-baseline, full 300k-row dispatches, MI355X" > /dev/null
 P="--pmc-sq $O/pmc_sq_counters.json --pmc-summary $O/pmc_k_shared_secret.json"
 step bench_default 400 python bench.py $P
 step bench_cfg3 400 python bench.py --rows 9400000 --labels 1 --steps 3 $P
