@@ -68,15 +68,16 @@ constexpr uint32_t MAX_BLOCKS = 4096;
 #define CUDASP_ROWS_A 4
 #endif
 #ifndef CUDASP_ROWS_B
-#define CUDASP_ROWS_B 4
+#define CUDASP_ROWS_B 6
 #endif
 constexpr int ROWS_A = CUDASP_ROWS_A;
 constexpr int ROWS_B = CUDASP_ROWS_B;
 static_assert(ROWS_A >= 1 && ROWS_A <= 8 && ROWS_B >= 1 && ROWS_B <= 8, "rows per thread");
 // Scratch words per slot: stage A's odd-multiple table + its pending rows;
-// stage B's label prefix products (10 L) + its pending rows.
+// stage B's label prefix products (FW L per row of the thread: one batched
+// inversion for all its rows' labels) + its pending rows.
 constexpr uint32_t VSCRATCH_WORDS = VB_SCRATCH_WORDS + PEND_WORDS * ROWS_A;
-inline uint32_t lscratch_words(uint32_t label_count) { return FW * label_count + PEND_WORDS * ROWS_B; }
+inline uint32_t lscratch_words(uint32_t label_count) { return (FW * label_count + PEND_WORDS) * ROWS_B; }
 }  // namespace
 
 // ----------------------------------------------------------------- kernels
@@ -178,10 +179,11 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
   const uint32_t stride = gridDim.x * blockDim.x;
   const Scratch sc = make_scratch(lscr, stride, slot);
   const uint32_t G = (n + ROWS_B - 1) / ROWS_B;
-  const int PB = FW * (int)k.label_count;
+  const int PB = FW * (int)k.label_count * ROWS_B;
   for (uint32_t g0 = blockIdx.x * blockDim.x; g0 < G; g0 += stride) {
     const uint32_t g = g0 + threadIdx.x;
     int count = 0;
+    uint32_t hits = 0;  // ROWS_B > 1: bit j = row j matches
     if (ROWS_B > 1 && g < G) {
 #pragma unroll 1
       for (int j = 0; j < ROWS_B; j++) {
@@ -196,6 +198,23 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
         count = j + 1;
       }
       pend_invert<ROWS_B>(sc, PB, count);
+      // base values of all rows, then the labels of all rows with one
+      // batched inversion (match_labels_rows)
+#pragma unroll 1
+      for (int j = 0; j < count; j++) {
+        const uint32_t row = g + (uint32_t)j * G;
+        const uint32_t orow = n == n_rows ? row : row % n_rows;
+        gej R;
+        fe zi;
+        pend_load(R, sc, PB, j);
+        scr_load(zi, sc, PEND_ZI(PB, j));
+        const uint32_t off = VALUES ? 0u : offs[orow];
+        const uint32_t len = VALUES ? 0u : lens[orow];
+        if (row_match_base(R, zi, k, outputs, off, len, sc, PB, j, VALUES ? values + row : nullptr)) hits |= 1u << j;
+      }
+      if (k.label_count)
+        hits |= match_labels_rows(k, labels, outputs, offs, lens, g, G, n, n_rows, count, sc, PB,
+                                  VALUES ? values : nullptr);
     }
 #pragma unroll 1
     for (int j = 0; j < ROWS_B; j++) {
@@ -211,14 +230,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
         hit = row_match(t, fb, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
         if (!VALUES) flags[row] = hit ? 1 : 0;
       } else if (j < count) {
-        gej R;
-        fe zi;
-        pend_load(R, sc, PB, j);
-        scr_load(zi, sc, PEND_ZI(PB, j));
-        const uint32_t orow = n == n_rows ? row : row % n_rows;
-        uint32_t off = VALUES ? 0u : offs[orow];
-        uint32_t len = VALUES ? 0u : lens[orow];
-        hit = row_match_finish(R, zi, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
+        hit = (hits >> j) & 1u;
         if (!VALUES) flags[row] = hit ? 1 : 0;
       }
       if (!VALUES && match_rows != nullptr) {

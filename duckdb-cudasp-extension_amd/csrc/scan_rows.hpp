@@ -562,6 +562,103 @@ CUDASP_HD bool row_match_finish(const gej& R, const fe& zi, const ScanConsts& k,
   return hit;
 }
 
+// Denominator (and numerator) of the label sum F + L (F, L affine,
+// normalized): L.x - F.x and L.y - F.y for a chord; 2 F.y and 3 F.x^2 when
+// F == L (doubling); d = 1, num = 0 and `true` (infinity) when F == -L --
+// the reference's Python oracle's cases (scripts/compute_bip352_expected.py:42-46).
+CUDASP_HD bool label_terms(fe& d, fe* num, const ge& F, const ge& L) {
+  if (!fe_equal_norm(L.x, F.x)) {
+    fe_sub<1>(d, L.x, F.x);
+    if (num) fe_sub<1>(*num, L.y, F.y);
+    return false;
+  }
+  if (fe_equal_norm(L.y, F.y)) {
+    fe_add(d, F.y, F.y);
+    if (num) {
+      fe_sqr(*num, F.x);
+      fe_mul_int(*num, *num, 3);
+    }
+    return false;
+  }
+  fe_set_int(d, 1);
+  if (num) fe_set_int(*num, 0);
+  return true;
+}
+
+// Stage B, base half of a pending row: F affine from (R, 1/Z), the base
+// compare value and match; F is written back over the row's pending X / Y
+// words for match_labels_rows.
+CUDASP_HD bool row_match_base(const gej& R, const fe& zi, const ScanConsts& k, const int64_t* outputs,
+                              uint32_t off, uint32_t len, const Scratch& sc, int pb, int j, int64_t* value) {
+  ge F;
+  gej_to_ge_zinv(F, R, zi);
+  scr_store(sc, PEND_X(pb, j), F.x);
+  scr_store(sc, PEND_Y(pb, j), F.y);
+  int64_t v = fe_upper64(F.x);
+  if (value) *value = v;
+  return outputs_match(k, outputs, off, len, F.x, v);
+}
+
+// Label sums F_j + L_l of a thread's pending rows j < count (rows g + j G),
+// all with ONE batched inversion over the count x L denominators (Montgomery's
+// trick; prefix products at scratch words (j L + l) FW) instead of one per
+// row.  Same values and hits as row_match_finish.  Returns the rows with a
+// label hit as a bit mask; with `values` (then outputs/offs/lens unused) the
+// label values go to values[(1 + l) n + row].
+CUDASP_HD uint32_t match_labels_rows(const ScanConsts& k, const uint32_t* labels, const int64_t* outputs,
+                                     const uint32_t* offs, const uint32_t* lens, uint32_t g, uint32_t G, uint32_t n,
+                                     uint32_t n_rows, int count, const Scratch& sc, int pb, int64_t* values) {
+  const int L = (int)k.label_count;
+  fe acc;
+  fe_set_int(acc, 1);
+  for (int j = 0; j < count; j++) {
+    ge F;
+    scr_load(F.x, sc, PEND_X(pb, j));
+    scr_load(F.y, sc, PEND_Y(pb, j));
+    for (int l = 0; l < L; l++) {
+      ge Ll;
+      ge_from_words(Ll, labels + (size_t)l * 16);
+      fe d;
+      label_terms(d, nullptr, F, Ll);
+      scr_store(sc, (j * L + l) * FW, acc);
+      fe_mul(acc, acc, d);
+    }
+  }
+  fe inv;
+  fe_inv(inv, acc);
+  uint32_t hits = 0;
+  for (int j = count - 1; j >= 0; j--) {
+    const uint32_t row = g + (uint32_t)j * G;
+    const uint32_t orow = n == n_rows ? row : row % n_rows;
+    const uint32_t off = values ? 0u : offs[orow];
+    const uint32_t len = values ? 0u : lens[orow];
+    ge F;
+    scr_load(F.x, sc, PEND_X(pb, j));
+    scr_load(F.y, sc, PEND_Y(pb, j));
+    bool hit = false;
+    for (int l = L - 1; l >= 0; l--) {
+      ge Ll;
+      ge_from_words(Ll, labels + (size_t)l * 16);
+      fe d, num, pre, dinv;
+      const bool infinity = label_terms(d, &num, F, Ll);
+      scr_load(pre, sc, (j * L + l) * FW);
+      fe_mul(dinv, inv, pre);
+      fe_mul(inv, inv, d);
+      fe lam, x3;
+      fe_mul(lam, num, dinv);
+      fe_sqr(x3, lam);
+      fe_sub<1>(x3, x3, F.x);
+      fe_sub<1>(x3, x3, Ll.x);
+      fe_normalize(x3);
+      const int64_t vl = infinity ? LABEL_INFINITY : fe_upper64(x3);
+      if (values) values[(size_t)(1 + l) * n + row] = vl;
+      if (!infinity) hit = hit || outputs_match(k, outputs, off, len, x3, vl);
+    }
+    if (hit) hits |= 1u << j;
+  }
+  return hits;
+}
+
 // Stage B for one row (one inversion per row).
 CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k,
                          const uint32_t* labels, const int64_t* outputs, uint32_t off, uint32_t len,

@@ -155,3 +155,26 @@ def test_default_stream_ordering(torch_cuda):
             s.row_values_device(dx, dy, dt, dv)
             s.sync()
             assert [int(v) for v in dv.cpu().numpy()[0]] == [r["v"] for r in rows]
+
+
+def test_exceptional_label_sums_shared_inversion(torch_cuda):
+    """Label sums that hit the exceptional cases -- F == L_j (doubling) and
+    F == -L_j (infinity, INT64_MIN) -- inside the batched inversion that all
+    rows of a thread share (match_labels_rows), next to ordinary labels and
+    rows; values bit-exact against the oracle, which follows the reference's
+    Python oracle there (scripts/compute_bip352_expected.py:42-46)."""
+    import variants as V
+    from cudasp_amd import Scanner
+    from oracle import oracle
+    rr = golden_io.load("random_rows.json")
+    rows = rr["rows"][:13]
+    scan, spend = bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"])
+    F = [V.row(scan, spend, [], bytes.fromhex(r["tweak"]))[0][0][0] for r in rows[:3]]
+    labels = [V.point_blob(F[0]), bytes.fromhex(rr["label_keys"][0]), V.point_blob(V.neg(F[1])),
+              V.point_blob(F[2])]
+    tw = golden_io.tweak_array([r["tweak"] for r in rows])
+    with Scanner(scan, spend, labels, max_rows=len(rows)) as s:
+        _, vals = _values(torch_cuda, s, tw)
+    _, want = oracle.scan(scan, spend, labels, tw, want_values=True)
+    assert (vals.T == want).all()
+    assert want[1, 3] == oracle.LABEL_INFINITY
