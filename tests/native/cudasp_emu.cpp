@@ -307,4 +307,53 @@ int emu_row_values(const uint8_t scan[32], const uint8_t spend[64], const uint8_
   return 0;
 }
 
+// The kernel's grouped stage B (k_match with ROWS_B > 1): rows g .. g+R-1
+// share one Z inversion (pend_invert) and one label inversion
+// (match_labels_rows).  values (column-major, values[c * n + row], c = 0 base,
+// 1.. labels) or flags with the outputs CSR -- one of the two per call, as in
+// the kernel's VALUES / match modes.
+int emu_row_values_grouped(const uint8_t scan[32], const uint8_t spend[64], const uint8_t* labels_bytes, uint32_t L,
+                           const uint8_t* tweaks, uint32_t n, int R, int64_t* values, const int64_t* outputs,
+                           const uint32_t* offs, const uint32_t* lens, uint8_t* flags) {
+  if (R < 1 || R > 8) return CUDASP_ERR_INVALID_ARG;
+  ScanConsts k;
+  std::vector<int8_t> naf;
+  std::vector<uint32_t> labels;
+  std::string err;
+  int rc = prepare_scan(scan, spend, labels_bytes, L, k, naf, labels, err);
+  if (rc != CUDASP_OK) return rc;
+  std::vector<uint32_t> vscr(VB_SCRATCH_WORDS);
+  std::vector<uint32_t> lscr((size_t)(FW * L + PEND_WORDS) * R);
+  Scratch sa{vscr.data(), 1, 0}, sb{lscr.data(), 1, 0};
+  const int PB = FW * (int)L * R;
+  LazyTable& tab = lazy_table();
+  for (uint32_t g = 0; g < n; g += (uint32_t)R) {
+    const int count = (int)(n - g < (uint32_t)R ? n - g : (uint32_t)R);
+    for (int j = 0; j < count; j++) {
+      uint32_t x[8], y[8], t[8];
+      words_from_row(x, y, tweaks + 64 * (size_t)(g + j));
+      row_shared_secret(t, x, y, naf.data(), k.naf_len, k.mid, sa);
+      tab.ensure_for(t);
+      gej P;
+      row_match_point(P, t, tab.table, k);
+      pend_store(sb, PB, j, P);
+    }
+    pend_invert<8>(sb, PB, count);
+    uint32_t hits = 0;
+    for (int j = 0; j < count; j++) {
+      const uint32_t row = g + (uint32_t)j;
+      gej P;
+      fe zi;
+      pend_load(P, sb, PB, j);
+      scr_load(zi, sb, PEND_ZI(PB, j));
+      const uint32_t off = values ? 0u : offs[row], len = values ? 0u : lens[row];
+      if (row_match_base(P, zi, k, outputs, off, len, sb, PB, j, values ? values + row : nullptr)) hits |= 1u << j;
+    }
+    if (L) hits |= match_labels_rows(k, labels.data(), outputs, offs, lens, g, 1, n, n, count, sb, PB, values);
+    if (flags)
+      for (int j = 0; j < count; j++) flags[g + j] = (hits >> j) & 1u;
+  }
+  return 0;
+}
+
 }  // extern "C"

@@ -286,3 +286,51 @@ def test_shared_inversion(emu):
         emu.emu_pend_invert(buf, len(zs), out)
         got = [int.from_bytes(bytes(out[32 * j:32 * j + 32]), "little") for j in range(len(zs))]
         assert got == [pow(z, P - 2, P) if z % P else 0 for z in zs], zs
+
+
+def _grouped(emu, scan, spend, labels, tw, R, outs=None, offs=None, lens=None):
+    n = len(tw) // 64
+    L = len(labels)
+    emu.emu_row_values_grouped.restype = ctypes.c_int
+    P_ = ctypes.c_void_p
+    emu.emu_row_values_grouped.argtypes = [P_, P_, P_, ctypes.c_uint32, P_, ctypes.c_uint32, ctypes.c_int, P_, P_, P_,
+                                           P_, P_]
+    lab = b"".join(labels) if labels else None
+    vals = (ctypes.c_int64 * (n * (1 + L)))()
+    assert emu.emu_row_values_grouped(scan, spend, lab, L, tw, n, R, vals, None, None, None, None) == 0
+    v = np.frombuffer(vals, dtype=np.int64).reshape(1 + L, n).T
+    f = None
+    if outs is not None:
+        fl = (ctypes.c_uint8 * n)()
+        p = lambda a: a.ctypes.data
+        assert emu.emu_row_values_grouped(scan, spend, lab, L, tw, n, R, None, p(outs) if outs.size else None,
+                                          p(offs), p(lens), fl) == 0
+        f = np.frombuffer(fl, dtype=np.uint8)
+    return v, f
+
+
+def test_grouped_stage_b_shared_label_inversion(emu):
+    """The kernel's grouped stage B (k_match, ROWS_B rows per thread): one Z
+    inversion and one label inversion shared by all rows of the group
+    (match_labels_rows), with the magnitude checks on.  Values equal the
+    per-row path and the oracle, including exceptional label sums inside the
+    shared batch and partial groups; flags equal the fixtures'."""
+    rr = golden_io.load("random_rows.json")
+    rows = rr["rows"][:14]
+    scan, spend = bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"])
+    tw = golden_io.tweak_array([r["tweak"] for r in rows])
+    labels = [bytes.fromhex(l) for l in rr["label_keys"]]
+    outs, offs, lens = golden_io.csr([r["outputs"] for r in rows])
+    per_row, _, _ = _values(emu, scan, spend, labels, tw.tobytes())
+    for R in (1, 4, 6, 8):
+        v, f = _grouped(emu, scan, spend, labels, tw.tobytes(), R, outs, offs, lens)
+        assert (v == per_row).all(), R
+        assert [bool(x) for x in f] == [r["match_all_labels"] for r in rows], R
+    # exceptional sums: L == F of row 0 (doubling), L == -F of row 1 (infinity)
+    import variants as Vv
+    F = [Vv.row(scan, spend, [], bytes.fromhex(r["tweak"]))[0][0][0] for r in rows[:2]]
+    ex = [Vv.point_blob(F[0]), labels[0], Vv.point_blob(Vv.neg(F[1]))]
+    v, _ = _grouped(emu, scan, spend, ex, tw.tobytes(), 6)
+    _, ov = oracle.scan(scan, spend, ex, tw, want_values=True)
+    assert (v == ov).all()
+    assert ov[1, 3] == oracle.LABEL_INFINITY
