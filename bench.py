@@ -471,7 +471,8 @@ def main():
     )
     if not args.no_layout_probe:
         result["layout_probe"] = layout_probe(lib, tab)
-        if os.path.exists(args.pmc_summary):
+        if os.path.exists(args.pmc_summary) and not args.outputs_max and args.outputs_per_row == 2:
+            # the PMC pass profiles the probe at 2 outputs per row (tools/gpu_measure.sh)
             with open(args.pmc_summary) as f:
                 probe_traffic = json.load(f).get("probe_hbm_bytes_per_row")
             if probe_traffic:
