@@ -294,24 +294,41 @@ def layout_probe(lib, tab, reps=5):
 
 
 def cpu_baseline(tab, labels, sample_rows, threads, output_count=1, label_negation=False):
+    """The CPU oracle (oracle/cudasp_oracle.c, `port`) timed on this box's host
+    cores over the first `sample_rows` rows of the rank table (whole batches,
+    so several scanners/streams are covered), and its flags compared row by
+    row with the GPU's flags of the last timed step."""
     sys.path.insert(0, ROOT)
     from oracle import oracle  # the C restatement: baseline + checker only
-    m = min(sample_rows, tab.sizes[0])
-    x = tab.cols(tab.tx, 0)[:, :m].cpu().numpy().view(np.uint32)
-    y = tab.cols(tab.ty, 0)[:, :m].cpu().numpy().view(np.uint32)
-    tweaks = np.ascontiguousarray(np.concatenate([x.T, y.T], axis=1).astype("<u4")).view(np.uint8).reshape(m, 64)
-    outs = tab.outs[0].cpu().numpy()
-    offs = tab.offs[0][:m].cpu().numpy().view(np.uint32)
-    lens = tab.lens[0][:m].cpu().numpy().view(np.uint32)
+    tw, outs, offs, lens, gflags = [], [], [], [], []
+    base, m = 0, 0
+    for b in range(tab.nb):
+        if m >= sample_rows:
+            break
+        mb = min(tab.sizes[b], sample_rows - m)
+        x = tab.cols(tab.tx, b)[:, :mb].cpu().numpy().view(np.uint32)
+        y = tab.cols(tab.ty, b)[:, :mb].cpu().numpy().view(np.uint32)
+        tw.append(np.ascontiguousarray(np.concatenate([x.T, y.T], axis=1).astype("<u4")).view(np.uint8).reshape(mb, 64))
+        ln = tab.lens[b][:mb].cpu().numpy().view(np.uint32)
+        of = tab.offs[b][:mb].cpu().numpy().view(np.uint32)
+        used = int(of[-1]) + int(ln[-1]) if mb else 0
+        outs.append(tab.outs[b][:used].cpu().numpy())
+        offs.append(of + np.uint32(base))
+        lens.append(ln)
+        gflags.append(tab.flags[b][:mb].cpu().numpy())
+        base += used
+        m += mb
+    tweaks = np.concatenate(tw)
+    outs, offs, lens, gflags = np.concatenate(outs), np.concatenate(offs), np.concatenate(lens), np.concatenate(gflags)
     t0 = time.perf_counter()
     flags, _ = oracle.scan_ex(SCAN_KEY, SPEND_KEY, labels, tweaks, outs, offs, lens, output_count=output_count,
                               label_negation=label_negation, threads=threads)
     dt = time.perf_counter() - t0
-    gpu_flags = tab.flags[0][:m].cpu().numpy()
+    nb = len(tw)
     return dict(value=m / dt, unit="tx/s", cores=threads, kind="port",
-                sample="first %d rows of the rank-0 table (batch 0), %d labels, "
-                       "oracle/cudasp_oracle.c with %d pthreads" % (m, len(labels), threads),
-                seconds=round(dt, 3), flags_match_gpu=bool(np.array_equal(flags, gpu_flags)),
+                sample="first %d rows (%d batches) of the rank-0 table, %d labels, oracle/cudasp_oracle.c with %d "
+                       "pthreads" % (m, nb, len(labels), threads),
+                seconds=round(dt, 3), flags_match_gpu=bool(np.array_equal(flags, gflags)),
                 sample_matches=int(flags.sum()))
 
 
