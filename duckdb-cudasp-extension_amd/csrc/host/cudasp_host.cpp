@@ -716,6 +716,14 @@ int cudasp_tf_function_columns(const cudasp_tf_bind_data* b, cudasp_tf_global* g
   if (c.count > 0 && (!c.txid_offsets || !c.txid_data || !c.height || !c.tweak_data || !c.list_offsets ||
                       (!c.tweak_offsets && c.tweak_fixed_width <= 0)))
     return host_fail(CUDASP_ERR_INVALID_ARG, "missing column buffer");
+  if (c.count > 0 && c.list_offsets[c.list_offset + c.count] > c.list_offsets[c.list_offset]) {
+    // the outputs child: int64 values, or with full_x 32-byte keys
+    const bool ok = b->opt.full_x ? (c.child_blob_data && (c.child_blob_offsets || c.child_blob_fixed_width > 0))
+                                  : c.child_values != nullptr;
+    if (!ok)
+      return host_fail(CUDASP_ERR_INVALID_ARG, b->opt.full_x ? "full_x needs the outputs child as binary (child_blob_*)"
+                                                              : "missing outputs child values");
+  }
   // DuckDB-sized pieces, with the same trigger as cudasp_tf_function.
   for (uint64_t r0 = 0; r0 < c.count; r0 += CUDASP_TF_VECTOR_SIZE) {
     const uint64_t r1 = r0 + CUDASP_TF_VECTOR_SIZE < c.count ? r0 + CUDASP_TF_VECTOR_SIZE : c.count;
