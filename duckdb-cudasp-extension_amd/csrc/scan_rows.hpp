@@ -22,12 +22,15 @@ constexpr int NAF_MAX = 136;
 // with FB_ENTRIES odd multiples (2j+1) 2^(FB_BITS i) G, 64 bytes per entry.
 // t (256 bits, made odd) = sum_i d_i 2^(FB_BITS i) + 2^(FB_BITS FB_WINDOWS),
 // so P0 = t G costs FB_WINDOWS gathers + mixed additions.  Default 22 bits:
-// 12 windows, 1.5 GiB per device (16 bits: 16 windows, 32 MiB).
+// 10 windows, 21.5 GB per device (22 bits: 12 windows, 1.5 GiB; 16 bits:
+// 16 windows, 32 MiB).  Chosen by A/B (profiles/r01_stage_ab_fb_windows26.txt):
+// 22 -> 24 -> 26 bits measured 158.4 -> 160.2 -> 160.9 M tx/s, stage B
+// -13%, for a 0.9 s one-time build per device; MI355X has 288 GB.
 #ifndef CUDASP_FB_BITS
-#define CUDASP_FB_BITS 22
+#define CUDASP_FB_BITS 26
 #endif
 constexpr int FB_BITS = CUDASP_FB_BITS;
-static_assert(FB_BITS >= 8 && FB_BITS <= 24, "fixed-base window width");
+static_assert(FB_BITS >= 8 && FB_BITS <= 27, "fixed-base window width");
 constexpr int FB_WINDOWS = (256 + FB_BITS - 1) / FB_BITS;
 constexpr uint32_t FB_ENTRIES = 1u << (FB_BITS - 1);
 constexpr int FB_WORDS = 16;
