@@ -502,7 +502,15 @@ int ensure_device_table(int device, const uint32_t** out) {
   uint32_t* d_bases = nullptr;
   uint32_t* d_table = nullptr;
   HIP_TRY(hipMalloc(&d_bases, bases.size() * 4));
-  HIP_TRY(hipMalloc(&d_table, (size_t)FB_WINDOWS * FB_ENTRIES * FB_WORDS * 4));
+  const size_t table_bytes = (size_t)FB_WINDOWS * FB_ENTRIES * FB_WORDS * 4;
+  if (hipMalloc(&d_table, table_bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(d_bases);
+    return set_error(CUDASP_ERR_HIP,
+                     "device %d: cannot allocate the %.1f GB fixed-base table (%d-bit windows); free device memory "
+                     "or build with a smaller CUDASP_FB_BITS (22: 1.5 GiB, 16: 32 MiB)",
+                     device, table_bytes / 1e9, FB_BITS);
+  }
   HIP_TRY(hipMemcpy(d_bases, bases.data(), bases.size() * 4, hipMemcpyHostToDevice));
   const uint32_t total = FB_WINDOWS * FB_ENTRIES;
   hipLaunchKernelGGL(k_fb_build, dim3((total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, 0, d_bases, d_table);
