@@ -341,8 +341,6 @@ __global__ __launch_bounds__(BLOCK) void k_layout_probe(const uint32_t* __restri
 // and splitmix64 outputs.  Generation only; never part of a scan.
 struct SynthConsts {
   uint32_t s0[8];  // < n
-  uint32_t c_odd[16];
-  uint32_t c_even[16];
 };
 
 __device__ __forceinline__ void add_index_mod_n(uint32_t s[8], const uint32_t s0[8], uint64_t idx) {
@@ -386,7 +384,7 @@ __global__ __launch_bounds__(BLOCK) void k_synth_tweaks(SynthConsts c, uint64_t 
     uint32_t s[8];
     add_index_mod_n(s, c.s0, first + row);
     gej R;
-    fixed_base_mul(R, s, fb, c.c_odd, c.c_even);
+    fixed_base_mul(R, s, fb);
     fe zi;
     fe_inv(zi, R.z);
     ge A;
@@ -976,9 +974,6 @@ int cudasp_synth_tweak_columns(int device, const uint8_t s0_le[32], uint64_t fir
   for (int i = 0; i < 32; i++) s0.w[i / 4] |= (uint32_t)s0_le[i] << (8 * (i % 4));
   s0 = host::scalar_reduce(s0);
   for (int i = 0; i < 8; i++) c.s0[i] = s0.w[i];
-  const GenPowers& gp = gen_powers();
-  hp_words(c.c_odd, gp.q[FB_WINDOWS]);
-  hp_words(c.c_even, hp_add(gp.q[FB_WINDOWS], hp_neg(gp.q[0])));
   hipLaunchKernelGGL(k_synth_tweaks, dim3(grid_for(n)), dim3(BLOCK), 0, plain_stream(stream), c, first_index, n, fb,
                      d_x, d_y);
   HIP_TRY(hipGetLastError());

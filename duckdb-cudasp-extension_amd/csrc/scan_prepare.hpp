@@ -192,11 +192,6 @@ inline int prepare_scan(const uint8_t scan_private_key[32], const uint8_t spend_
   k.label_count = negate ? 2 * label_count : label_count;
   k.output_count = K;
   k.full_x = opt && opt->full_x ? 1u : 0u;
-  const GenPowers& gp = gen_powers();
-  HPoint co = gp.q[FB_WINDOWS];
-  HPoint ce = hp_add(co, hp_neg(gp.q[0]));
-  hp_words(k.c_odd, co);
-  hp_words(k.c_even, ce);
   hp_words(k.spend, hp_from_bytes(spend_public_key));
   labels.assign(16 * (size_t)(k.label_count ? k.label_count : 1), 0);
   for (uint32_t j = 0; j < label_count; j++) {

@@ -38,8 +38,6 @@ constexpr int FB_WORDS = 16;
 // Per-query constants, passed to the kernels by value.
 struct ScanConsts {
   uint32_t mid[8];      // SHA-256 state after the constant block H(tag)||H(tag)
-  uint32_t c_odd[16];   // 2^(FB_BITS FB_WINDOWS) G      (x[8], y[8], normalized LE words)
-  uint32_t c_even[16];  // 2^(FB_BITS FB_WINDOWS) G - G  (used when the hash t is even)
   uint32_t spend[16];   // B, the spend public key (normalized)
   uint32_t naf_len;     // digits in each GLV half
   uint32_t label_count; // label keys in the label buffer (negated copies included)
@@ -442,24 +440,59 @@ CUDASP_HD void fb_entry(ge& P, const uint32_t* table, int window, uint32_t bits)
   if (neg) ge_neg(P, P);
 }
 
+// secp256k1 group order n, 8 LE words.
+CUDASP_HD uint32_t order_word(int i) {
+  const uint32_t n[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
+                         0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  return n[i];
+}
+
+// The odd representative of a scalar for the odd-digit recoding: t = in mod n
+// (in < 2^256 < 2n: one conditional subtraction; in >= n has probability
+// ~2^-128), then n - t when t is even (n is odd, and (n - t) G = -t G).
+// Returns whether the result stands for -t (the caller negates the point).
+// Branch-free: lanes of a wave differ in parity.
+CUDASP_HD bool scalar_odd_rep(uint32_t t[8], const uint32_t in[8]) {
+  uint32_t d[8];
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t x = (uint64_t)in[i] - order_word(i) - borrow;
+    d[i] = (uint32_t)x;
+    borrow = x >> 63;
+  }
+  const bool ge = borrow == 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = ge ? d[i] : in[i];
+  const bool even = (t[0] & 1u) == 0;
+  borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t x = (uint64_t)order_word(i) - t[i] - borrow;
+    d[i] = (uint32_t)x;
+    borrow = x >> 63;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = even ? d[i] : t[i];
+  return even;
+}
+
 // P = t*G (Jacobian) from the fixed-base table.  t: 8 LE words, any 256-bit
 // value (not reduced mod n, like the reference, src/cudasp_gpu.cu:862-877;
-// n*G = O makes that irrelevant).  c_odd / c_even: 2^(FB_BITS FB_WINDOWS) G
-// and that minus G.
-CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb_table, const uint32_t* c_odd,
-                              const uint32_t* c_even) {
-  // t even -> use t+1 and add -G at the end (odd-digit recoding needs an odd
-  // scalar).
+// n*G = O makes that irrelevant).  FB_WINDOWS gathers and FB_WINDOWS - 1 mixed
+// additions, no constant term.
+CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb_table) {
   uint32_t t[9];
-#pragma unroll
-  for (int i = 0; i < 8; i++) t[i] = t_in[i];
+  const bool negate = scalar_odd_rep(t, t_in);
   t[8] = 0;
-  bool even = (t[0] & 1u) == 0;
-  t[0] |= 1u;
-  // t = sum_{i<W} d_i 2^(w i) + 2^(w W) with odd d_i = 2 b_i + 1 - 2^w,
-  // b_i = bits [w i + 1, w i + w] of t (w = FB_BITS, W = FB_WINDOWS; bits past
-  // 255 are 0).  2^(w W) G (- G) is the constant c_odd / c_even.
-  // The window loop is not unrolled (16 mixed additions would blow the
+  // odd t' < n = 1 + sum_{i<W} 2 b_i 2^(w i), b_i = bits [w i + 1, w i + w] of
+  // t' (w = FB_BITS, W = FB_WINDOWS), written with signed odd digits
+  // d_i = 2 b_i + 1 - 2^w below the top window and the positive top digit
+  // d_(W-1) = 2 b_(W-1) + 1: the (1 - 2^w) 2^(w i) terms telescope to
+  // 1 - 2^(w (W-1)), which the top digit's + 2^(w (W-1)) cancels, so
+  // t' = sum d_i 2^(w i) exactly.  t' < 2^256 keeps b_(W-1) < 2^(w-1), a valid
+  // table index.
+  // The window loop is not unrolled (the mixed additions would blow the
   // instruction cache), so t is consumed by shifting instead of indexing a
   // register array with the loop counter (that would spill to scratch).
 #pragma unroll 1
@@ -469,22 +502,28 @@ CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb
     for (int q = 0; q < 8; q++) t[q] = (t[q] >> FB_BITS) | (t[q + 1] << (32 - FB_BITS));
     t[8] >>= FB_BITS;
     ge P;
-    fb_entry(P, fb_table, i, bits);
+    if (i < FB_WINDOWS - 1)
+      fb_entry(P, fb_table, i, bits);
+    else
+      fb_entry(P, fb_table, i, bits | FB_ENTRIES);  // positive digit 2 bits + 1: entry bits
     if (i == 0) {
       gej_set_ge(R, P);
     } else {
       gej_add_ge(R, R, P);
     }
   }
-  ge C;
-  ge_from_words(C, even ? c_even : c_odd);
-  gej_add_ge(R, R, C);
+  // -P0 for an even t: y negated (a per-lane select; magnitudes differ per
+  // layout, so normalize first)
+  fe ny = R.y;
+  fe_normalize_weak(ny);
+  fe_negate<1>(ny, ny);
+  if (negate) R.y = ny;
 }
 
 // Stage B, first half: F = t G + B as a Jacobian point.
 CUDASP_HD void row_match_point(gej& R, const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k) {
-  fixed_base_mul(R, t_in, fb_table, k.c_odd, k.c_even);  // P0 = t*G
-  // B is added on its own (not folded into c_*), so F = P0 + B is the same
+  fixed_base_mul(R, t_in, fb_table);  // P0 = t*G
+  // B is added on its own (not folded into the table), so F = P0 + B is the same
   // single chord addition as the reference's even for a spend key that is not
   // on the curve.
   ge B;

@@ -77,16 +77,18 @@ struct LazyTable {
     fb_build_entry(&table[idx * FB_WORDS], Q, j);
     filled[idx] = 1;
   }
-  // Same recoding as fixed_base_mul: t made odd, b_i = bits [w i + 1, w i + w].
+  // Same recoding as fixed_base_mul: the odd representative of t mod n,
+  // b_i = bits [w i + 1, w i + w], signed digits below the top window, a
+  // positive top digit.
   void ensure_for(const uint32_t t_in[8]) {
     uint32_t t[9];
-    for (int i = 0; i < 8; i++) t[i] = t_in[i];
+    scalar_odd_rep(t, t_in);
     t[8] = 0;
-    t[0] |= 1u;
     for (int i = 0; i < FB_WINDOWS; i++) {
       uint32_t bits = (t[0] >> 1) & ((FB_ENTRIES << 1) - 1);
       for (int q = 0; q < 8; q++) t[q] = (t[q] >> FB_BITS) | (t[q + 1] << (32 - FB_BITS));
       t[8] >>= FB_BITS;
+      if (i == FB_WINDOWS - 1) bits |= FB_ENTRIES;
       bool neg = (bits & FB_ENTRIES) == 0;
       ensure(i, (bits ^ (neg ? FB_ENTRIES - 1 : 0u)) & (FB_ENTRIES - 1));
     }
@@ -239,6 +241,22 @@ int emu_fb_entry(uint32_t window, uint32_t j, uint32_t out[16]) {
   ge Q;
   ge_from_words(Q, &bases[window * 16]);
   fb_build_entry(out, Q, j);
+  return 0;
+}
+
+// P = t G through fixed_base_mul (the kernels' recoding: odd representative
+// of t mod n, signed digits, positive top digit): affine x, y as 8 LE words.
+int emu_fixed_base_mul(const uint32_t t[8], uint32_t out[16]) {
+  LazyTable& tab = lazy_table();
+  tab.ensure_for(t);
+  gej R;
+  fixed_base_mul(R, t, tab.table);
+  fe zi;
+  fe_inv(zi, R.z);
+  ge A;
+  gej_to_ge_zinv(A, R, zi);
+  fe_to_u32x8(out, A.x);
+  fe_to_u32x8(out + 8, A.y);
   return 0;
 }
 

@@ -206,6 +206,23 @@ def test_fixed_base_entries(emu):
         assert (x, y) == _mul((2 * j + 1) << (bits * w))
 
 
+def test_fixed_base_mul_recoding(emu):
+    """fixed_base_mul's constant-free recoding: t mod n (t >= n is possible,
+    the hash is not reduced), the odd representative n - t for even t (the
+    point negated), signed digits with a positive top digit."""
+    rng = random.Random(17)
+    ts = [1, 2, 3, N - 1, N - 2, N + 1, N + 2, N + 12345, (1 << 256) - 1, (1 << 256) - 2, 1 << 255,
+          (1 << 255) + 1, 2 * N - (1 << 256) + 7]
+    ts += [rng.getrandbits(256) for _ in range(24)]
+    out = (ctypes.c_uint32 * 16)()
+    for t in ts:
+        tw = (ctypes.c_uint32 * 8)(*[(t >> (32 * i)) & 0xFFFFFFFF for i in range(8)])
+        assert emu.emu_fixed_base_mul(tw, out) == 0
+        x = sum(out[i] << (32 * i) for i in range(8))
+        y = sum(out[8 + i] << (32 * i) for i in range(8))
+        assert (x, y) == _mul(t % N), hex(t)
+
+
 def _values(emu, scan, spend, labels, tweaks, outs=None, offs=None, lens=None):
     n = len(tweaks) // 64
     L = len(labels)
