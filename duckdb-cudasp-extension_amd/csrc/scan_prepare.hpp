@@ -95,8 +95,8 @@ HPoint hp_generator() {
   return hp_from_bytes(gbytes);
 }
 
-// 2^(FB_BITS i) G for i = 0..FB_WINDOWS (the last one is the recoding
-// constant 2^(FB_BITS FB_WINDOWS) G), computed once.
+// 2^(FB_BITS i) G for i = 0..FB_WINDOWS (the bases of the fixed-base
+// windows, and one more), computed once.
 struct GenPowers {
   HPoint q[FB_WINDOWS + 1];
   GenPowers() {

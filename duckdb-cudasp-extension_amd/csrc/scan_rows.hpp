@@ -18,11 +18,11 @@ namespace cudasp {
 // Variable-base window: odd multiples 1,3,...,15 of T (width-5 NAF digits).
 constexpr int VB_ENTRIES = 8;
 constexpr int NAF_MAX = 136;
-// Fixed-base table: FB_WINDOWS windows of FB_BITS-bit signed odd digits, each
-// with FB_ENTRIES odd multiples (2j+1) 2^(FB_BITS i) G, 64 bytes per entry.
-// t (256 bits, made odd) = sum_i d_i 2^(FB_BITS i) + 2^(FB_BITS FB_WINDOWS),
-// so P0 = t G costs FB_WINDOWS gathers + mixed additions.  Default 22 bits:
-// 10 windows, 21.5 GB per device (22 bits: 12 windows, 1.5 GiB; 16 bits:
+// Fixed-base table: FB_WINDOWS windows of FB_BITS-bit odd digits, each with
+// FB_ENTRIES odd multiples (2j+1) 2^(FB_BITS i) G, 64 bytes per entry.  The odd
+// representative t' of t mod n is sum_i d_i 2^(FB_BITS i) (fixed_base_mul), so
+// P0 = t G costs FB_WINDOWS gathers and FB_WINDOWS - 1 mixed additions.
+// Default 26 bits: 10 windows, 21.5 GB per device (22 bits: 12 windows, 1.5 GiB; 16 bits:
 // 16 windows, 32 MiB).  Chosen by A/B (profiles/r01_stage_ab_fb_windows26.txt):
 // 22 -> 24 -> 26 bits measured 158.4 -> 160.2 -> 160.9 M tx/s, stage B
 // -13%, for a 0.9 s one-time build per device; MI355X has 288 GB.

@@ -58,7 +58,7 @@ void words_from_row(uint32_t x[8], uint32_t y[8], const uint8_t* row) {
 
 // Lazily filled copy of the device fixed-base table.  The arrays come from
 // calloc, so only the pages of entries actually built are ever touched (the
-// full table is 1.5 GiB at the default 22-bit windows).
+// full table is 21.5 GB at the default 26-bit windows).
 struct LazyTable {
   uint32_t* table;
   uint8_t* filled;
