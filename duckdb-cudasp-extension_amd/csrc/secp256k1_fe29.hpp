@@ -124,6 +124,13 @@ CUDASP_HD void fe_add(fe& r, const fe& a, const fe& b) {
   FE_CHECK_SUM(r, "add");
 }
 
+// r = 2 (a + b): one v_add_lshl_u32 per limb.
+CUDASP_HD void fe_add_x2(fe& r, const fe& a, const fe& b) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.n[i] = (a.n[i] + b.n[i]) << 1;
+  FE_CHECK_SUM(r, "add_x2");
+}
+
 CUDASP_HD void fe_add_to(fe& r, const fe& a) {
 #pragma unroll
   for (int i = 0; i < 9; i++) r.n[i] += a.n[i];

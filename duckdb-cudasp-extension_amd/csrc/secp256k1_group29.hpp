@@ -82,7 +82,7 @@ CUDASP_HD void gej_add_ge(gej& r, const gej& a, const ge& b, fe* zr = nullptr) {
 // Z3 = Yh Z (= 2 Y Z), A = Yh^2 (= 4 Y^2), B = X A (= 4 X Y^2), M = 3 X^2,
 // X3 = M^2 - 2 B, Yh3 = 2 M (X3 - B) + A^2 (= -2 Y3).  r may alias a.
 CUDASP_HD void gej_double_neg_yh(gej& r, const gej& a) {
-  fe A, M, B, w;
+  fe A, M, B, nb, w;
   FE_CHECK(a.x, 1, "dblh x");
   FE_CHECK(a.y, 2, "dblh y");
   FE_CHECK(a.z, 2, "dblh z");
@@ -90,12 +90,11 @@ CUDASP_HD void gej_double_neg_yh(gej& r, const gej& a) {
   fe_sqr(A, a.y);           // A = Yh^2                           (1)
   fe_sqr3(M, a.x);          // M = 3 X^2                          (1)
   fe_mul(B, a.x, A);        // B = X A                            (1)
-  fe_negate<1>(w, B);
-  fe_add(w, w, w);          // -2B                                (4)
+  fe_negate<1>(nb, B);      // -B                                 (2)
+  fe_add(w, nb, nb);        // -2B                                (4)
   fe_sqr_add(r.x, M, w);    // X3 = M^2 - 2B                      (1)
-  fe_sub<1>(w, r.x, B);     // X3 - B                             (3)
-  fe_add(M, M, M);          // 2M                                 (2)
-  fe_mulsqr(r.y, M, w, A);  // Yh3' = 2M (X3 - B) + A^2           2 * 3 + 1 -> (1)
+  fe_add_x2(w, r.x, nb);    // 2 (X3 - B)                         (6)
+  fe_mulsqr(r.y, M, w, A);  // Yh3' = M 2 (X3 - B) + A^2          1 * 6 + 1 -> (1)
 }
 
 // r = a + b (Yh form, b affine with yh = 2y, possibly negated).  Input:
