@@ -257,10 +257,24 @@ CUDASP_HD void fe_half(fe& r, const fe& a) {
 #pragma unroll
   for (int i = 2; i < 8; i++) t[i] = a.n[i] + (M29 & odd);
   t[8] = a.n[8] + (M24 & odd);
-  // (t_i + (t_(i+1) mod 2) 2^29) / 2: and, shift-add, shift per limb
-  // (t_i <= 2^30 + 2^15, so the sum stays below 2^32).
+  // (t_i + (t_(i+1) mod 2) 2^29) / 2 = (t_i >> 1) + (t_(i+1) mod 2) 2^28 (2^29 is
+  // even): and, shift, shift-add (v_lshl_add_u32) per limb.
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.n[i] = (t[i] + ((t[i + 1] & 1u) << 29)) >> 1;
+  for (int i = 0; i < 8; i++) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // 3 instructions (the compiler turns (x & 1) << 28 into a shift and a
+    // mask and does not form the shift-add: 4)
+    uint32_t b, h;
+    asm("v_and_b32 %0, 1, %2\n"
+        "v_lshrrev_b32 %1, 1, %3\n"
+        "v_lshl_add_u32 %1, %0, 28, %1"
+        : "=&v"(b), "=&v"(h)
+        : "v"(t[i + 1]), "v"(t[i]));
+    r.n[i] = h;
+#else
+    r.n[i] = (t[i] >> 1) + ((t[i + 1] & 1u) << 28);
+#endif
+  }
   r.n[8] = t[8] >> 1;
 }
 
