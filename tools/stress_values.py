@@ -42,7 +42,7 @@ def main():
     ty = torch.empty((8, n), dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream()
     _native.check(lib.cudasp_synth_tweak_columns(0, bench.synth_s0(), 12345, n, tx.data_ptr(), ty.data_ptr(),
-                                                 ctypes_stream(st)))
+                                                 _native.stream_arg(st)))
     torch.cuda.synchronize()
     big = Scanner(bench.SCAN_KEY, bench.SPEND_KEY, [], max_rows=n, device=0)
     t_ref = torch.empty((8, n), dtype=torch.int32, device=dev)
@@ -78,11 +78,6 @@ def main():
                                   bad_v_by_j=bad_v)), flush=True)
     small.close()
     big.close()
-
-
-def ctypes_stream(st):
-    import ctypes
-    return _native.stream_arg(st)
 
 
 if __name__ == "__main__":
