@@ -455,6 +455,8 @@ __global__ __launch_bounds__(BLOCK) void k_debug_field_ops(int op, const uint32_
     fe_mul(r, x, y);
   } else if (op == 1) {
     fe_sqr(r, x);
+  } else if (op == 7) {
+    fe_inv(r, x);
   } else {
 #if CUDASP_FE_LIMBS == 9
     fe c, e;
@@ -1023,8 +1025,9 @@ int cudasp_field_layout(int* limbs, int* bits, int* mul_mag_max, int* sqr_mag_ma
 
 int cudasp_debug_field_ops(int op, const uint32_t* d_a, const uint32_t* d_b, uint32_t* d_out, uint32_t n) {
   if (n == 0) return CUDASP_OK;
-  if (op < 0 || op > (CUDASP_FE_LIMBS == 9 ? 6 : 1))
-    return set_error(CUDASP_ERR_INVALID_ARG, "op must be 0 (mul) or 1 (sqr), or 2..6 (fused, 9 x 29 layout)");
+  if (op < 0 || op > 7 || (op >= 2 && op <= 6 && CUDASP_FE_LIMBS != 9))
+    return set_error(CUDASP_ERR_INVALID_ARG,
+                     "op must be 0 (mul), 1 (sqr), 7 (inverse), or 2..6 (fused, 9 x 29 layout)");
   if (!d_a || !d_b || !d_out) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   hipLaunchKernelGGL(k_debug_field_ops, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, 0, op, d_a, d_b, d_out, n);
   HIP_TRY(hipGetLastError());

@@ -8,10 +8,11 @@
 // round runs 30 divsteps on the low 30 bits of f and g to get the transition
 // matrix T (entries bounded by 2^30), then [f g] <- T [f g] / 2^30 exactly and
 // [d e] <- T [d e] / 2^30 mod p.  At the end g = 0, f = +-1, 1/x = d f.
-// The half-delta divstep is tracked as h = 2*delta (odd, starts at 1):
-//   h > 0 and g odd:  h <- 2 - h,  (f, g) <- (g, (g - f)/2)
-//   g odd:            h <- h + 2,  g <- (g + f)/2
-//   otherwise:        h <- h + 2,  g <- g/2
+// The half-delta divstep is tracked as zeta = -(delta + 1/2) (starts at -1,
+// delta > 0 iff zeta < 0):
+//   delta > 0 and g odd:  zeta <- -zeta - 2,  (f, g) <- (g, (g - f)/2)
+//   g odd:                zeta <- zeta - 1,   g <- (g + f)/2
+//   otherwise:            zeta <- zeta - 1,   g <- g/2
 #pragma once
 #include "secp256k1_fe.hpp"
 
@@ -28,46 +29,103 @@ constexpr int32_t P30_1 = -4;
 constexpr int32_t P30_8 = 65536;
 constexpr uint32_t P_INV30 = 0x2DDACACFu;  // p^-1 mod 2^30
 
-// 30 divsteps on the low bits; returns the new h and the matrix (scaled by 2^30).
-CUDASP_HD int32_t divsteps_30(int32_t h, uint32_t f, uint32_t g, int32_t& tu, int32_t& tv, int32_t& tq,
+// a + b + c as one v_add3_u32.  In plain C the compiler rewrites
+// x + (m & 1) for a 0 / -1 mask m into x - m and then needs a separate sub.
+CUDASP_HD uint32_t add3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return a + b + c;
+#endif
+}
+
+// 30 divsteps on the low bits; returns the new zeta and the matrix (scaled by
+// 2^30).  Per step: g += odd ? (swap ? -f : f) : 0 is written as
+// g + ((f ^ swap) & odd) + (swap & 1) -- one 3-input bit operation and one
+// 3-input add on gfx950 (v_bitop3_b32, v_add3_u32) instead of xor, sub, and,
+// add -- and the zeta update (zeta ^ swap) - 1 is one v_xad_u32.
+CUDASP_HD int32_t divsteps_30(int32_t zeta, uint32_t f, uint32_t g, int32_t& tu, int32_t& tv, int32_t& tq,
                               int32_t& tr) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t z = (uint32_t)zeta;
 #pragma unroll
   for (int i = 0; i < 30; i++) {
-    uint32_t m_odd = 0u - (g & 1u);
-    uint32_t m_pos = (uint32_t)((0 - h) >> 31);  // all ones iff h > 0
-    uint32_t m_swap = m_odd & m_pos;
-    uint32_t x = (f ^ m_swap) - m_swap;  // swap ? -f : f
-    uint32_t y = (u ^ m_swap) - m_swap;
-    uint32_t z = (v ^ m_swap) - m_swap;
-    g += x & m_odd;
-    q += y & m_odd;
-    r += z & m_odd;
+    const uint32_t m_pos = (uint32_t)((int32_t)z >> 31);  // all ones iff delta > 0
+    const uint32_t m_odd = 0u - (g & 1u);
+    const uint32_t m_swap = m_odd & m_pos;
+    const uint32_t n_swap = m_swap & 1u;  // -m_swap
+    g = add3(g, (f ^ m_swap) & m_odd, n_swap);
+    q = add3(q, (u ^ m_swap) & m_odd, n_swap);
+    r = add3(r, (v ^ m_swap) & m_odd, n_swap);
+    z = (z ^ m_swap) - 1u;
     f += g & m_swap;  // swap: f <- old g (= new g + f)
-    u += q & m_swap;
-    v += r & m_swap;
+    u = (u + (q & m_swap)) << 1;
+    v = (v + (r & m_swap)) << 1;
     g >>= 1;
-    u <<= 1;
-    v <<= 1;
-    h = (int32_t)(((uint32_t)h ^ m_swap) - m_swap) + 2;
   }
   tu = (int32_t)u;
   tv = (int32_t)v;
   tq = (int32_t)q;
   tr = (int32_t)r;
-  return h;
+  return (int32_t)z;
+}
+
+// c + a * b (signed 32 x 32 -> 64) as one v_mad_i64_i32.  Compiled C builds
+// these sums from unsigned 64-bit multiplies with sign corrections (about 3x
+// the instructions).
+CUDASP_HD int64_t mad_i64(int32_t a, int32_t b, int64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  int64_t r;
+  uint64_t carry;  // unused carry-out; its own SGPR pair, no vcc hazards
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return c + (int64_t)a * b;
+#endif
+}
+
+// cf += u a + v b and cg += q a + r b: the four mads of one limb of a matrix
+// update in one asm block (separate asm statements each get an s_nop).
+CUDASP_HD void mad_2x2(int64_t& cf, int64_t& cg, int32_t u, int32_t v, int32_t q, int32_t r, int32_t a, int32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t carry;
+  asm("v_mad_i64_i32 %0, %2, %3, %7, %0\n\t"
+      "v_mad_i64_i32 %1, %2, %5, %7, %1\n\t"
+      "v_mad_i64_i32 %0, %2, %4, %8, %0\n\t"
+      "v_mad_i64_i32 %1, %2, %6, %8, %1"
+      : "+v"(cf), "+v"(cg), "=s"(carry)
+      : "v"(u), "v"(v), "v"(q), "v"(r), "v"(a), "v"(b));
+#else
+  cf += (int64_t)u * a + (int64_t)v * b;
+  cg += (int64_t)q * a + (int64_t)r * b;
+#endif
+}
+
+// cd += P md and ce += P me (P a constant limb of p) in one asm block.
+CUDASP_HD void mad_p2(int64_t& cd, int64_t& ce, int32_t P, int32_t md, int32_t me) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t carry;
+  asm("v_mad_i64_i32 %0, %2, %3, %4, %0\n\t"
+      "v_mad_i64_i32 %1, %2, %3, %5, %1"
+      : "+v"(cd), "+v"(ce), "=s"(carry)
+      : "v"(P), "v"(md), "v"(me));
+#else
+  cd += (int64_t)P * md;
+  ce += (int64_t)P * me;
+#endif
 }
 
 // [f g] <- T [f g] / 2^30 (exact).
 CUDASP_HD void s30_update_fg(s30& f, s30& g, int32_t u, int32_t v, int32_t q, int32_t r) {
-  int64_t cf = (int64_t)u * f.v[0] + (int64_t)v * g.v[0];
-  int64_t cg = (int64_t)q * f.v[0] + (int64_t)r * g.v[0];
+  int64_t cf = 0, cg = 0;
+  mad_2x2(cf, cg, u, v, q, r, f.v[0], g.v[0]);
   cf >>= 30;
   cg >>= 30;
 #pragma unroll
   for (int i = 1; i < 9; i++) {
-    cf += (int64_t)u * f.v[i] + (int64_t)v * g.v[i];
-    cg += (int64_t)q * f.v[i] + (int64_t)r * g.v[i];
+    mad_2x2(cf, cg, u, v, q, r, f.v[i], g.v[i]);
     f.v[i - 1] = (int32_t)cf & S30_MASK;
     g.v[i - 1] = (int32_t)cg & S30_MASK;
     cf >>= 30;
@@ -83,33 +141,31 @@ CUDASP_HD void s30_update_de(s30& d, s30& e, int32_t u, int32_t v, int32_t q, in
   // Work with d + p (if d < 0) and e + p (if e < 0) so the result stays in range.
   int32_t md = (u & sd) + (v & se);
   int32_t me = (q & sd) + (r & se);
-  int64_t cd = (int64_t)u * d.v[0] + (int64_t)v * e.v[0];
-  int64_t ce = (int64_t)q * d.v[0] + (int64_t)r * e.v[0];
+  int64_t cd = 0, ce = 0;
+  mad_2x2(cd, ce, u, v, q, r, d.v[0], e.v[0]);
   // Pick md, me so that the low 30 bits cancel.
   md -= (int32_t)((P_INV30 * (uint32_t)cd + (uint32_t)md) & (uint32_t)S30_MASK);
   me -= (int32_t)((P_INV30 * (uint32_t)ce + (uint32_t)me) & (uint32_t)S30_MASK);
-  cd += (int64_t)P30_0 * md;
-  ce += (int64_t)P30_0 * me;
+  mad_p2(cd, ce, P30_0, md, me);
   cd >>= 30;
   ce >>= 30;
   // limb 1 (p has -4 there)
-  cd += (int64_t)u * d.v[1] + (int64_t)v * e.v[1] + (int64_t)P30_1 * md;
-  ce += (int64_t)q * d.v[1] + (int64_t)r * e.v[1] + (int64_t)P30_1 * me;
+  mad_2x2(cd, ce, u, v, q, r, d.v[1], e.v[1]);
+  mad_p2(cd, ce, P30_1, md, me);
   d.v[0] = (int32_t)cd & S30_MASK;
   e.v[0] = (int32_t)ce & S30_MASK;
   cd >>= 30;
   ce >>= 30;
 #pragma unroll
   for (int i = 2; i < 8; i++) {
-    cd += (int64_t)u * d.v[i] + (int64_t)v * e.v[i];
-    ce += (int64_t)q * d.v[i] + (int64_t)r * e.v[i];
+    mad_2x2(cd, ce, u, v, q, r, d.v[i], e.v[i]);
     d.v[i - 1] = (int32_t)cd & S30_MASK;
     e.v[i - 1] = (int32_t)ce & S30_MASK;
     cd >>= 30;
     ce >>= 30;
   }
-  cd += (int64_t)u * d.v[8] + (int64_t)v * e.v[8] + (int64_t)P30_8 * md;
-  ce += (int64_t)q * d.v[8] + (int64_t)r * e.v[8] + (int64_t)P30_8 * me;
+  mad_2x2(cd, ce, u, v, q, r, d.v[8], e.v[8]);
+  mad_p2(cd, ce, P30_8, md, me);
   d.v[7] = (int32_t)cd & S30_MASK;
   e.v[7] = (int32_t)ce & S30_MASK;
   cd >>= 30;
@@ -151,11 +207,11 @@ CUDASP_HD void fe_inv_safegcd(fe& r, const fe& a_in) {
     e.v[i] = 0;
   }
   e.v[0] = 1;
-  int32_t h = 1;
+  int32_t zeta = -1;  // delta = 1/2
 #pragma unroll 1
   for (int it = 0; it < 20; it++) {
     int32_t u, v, q, rr;
-    h = divsteps_30(h, (uint32_t)f.v[0], (uint32_t)g.v[0], u, v, q, rr);
+    zeta = divsteps_30(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], u, v, q, rr);
     s30_update_de(d, e, u, v, q, rr);
     s30_update_fg(f, g, u, v, q, rr);
   }

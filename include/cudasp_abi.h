@@ -182,8 +182,9 @@ int cudasp_synth_output_values(uint64_t seed, uint64_t first_index, uint32_t n, 
  * (op 1) mod p, operands `limbs` u32 limbs each (row-major, any magnitude the
  * kernels accept); the result has magnitude 1, not fully reduced.  The 9 x 29
  * layout adds its fused forms, reading d_b as three n-element arrays b, c, e:
- * op 2 a*b + c*e, op 3 a*b + c^2, op 4 a*b + c, op 5 a^2 + c, op 6 3*a^2.  Device
- * buffers; synchronous. */
+ * op 2 a*b + c*e, op 3 a*b + c^2, op 4 a*b + c, op 5 a^2 + c, op 6 3*a^2.
+ * op 7: out[i] = a[i]^-1 mod p, fully reduced (0 for a[i] = 0 mod p; d_b is
+ * not read).  Device buffers; synchronous. */
 int cudasp_field_layout(int* limbs, int* bits, int* mul_mag_max, int* sqr_mag_max, int* limb_mag_max);
 int cudasp_debug_field_ops(int op, const uint32_t* d_a, const uint32_t* d_b, uint32_t* d_out, uint32_t n);
 

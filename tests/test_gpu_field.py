@@ -152,3 +152,30 @@ def test_fused_magnitudes(torch, layout):
         for i in range(a.shape[0]):
             want = f(value(layout, a[i]), value(layout, b[i]), value(layout, c[i]), value(layout, e[i])) % P
             assert value(layout, r[i]) % P == want, (op, ma, mb, mc, me, i)
+
+
+def test_inverse(torch, layout):
+    """fe_inv (safegcd divsteps; on gfx950 partly asm) against pow(a, -1, p):
+    random values of every magnitude the kernels pass in, 0, 1, p - 1, p,
+    small and 2^k values, and values congruent to them."""
+    rng = np.random.default_rng(4242)
+    lay = layout
+    vals = [0, 1, 2, 3, P - 1, P - 2, P, P + 1, 2 * P - 1, 2**255, 2**256 - 1, (P + 1) // 2, 977, 2**32 + 977]
+    vals += [2**k for k in range(0, 256, 17)]
+    rows = []
+    for v in vals:
+        limbs, x = [], v
+        for k in range(lay["limbs"]):
+            w = lay["bits"] if k < lay["limbs"] - 1 else 32
+            limbs.append(x & ((1 << w) - 1))
+            x >>= w
+        assert x == 0
+        rows.append(limbs)
+    a = np.concatenate([np.array(rows, dtype=np.uint64).astype(np.uint32),
+                        operands(lay, rng, 1, 4000), operands(lay, rng, 2, 4000)])
+    r = run(torch, 7, a, np.zeros_like(a))
+    for i in range(a.shape[0]):
+        x = value(lay, a[i]) % P
+        got = value(lay, r[i])
+        assert got < P, i
+        assert got == (pow(x, -1, P) if x else 0), (i, hex(x))
