@@ -15,6 +15,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -76,7 +77,8 @@ static_assert(ROWS_A >= 1 && ROWS_A <= 8 && ROWS_B >= 1 && ROWS_B <= 8, "rows pe
 // Scratch words per slot: stage A's odd-multiple table + its pending rows;
 // stage B's label prefix products (FW L per row of the thread: one batched
 // inversion for all its rows' labels) + its pending rows.
-constexpr uint32_t VSCRATCH_WORDS = VB_SCRATCH_WORDS + PEND_WORDS * ROWS_A;
+constexpr uint32_t vscratch_words(int rows) { return VB_SCRATCH_WORDS + PEND_WORDS * (uint32_t)rows; }
+constexpr uint32_t VSCRATCH_WORDS = vscratch_words(ROWS_A);
 inline uint32_t lscratch_words(uint32_t label_count) { return (FW * label_count + PEND_WORDS) * ROWS_B; }
 }  // namespace
 
@@ -96,8 +98,11 @@ __device__ __forceinline__ void store_t(uint32_t* __restrict__ t_out, uint32_t n
   }
 }
 
-// Stage A: thread `slot` takes the rows g, g + G, ... (G = ceil(n / ROWS_A)) of
-// each of its groups g, so every row access stays coalesced.
+// Stage A: thread `slot` takes the rows g, g + G, ... (G = ceil(n / R)) of
+// each of its groups g, so every row access stays coalesced.  R = ROWS_A rows
+// per thread share one inversion; launches too small to fill the GPU use 2 or
+// 1 (rows_a_for), which shortens the launch (its rows run in sequence).
+template <int R>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const uint32_t* __restrict__ tx,
                                                          const uint32_t* __restrict__ ty, uint32_t n,
                                                          const int8_t* __restrict__ naf, ScanConsts k,
@@ -106,7 +111,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
   const Scratch sc = make_scratch(vscr, stride, slot);
-  if constexpr (ROWS_A == 1) {
+  if constexpr (R == 1) {
     for (uint32_t row = slot; row < n; row += stride) {
       uint32_t x[8], y[8];
 #pragma unroll
@@ -114,22 +119,22 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
         x[w] = tx[(size_t)w * n + row];
         y[w] = ty[(size_t)w * n + row];
       }
-      gej R;
-      row_shared_secret_point(R, x, y, naf, k.naf_len, sc);
+      gej P;
+      row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
       fe zi;
-      fe_inv(zi, R.z);
+      fe_inv(zi, P.z);
       uint32_t sx[8];
-      const uint32_t y_odd = row_shared_secret_affine(sx, R, zi);
+      const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
       store_t(t_out, n, k.output_count, row, sx, y_odd, k.mid);
     }
     return;
   }
-  const uint32_t G = (n + ROWS_A - 1) / ROWS_A;
+  const uint32_t G = (n + R - 1) / R;
   constexpr int PB = VB_SCRATCH_WORDS;
   for (uint32_t g = slot; g < G; g += stride) {
     int count = 0;
 #pragma unroll 1
-    for (int j = 0; j < ROWS_A; j++) {
+    for (int j = 0; j < R; j++) {
       const uint32_t row = g + (uint32_t)j * G;
       if (row >= n) break;
       uint32_t x[8], y[8];
@@ -138,21 +143,21 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
         x[w] = tx[(size_t)w * n + row];
         y[w] = ty[(size_t)w * n + row];
       }
-      gej R;
-      row_shared_secret_point(R, x, y, naf, k.naf_len, sc);
-      pend_store(sc, PB, j, R);
+      gej P;
+      row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
+      pend_store(sc, PB, j, P);
       count = j + 1;
     }
-    pend_invert<ROWS_A>(sc, PB, count);
+    pend_invert<R>(sc, PB, count);
 #pragma unroll 1
     for (int j = 0; j < count; j++) {
       const uint32_t row = g + (uint32_t)j * G;
-      gej R;
+      gej P;
       fe zi;
-      pend_load(R, sc, PB, j);
+      pend_load(P, sc, PB, j);
       scr_load(zi, sc, PEND_ZI(PB, j));
       uint32_t sx[8];
-      const uint32_t y_odd = row_shared_secret_affine(sx, R, zi);
+      const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
       store_t(t_out, n, k.output_count, row, sx, y_odd, k.mid);
     }
   }
@@ -544,6 +549,8 @@ struct cudasp_scanner {
   uint32_t* d_vscratch = nullptr;  // VSCRATCH_WORDS x slots_a
   uint32_t* d_lscratch = nullptr;  // lscratch_words(L) x slots_b
   uint32_t slots_a = 0, slots_b = 0;
+  uint32_t fill_threads = 0;  // stage-A threads per launch that fill the device (rows_a_for)
+  int rows_a_force = 0;       // CUDASP_ROWS_A_FORCE (tests): fixed rows per stage-A thread
   // host-path staging
   uint8_t* d_rows = nullptr;   // capacity x 64
   uint32_t* d_tx = nullptr;    // 8 x capacity
@@ -566,9 +573,38 @@ uint32_t grid_for(uint32_t n) {
 
 // Blocks for a batch of n rows in stage A / B (one thread per group of
 // ROWS_A / ROWS_B rows), within the scratch slots the scanner allocated.
-uint32_t grid_a(const cudasp_scanner* s, uint32_t n) {
-  uint32_t b = grid_for((n + ROWS_A - 1) / ROWS_A);
-  return b * BLOCK > s->slots_a ? s->slots_a / BLOCK : b;
+uint32_t grid_a(const cudasp_scanner* s, uint32_t n, int rows = ROWS_A) {
+  uint32_t b = grid_for((n + rows - 1) / rows);
+  // the scratch holds slots_a slots of VSCRATCH_WORDS; fewer rows per thread
+  // take fewer words per slot
+  const uint64_t cap = (uint64_t)s->slots_a * VSCRATCH_WORDS / ((uint64_t)vscratch_words(rows) * BLOCK);
+  return b > cap ? (uint32_t)(cap ? cap : 1) : b;
+}
+
+// Rows per stage-A thread for a launch of n rows.  ROWS_A rows share one
+// inversion, but a thread scans them in sequence, so a launch lasts at least
+// ROWS_A row-times however few rows it has.  The HIP runtime runs a process's
+// launches on 4 hardware queues (GPU_MAX_HW_QUEUES), so a launch with fewer
+// threads than a quarter of the device's wave slots leaves the GPU part idle:
+// such launches take 2 or 1 rows per thread instead.
+int rows_a_for(const cudasp_scanner* s, uint32_t n) {
+  if (s->rows_a_force) return s->rows_a_force;
+  int r = ROWS_A;
+  while (r > 1 && (n + r - 1) / (uint32_t)r < s->fill_threads) r = r > 2 ? 2 : 1;
+  return r;
+}
+
+void launch_a(const cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, uint32_t n, uint32_t* t,
+              hipStream_t st) {
+  const int r = rows_a_for(s, n);
+  const dim3 grid(grid_a(s, n, r)), block(BLOCK);
+  if (r == 1)
+    hipLaunchKernelGGL(k_shared_secret<1>, grid, block, 0, st, tx, ty, n, s->d_naf, s->consts, s->d_vscratch, t);
+  else if (r == 2)
+    hipLaunchKernelGGL(k_shared_secret<2>, grid, block, 0, st, tx, ty, n, s->d_naf, s->consts, s->d_vscratch, t);
+  else
+    hipLaunchKernelGGL(k_shared_secret<ROWS_A>, grid, block, 0, st, tx, ty, n, s->d_naf, s->consts,
+                       s->d_vscratch, t);
 }
 uint32_t grid_b(const cudasp_scanner* s, uint32_t n) {
   uint32_t b = grid_for((n + ROWS_B - 1) / ROWS_B);
@@ -640,8 +676,7 @@ int launch_pipeline(cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, c
   if (n == 0) return CUDASP_OK;
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
   uint32_t* t = t_out ? t_out : s->d_t;
-  hipLaunchKernelGGL(k_shared_secret, dim3(grid_a(s, n)), dim3(BLOCK), 0, st, tx, ty, n, s->d_naf, s->consts,
-                     s->d_vscratch, t);
+  launch_a(s, tx, ty, n, t, st);
   HIP_TRY(hipGetLastError());
   return launch_match(s, t, n, outputs, offs, lens, flags, match_rows, match_count, values, st);
 }
@@ -713,6 +748,17 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
   };
   s->slots_a = slots_for((max_rows + ROWS_A - 1) / ROWS_A, VSCRATCH_WORDS);
   s->slots_b = slots_for((max_rows + ROWS_B - 1) / ROWS_B, lscratch_words(label_count));
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+      cus = 256;
+    // a quarter of the wave slots (4 SIMDs per CU, CUDASP_WAVES_A waves each)
+    s->fill_threads = (uint32_t)cus * 4 * CUDASP_WAVES_A * 64 / 4;
+    if (const char* f = getenv("CUDASP_ROWS_A_FORCE")) {
+      const int r = atoi(f);
+      if (r == 1 || r == 2 || r == ROWS_A) s->rows_a_force = r;
+    }
+  }
   if ((uint64_t)lscratch_words(label_count) * 4 * BLOCK > (1ull << 32) - 1) {
     delete s;
     return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys (%u)", label_count);
@@ -942,8 +988,7 @@ int cudasp_stage_shared_secret_device(cudasp_scanner* s, const uint32_t* d_tweak
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
   DeviceGuard g(s->device);
   hipStream_t st = scanner_stream(s, stream);
-  hipLaunchKernelGGL(k_shared_secret, dim3(grid_a(s, n)), dim3(BLOCK), 0, st, d_tweak_x, d_tweak_y, n, s->d_naf,
-                     s->consts, s->d_vscratch, d_t);
+  launch_a(s, d_tweak_x, d_tweak_y, n, d_t, st);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
 }

@@ -77,6 +77,47 @@ def test_values_match_oracle_with_labels(torch):
     assert (v.cpu().numpy().T == ov).all()
 
 
+@pytest.mark.parametrize("rows_a", ["1", "2", "4", None])
+def test_rows_per_thread_variants(torch, monkeypatch, rows_a):
+    """Stage A at 1, 2 or 4 rows per thread (4 by default; launches too small
+    to fill the GPU take 2 or 1, rows_a_for in scan_kernels.hip; forced here
+    with CUDASP_ROWS_A_FORCE): 3001 synthetic rows (not a multiple of 2 or 4)
+    with a label, values equal to the oracle's."""
+    from cudasp_amd import Scanner
+    from oracle import oracle
+    if rows_a:
+        monkeypatch.setenv("CUDASP_ROWS_A_FORCE", rows_a)
+    else:
+        monkeypatch.delenv("CUDASP_ROWS_A_FORCE", raising=False)
+    n = 3001
+    x, y, _, _, _ = synth(torch, 555, n)
+    with Scanner(SCAN, SPEND, [LABEL], max_rows=n) as s:
+        t = torch.empty((8, n), dtype=torch.int32, device="cuda")
+        v = torch.empty((2, n), dtype=torch.int64, device="cuda")
+        s.row_values_device(x, y, t, v)
+        s.sync()
+    _, ov = oracle.scan(SCAN, SPEND, [LABEL], rows_of(x, y), threads=16, want_values=True)
+    assert (v.cpu().numpy().T == ov).all()
+
+
+def test_rows_per_thread_large_launch(torch, monkeypatch):
+    """200k rows at 1, 2 and 4 rows per thread give identical t: the 1- and
+    2-row launches need more scratch slots than the scanner holds, so their
+    grids are capped and the grid-stride loop takes the remaining rows."""
+    from cudasp_amd import Scanner
+    n = 200000
+    x, y, _, _, _ = synth(torch, 31337, n)
+    ts = []
+    for r in ("4", "2", "1"):
+        monkeypatch.setenv("CUDASP_ROWS_A_FORCE", r)
+        with Scanner(SCAN, SPEND, [], max_rows=n) as s:
+            t = torch.zeros((8, n), dtype=torch.int32, device="cuda")
+            s.stage_shared_secret(x, y, n, t_out=t)
+            s.sync()
+        ts.append(t.cpu())
+    assert torch.equal(ts[0], ts[1]) and torch.equal(ts[0], ts[2])
+
+
 def _plant(torch, x, y, outs, labels, every=1000):
     from cudasp_amd import Scanner
     n = x.shape[1]
