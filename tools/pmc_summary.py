@@ -20,8 +20,20 @@ import argparse
 import collections
 import csv
 import json
+import re
 
 SCAN_KERNELS = ("k_shared_secret", "void k_match<false>", "void k_match<true>", "k_layout_probe")
+
+
+def kernel_key(name):
+    """Kernel name without arguments; stage A's full-batch instance (4 rows
+    per thread, CUDASP_ROWS_A) keeps the plain name bench.py looks up, the
+    small-launch instances (rows_a_for) stay separate."""
+    k = name.split("(")[0]
+    m = re.fullmatch(r"void k_shared_secret<(\d+)>", k)
+    if m:
+        k = "k_shared_secret" if m.group(1) == "4" else "k_shared_secret<%s>" % m.group(1)
+    return k
 
 
 def load(paths):
@@ -29,7 +41,7 @@ def load(paths):
     per = collections.defaultdict(lambda: collections.defaultdict(dict))
     for p in paths:
         for r in csv.DictReader(open(p)):
-            k = r["Kernel_Name"].split("(")[0]
+            k = kernel_key(r["Kernel_Name"])
             key = (p, r["Dispatch_Id"])
             grid = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
             c = r["Counter_Name"]
