@@ -79,7 +79,9 @@ static_assert(ROWS_A >= 1 && ROWS_A <= 8 && ROWS_B >= 1 && ROWS_B <= 8, "rows pe
 // inversion for all its rows' labels) + its pending rows.
 constexpr uint32_t vscratch_words(int rows) { return VB_SCRATCH_WORDS + PEND_WORDS * (uint32_t)rows; }
 constexpr uint32_t VSCRATCH_WORDS = vscratch_words(ROWS_A);
-inline uint32_t lscratch_words(uint32_t label_count) { return (FW * label_count + PEND_WORDS) * ROWS_B; }
+inline uint32_t lscratch_words(uint32_t label_count, int rows = ROWS_B) {
+  return (FW * label_count + PEND_WORDS) * (uint32_t)rows;
+}
 }  // namespace
 
 // ----------------------------------------------------------------- kernels
@@ -163,12 +165,13 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
   }
 }
 
-// Stage B: rows g, g + G, ... (G = ceil(n / ROWS_B)) per thread as in stage A;
-// the block walks its groups together so that the compaction ballots see
+// Stage B: rows g, g + G, ... (G = ceil(n / R)) per thread as in stage A
+// (R = ROWS_B, or 2 for launches too small to fill the GPU: rows_b_for); the
+// block walks its groups together so that the compaction ballots see
 // consecutive rows of full waves.  n counts virtual rows kk * n_rows + row
 // (K output indices per input row; n == n_rows when K = 1): t, flags and
 // values are indexed by the virtual row, the outputs lists by the input row.
-template <bool VALUES>
+template <bool VALUES, int R>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t* __restrict__ t_in, uint32_t n,
                                                  uint32_t n_rows,
                                                  const uint32_t* __restrict__ fb, ScanConsts k,
@@ -183,49 +186,49 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
   const Scratch sc = make_scratch(lscr, stride, slot);
-  const uint32_t G = (n + ROWS_B - 1) / ROWS_B;
-  const int PB = FW * (int)k.label_count * ROWS_B;
+  const uint32_t G = (n + R - 1) / R;
+  const int PB = FW * (int)k.label_count * R;
   for (uint32_t g0 = blockIdx.x * blockDim.x; g0 < G; g0 += stride) {
     const uint32_t g = g0 + threadIdx.x;
     int count = 0;
-    uint32_t hits = 0;  // ROWS_B > 1: bit j = row j matches
-    if (ROWS_B > 1 && g < G) {
+    uint32_t hits = 0;  // R > 1: bit j = row j matches
+    if (R > 1 && g < G) {
 #pragma unroll 1
-      for (int j = 0; j < ROWS_B; j++) {
+      for (int j = 0; j < R; j++) {
         const uint32_t row = g + (uint32_t)j * G;
         if (row >= n) break;
         uint32_t t[8];
 #pragma unroll
         for (int w = 0; w < 8; w++) t[w] = t_in[(size_t)w * n + row];
-        gej R;
-        row_match_point(R, t, fb, k);
-        pend_store(sc, PB, j, R);
+        gej P;
+        row_match_point(P, t, fb, k);
+        pend_store(sc, PB, j, P);
         count = j + 1;
       }
-      pend_invert<ROWS_B>(sc, PB, count);
+      pend_invert<R>(sc, PB, count);
       // base values of all rows, then the labels of all rows with one
       // batched inversion (match_labels_rows)
 #pragma unroll 1
       for (int j = 0; j < count; j++) {
         const uint32_t row = g + (uint32_t)j * G;
         const uint32_t orow = n == n_rows ? row : row % n_rows;
-        gej R;
+        gej P;
         fe zi;
-        pend_load(R, sc, PB, j);
+        pend_load(P, sc, PB, j);
         scr_load(zi, sc, PEND_ZI(PB, j));
         const uint32_t off = VALUES ? 0u : offs[orow];
         const uint32_t len = VALUES ? 0u : lens[orow];
-        if (row_match_base(R, zi, k, outputs, off, len, sc, PB, j, VALUES ? values + row : nullptr)) hits |= 1u << j;
+        if (row_match_base(P, zi, k, outputs, off, len, sc, PB, j, VALUES ? values + row : nullptr)) hits |= 1u << j;
       }
       if (k.label_count)
         hits |= match_labels_rows(k, labels, outputs, offs, lens, g, G, n, n_rows, count, sc, PB,
                                   VALUES ? values : nullptr);
     }
 #pragma unroll 1
-    for (int j = 0; j < ROWS_B; j++) {
+    for (int j = 0; j < R; j++) {
       const uint32_t row = g + (uint32_t)j * G;
       bool hit = false;
-      if (ROWS_B == 1 && g < n) {
+      if (R == 1 && g < n) {
         uint32_t t[8];
 #pragma unroll
         for (int w = 0; w < 8; w++) t[w] = t_in[(size_t)w * n + row];
@@ -549,8 +552,10 @@ struct cudasp_scanner {
   uint32_t* d_vscratch = nullptr;  // VSCRATCH_WORDS x slots_a
   uint32_t* d_lscratch = nullptr;  // lscratch_words(L) x slots_b
   uint32_t slots_a = 0, slots_b = 0;
-  uint32_t fill_threads = 0;  // stage-A threads per launch that fill the device (rows_a_for)
-  int rows_a_force = 0;       // CUDASP_ROWS_A_FORCE (tests): fixed rows per stage-A thread
+  uint32_t fill_threads = 0;    // stage-A threads per launch that fill the device (rows_a_for)
+  uint32_t fill_threads_b = 0;  // the same for stage B (rows_b_for)
+  int rows_a_force = 0;         // CUDASP_ROWS_A_FORCE (tests): fixed rows per stage-A thread
+  int rows_b_force = 0;         // CUDASP_ROWS_B_FORCE (tests): fixed rows per stage-B thread
   // host-path staging
   uint8_t* d_rows = nullptr;   // capacity x 64
   uint32_t* d_tx = nullptr;    // 8 x capacity
@@ -606,9 +611,19 @@ void launch_a(const cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, u
     hipLaunchKernelGGL(k_shared_secret<ROWS_A>, grid, block, 0, st, tx, ty, n, s->d_naf, s->consts,
                        s->d_vscratch, t);
 }
-uint32_t grid_b(const cudasp_scanner* s, uint32_t n) {
-  uint32_t b = grid_for((n + ROWS_B - 1) / ROWS_B);
-  return b * BLOCK > s->slots_b ? s->slots_b / BLOCK : b;
+uint32_t grid_b(const cudasp_scanner* s, uint32_t n, int rows = ROWS_B) {
+  uint32_t b = grid_for((n + rows - 1) / rows);
+  // the label scratch holds slots_b slots sized for label_cap labels
+  const uint64_t cap = (uint64_t)s->slots_b * lscratch_words(s->label_cap) /
+                       ((uint64_t)lscratch_words(s->label_count, rows) * BLOCK);
+  return b > cap ? (uint32_t)(cap ? cap : 1) : b;
+}
+
+// Rows per stage-B thread: ROWS_B, or 2 for launches with fewer threads than
+// a quarter of the device's wave slots (as rows_a_for).
+int rows_b_for(const cudasp_scanner* s, uint32_t n) {
+  if (s->rows_b_force) return s->rows_b_force;
+  return (n + ROWS_B - 1) / ROWS_B >= s->fill_threads_b ? ROWS_B : 2;
 }
 
 struct DeviceGuard {
@@ -652,16 +667,19 @@ int launch_match(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t
                  hipStream_t st) {
   const uint32_t K = s->consts.output_count;
   const uint32_t N = K * n;
-  const uint32_t blocks_b = grid_b(s, N);
+  const int r = rows_b_for(s, N);
+  const uint32_t blocks_b = grid_b(s, N, r);
+  auto kv = r == ROWS_B ? k_match<true, ROWS_B> : k_match<true, 2>;
+  auto kf = r == ROWS_B ? k_match<false, ROWS_B> : k_match<false, 2>;
   if (values) {
-    hipLaunchKernelGGL(k_match<true>, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels,
-                       nullptr, nullptr, nullptr, s->d_lscratch, nullptr, nullptr, nullptr, values);
+    hipLaunchKernelGGL(kv, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels, nullptr,
+                       nullptr, nullptr, s->d_lscratch, nullptr, nullptr, nullptr, values);
   } else if (K == 1) {
-    hipLaunchKernelGGL(k_match<false>, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels,
-                       outputs, offs, lens, s->d_lscratch, flags, match_rows, match_count, nullptr);
+    hipLaunchKernelGGL(kf, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels, outputs,
+                       offs, lens, s->d_lscratch, flags, match_rows, match_count, nullptr);
   } else {
-    hipLaunchKernelGGL(k_match<false>, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels,
-                       outputs, offs, lens, s->d_lscratch, s->d_vflags, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL(kf, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels, outputs,
+                       offs, lens, s->d_lscratch, s->d_vflags, nullptr, nullptr, nullptr);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_or_flags, dim3(grid_for(n)), dim3(BLOCK), 0, st, s->d_vflags, n, K, flags, match_rows,
                        match_count);
@@ -754,9 +772,14 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
       cus = 256;
     // a quarter of the wave slots (4 SIMDs per CU, CUDASP_WAVES_A waves each)
     s->fill_threads = (uint32_t)cus * 4 * CUDASP_WAVES_A * 64 / 4;
+    s->fill_threads_b = (uint32_t)cus * 4 * CUDASP_WAVES_B * 64 / 4;
     if (const char* f = getenv("CUDASP_ROWS_A_FORCE")) {
       const int r = atoi(f);
       if (r == 1 || r == 2 || r == ROWS_A) s->rows_a_force = r;
+    }
+    if (const char* f = getenv("CUDASP_ROWS_B_FORCE")) {
+      const int r = atoi(f);
+      if (r == 2 || r == ROWS_B) s->rows_b_force = r;
     }
   }
   if ((uint64_t)lscratch_words(label_count) * 4 * BLOCK > (1ull << 32) - 1) {

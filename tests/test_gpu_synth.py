@@ -77,33 +77,48 @@ def test_values_match_oracle_with_labels(torch):
     assert (v.cpu().numpy().T == ov).all()
 
 
-@pytest.mark.parametrize("rows_a", ["1", "2", "4", None])
-def test_rows_per_thread_variants(torch, monkeypatch, rows_a):
-    """Stage A at 1, 2 or 4 rows per thread (4 by default; launches too small
-    to fill the GPU take 2 or 1, rows_a_for in scan_kernels.hip; forced here
-    with CUDASP_ROWS_A_FORCE): 3001 synthetic rows (not a multiple of 2 or 4)
-    with a label, values equal to the oracle's."""
+@pytest.mark.parametrize("rows_a,rows_b", [("1", "2"), ("2", "6"), ("4", "6"), ("4", "2"), (None, None)])
+def test_rows_per_thread_variants(torch, monkeypatch, rows_a, rows_b):
+    """Stage A at 1, 2 or 4 rows per thread and stage B at 2 or 6 (4 / 6 by
+    default; launches too small to fill the GPU take fewer, rows_a_for /
+    rows_b_for in scan_kernels.hip; forced here with CUDASP_ROWS_A_FORCE /
+    CUDASP_ROWS_B_FORCE): 3001 synthetic rows (not a multiple of 2, 4 or 6)
+    with two labels, values and flags equal to the oracle's."""
     from cudasp_amd import Scanner
     from oracle import oracle
-    if rows_a:
-        monkeypatch.setenv("CUDASP_ROWS_A_FORCE", rows_a)
-    else:
-        monkeypatch.delenv("CUDASP_ROWS_A_FORCE", raising=False)
+    for var, val in (("CUDASP_ROWS_A_FORCE", rows_a), ("CUDASP_ROWS_B_FORCE", rows_b)):
+        if val:
+            monkeypatch.setenv(var, val)
+        else:
+            monkeypatch.delenv(var, raising=False)
     n = 3001
-    x, y, _, _, _ = synth(torch, 555, n)
-    with Scanner(SCAN, SPEND, [LABEL], max_rows=n) as s:
+    labels = [LABEL, SPEND]
+    x, y, outs, offs, lens = synth(torch, 555, n)
+    rows = rows_of(x, y)
+    _, ov = oracle.scan(SCAN, SPEND, labels, rows, threads=16, want_values=True)
+    # plant every 7th row's second-label value as its first output
+    o = outs.cpu().numpy().reshape(n, 2)
+    o[::7, 0] = ov[::7, 2]
+    outs.copy_(torch.from_numpy(o.reshape(-1)))
+    with Scanner(SCAN, SPEND, labels, max_rows=n) as s:
         t = torch.empty((8, n), dtype=torch.int32, device="cuda")
-        v = torch.empty((2, n), dtype=torch.int64, device="cuda")
+        v = torch.empty((3, n), dtype=torch.int64, device="cuda")
         s.row_values_device(x, y, t, v)
+        flags = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        s.scan_device(x, y, outs, offs, lens, flags)
         s.sync()
-    _, ov = oracle.scan(SCAN, SPEND, [LABEL], rows_of(x, y), threads=16, want_values=True)
     assert (v.cpu().numpy().T == ov).all()
+    want, _ = oracle.scan(SCAN, SPEND, labels, rows, o.reshape(-1), offs.cpu().numpy().view(np.uint32),
+                          lens.cpu().numpy().view(np.uint32), threads=16)
+    assert int(want.sum()) >= n // 7
+    assert (flags.cpu().numpy() == want).all()
 
 
 def test_rows_per_thread_large_launch(torch, monkeypatch):
     """200k rows at 1, 2 and 4 rows per thread give identical t: the 1- and
     2-row launches need more scratch slots than the scanner holds, so their
-    grids are capped and the grid-stride loop takes the remaining rows."""
+    grids are capped and the grid-stride loop takes the remaining rows.  Stage
+    B at 6 and 2 rows per thread gives identical values."""
     from cudasp_amd import Scanner
     n = 200000
     x, y, _, _, _ = synth(torch, 31337, n)
@@ -116,6 +131,17 @@ def test_rows_per_thread_large_launch(torch, monkeypatch):
             s.sync()
         ts.append(t.cpu())
     assert torch.equal(ts[0], ts[1]) and torch.equal(ts[0], ts[2])
+    # stage B at 6 and 2 rows per thread on the same t: identical values
+    vs = []
+    for r in ("6", "2"):
+        monkeypatch.setenv("CUDASP_ROWS_B_FORCE", r)
+        with Scanner(SCAN, SPEND, [LABEL], max_rows=n) as s:
+            t = torch.zeros((8, n), dtype=torch.int32, device="cuda")
+            v = torch.zeros((2, n), dtype=torch.int64, device="cuda")
+            s.row_values_device(x, y, t, v)
+            s.sync()
+        vs.append(v.cpu())
+    assert torch.equal(vs[0], vs[1])
 
 
 def _plant(torch, x, y, outs, labels, every=1000):

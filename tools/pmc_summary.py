@@ -26,13 +26,17 @@ SCAN_KERNELS = ("k_shared_secret", "void k_match<false>", "void k_match<true>", 
 
 
 def kernel_key(name):
-    """Kernel name without arguments; stage A's full-batch instance (4 rows
-    per thread, CUDASP_ROWS_A) keeps the plain name bench.py looks up, the
-    small-launch instances (rows_a_for) stay separate."""
+    """Kernel name without arguments; the full-batch instances of stage A
+    (4 rows per thread, CUDASP_ROWS_A) and stage B (6, CUDASP_ROWS_B) keep the
+    plain names bench.py looks up, the small-launch instances (rows_a_for,
+    rows_b_for) stay separate."""
     k = name.split("(")[0]
     m = re.fullmatch(r"void k_shared_secret<(\d+)>", k)
     if m:
         k = "k_shared_secret" if m.group(1) == "4" else "k_shared_secret<%s>" % m.group(1)
+    m = re.fullmatch(r"void k_match<(true|false), (\d+)>", k)
+    if m:  # stage B: 6 rows per thread (CUDASP_ROWS_B) for full batches
+        k = "void k_match<%s>" % m.group(1) if m.group(2) == "6" else "void k_match<%s, %s>" % m.groups()
     return k
 
 
