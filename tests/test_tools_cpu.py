@@ -1,0 +1,40 @@
+"""CPU: the measurement tooling that bench.py's roofline fields depend on.
+
+bench.py reads the committed PMC summaries (profiles/r01_pmc_*.json) by
+kernel name.  The kernels are templates on their rows per thread (rows_a_for /
+rows_b_for), so rocprofv3 reports e.g. `void k_shared_secret<4>`; the summary
+tool must map the full-batch instances to the names bench.py looks up."""
+import importlib.util
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _pmc_summary():
+    spec = importlib.util.spec_from_file_location("pmc_summary", os.path.join(ROOT, "tools", "pmc_summary.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_kernel_names():
+    k = _pmc_summary().kernel_key
+    assert k("void k_shared_secret<4>(unsigned int const*, unsigned int const*, unsigned int)") == "k_shared_secret"
+    assert k("void k_shared_secret<1>(unsigned int const*)") == "k_shared_secret<1>"
+    assert k("void k_match<false, 6>(unsigned int const*, unsigned int)") == "void k_match<false>"
+    assert k("void k_match<true, 6>(x)") == "void k_match<true>"
+    assert k("void k_match<false, 2>(x)") == "void k_match<false, 2>"
+    assert k("k_layout_probe(unsigned int const*)") == "k_layout_probe"
+
+
+def test_committed_profiles_have_bench_keys():
+    """The summaries bench.py reads by default carry the counters it uses."""
+    sq = json.load(open(os.path.join(ROOT, "profiles", "r01_pmc_sq_counters.json")))["per_kernel"]
+    for name in ("k_shared_secret", "void k_match<false>"):
+        assert sq[name]["SQ_INSTS_VALU"] > 0, name
+    hbm = json.load(open(os.path.join(ROOT, "profiles", "r01_pmc_k_shared_secret.json")))
+    assert hbm["hbm_bytes_per_launch"] > 0
+    per = hbm["per_kernel"]
+    assert per["k_shared_secret"]["FETCH_SIZE_KiB_per_launch"] > 0
+    assert per["k_layout_probe"]["FETCH_SIZE_KiB_per_launch"] > 0
