@@ -1,7 +1,7 @@
 # Host end-to-end A/B: the in-tree library vs build_variants/old (same ABI), rows and columns, 8 threads, 2 rounds.
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O; cd $R
-for round in 1 2; do
+for round in $(seq ${AB_ROUNDS:-2}); do
 for v in new old; do
 for mode in rows columns; do
   if [ $v = old ]; then export LD_LIBRARY_PATH=$R/build_variants/old; else unset LD_LIBRARY_PATH; fi
