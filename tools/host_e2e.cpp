@@ -10,6 +10,7 @@
 // Prints one JSON line.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -149,6 +150,7 @@ int main(int argc, char** argv) {
   double gen_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - g0).count();
 
   // ---------------- the query --------------------------------------------
+  char stats[512] = "";
   auto run = [&](double* secs, uint64_t* found) {
     cudasp_tf_blob_arg a_scan{scan, 32, 1}, a_spend{spend, 64, 1};
     std::vector<cudasp_tf_blob_arg> a_lab(nlabels);
@@ -165,7 +167,11 @@ int main(int argc, char** argv) {
     for (int t = 0; t < threads; t++) CK(cudasp_tf_local_init(gs, &ls[t]));
     std::atomic<uint64_t> next{0};
     std::atomic<uint64_t> emitted{0};
+    // per thread: seconds inside the table-function calls, inside final (the
+    // last batch and the wait for it), and until the thread is done
+    std::vector<double> t_calls(threads, 0.0), t_final(threads, 0.0), t_done(threads, 0.0), t_long(threads, 0.0);
     auto t0 = std::chrono::steady_clock::now();
+    auto now_s = [&t0]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
     std::vector<std::thread> th;
     for (int t = 0; t < threads && columnar; t++) {
       th.emplace_back([&, t]() {
@@ -186,8 +192,13 @@ int main(int argc, char** argv) {
           c.list_offsets = list_off32.data();
           c.list_offset = c0;
           c.child_values = outputs.data();
+          const double c0s = now_s();
           CK(cudasp_tf_function_columns(bd, gs, ls[t], &c));
+          const double dt = now_s() - c0s;
+          t_calls[t] += dt;
+          if (dt > 5e-4) t_long[t] += dt;  // calls that launched a batch / waited for one
         }
+        const double f0s = now_s();
         cudasp_tf_output* out = new cudasp_tf_output;
         for (;;) {
           int rc = cudasp_tf_final(bd, gs, ls[t], out);
@@ -196,6 +207,8 @@ int main(int argc, char** argv) {
           if (rc != CUDASP_TF_HAVE_MORE_OUTPUT) break;
         }
         delete out;
+        t_final[t] = now_s() - f0s;
+        t_done[t] = now_s();
       });
     }
     for (int t = 0; t < threads && !columnar; t++) {
@@ -222,8 +235,13 @@ int main(int argc, char** argv) {
           c.list_offset = loff.data();
           c.list_length = list_len.data() + c0;
           c.child_values = outputs.data() + list_off[c0];
+          const double c0s = now_s();
           CK(cudasp_tf_function(bd, gs, ls[t], &c));
+          const double dt = now_s() - c0s;
+          t_calls[t] += dt;
+          if (dt > 5e-4) t_long[t] += dt;  // calls that launched a batch / waited for one
         }
+        const double f0s = now_s();
         cudasp_tf_output* out = new cudasp_tf_output;
         for (;;) {
           int rc = cudasp_tf_final(bd, gs, ls[t], out);
@@ -232,11 +250,19 @@ int main(int argc, char** argv) {
           if (rc != CUDASP_TF_HAVE_MORE_OUTPUT) break;
         }
         delete out;
+        t_final[t] = now_s() - f0s;
+        t_done[t] = now_s();
       });
     }
     for (auto& x : th) x.join();
     *secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     *found = emitted.load();
+    auto mean = [](const std::vector<double>& v) { double a = 0; for (double x : v) a += x; return a / v.size(); };
+    snprintf(stats, sizeof(stats),
+             "\"thread_call_s_mean\": %.4f, \"thread_long_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
+             "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f",
+             mean(t_calls), mean(t_long), mean(t_final), *std::min_element(t_done.begin(), t_done.end()),
+             *std::max_element(t_done.begin(), t_done.end()));
     for (auto* l : ls) cudasp_tf_local_free(l);
     cudasp_tf_global_free(gs);
     cudasp_tf_bind_free(bd);
@@ -250,10 +276,10 @@ int main(int argc, char** argv) {
   printf("{\"what\": \"table-function host end-to-end (host memory -> matches, PCIe-inclusive)\", \"input\": \"%s\", "
          "\"rows\": %llu, \"threads\": %d, \"batch_size\": %lld, \"labels\": %d, \"outputs_per_row\": %d, "
          "\"seconds\": %.4f, \"tx_per_s\": %.1f, \"matches\": %llu, \"planted\": %llu, \"warmup_seconds\": %.3f, "
-         "\"generate_seconds\": %.2f, \"devices\": %d}\n",
+         "\"generate_seconds\": %.2f, \"devices\": %d, %s}\n",
          columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)rows, threads, (long long)batch, nlabels,
          k, secs, rows / secs,
-         (unsigned long long)found, (unsigned long long)planted, warm_s, gen_s, cudasp_device_count());
+         (unsigned long long)found, (unsigned long long)planted, warm_s, gen_s, cudasp_device_count(), stats);
   return found == planted ? 0 : 2;
 }
 
