@@ -60,6 +60,9 @@ static uint64_t splitmix64(uint64_t z) {
   } while (0)
 
 int main(int argc, char** argv) {
+  // As the DuckDB extension does when it loads (duckdb_ext/cudasp_extension.cpp):
+  // 16 hardware queues unless the environment sets a value; before any HIP call.
+  setenv("GPU_MAX_HW_QUEUES", "16", 0);
   uint64_t rows = argc > 1 ? strtoull(argv[1], 0, 10) : 32700000ull;
   int threads = argc > 2 ? atoi(argv[2]) : 16;
   int64_t batch = argc > 3 ? atoll(argv[3]) : 300000;
@@ -276,10 +279,11 @@ int main(int argc, char** argv) {
   printf("{\"what\": \"table-function host end-to-end (host memory -> matches, PCIe-inclusive)\", \"input\": \"%s\", "
          "\"rows\": %llu, \"threads\": %d, \"batch_size\": %lld, \"labels\": %d, \"outputs_per_row\": %d, "
          "\"seconds\": %.4f, \"tx_per_s\": %.1f, \"matches\": %llu, \"planted\": %llu, \"warmup_seconds\": %.3f, "
-         "\"generate_seconds\": %.2f, \"devices\": %d, %s}\n",
+         "\"generate_seconds\": %.2f, \"devices\": %d, \"gpu_max_hw_queues\": \"%s\", %s}\n",
          columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)rows, threads, (long long)batch, nlabels,
          k, secs, rows / secs,
-         (unsigned long long)found, (unsigned long long)planted, warm_s, gen_s, cudasp_device_count(), stats);
+         (unsigned long long)found, (unsigned long long)planted, warm_s, gen_s, cudasp_device_count(),
+         getenv("GPU_MAX_HW_QUEUES") ? getenv("GPU_MAX_HW_QUEUES") : "", stats);
   return found == planted ? 0 : 2;
 }
 
