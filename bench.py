@@ -7,26 +7,32 @@ Contract (see DESIGN.md "Measurement"):
   torch.distributed.run; ranks read RANK / LOCAL_RANK / WORLD_SIZE.
 
 Workload (BASELINE.json metric "tx/sec through cudasp_scan on 32M-row tweak
-table", configs[3] shape): every rank holds its own 32.7M-row synthetic table
-resident in HBM (weak scaling: per-GPU work is fixed as N grows) laid out as the
-reference's batches of batch_size = 300000 rows, tweak limbs column-major per
-batch.  A step is one pass of the hot path over the rank's whole table: every
-batch goes through cudasp_scan_device (stage A: d*T + tagged hash; stage B:
-t*G + B, labels, compare, flag + ballot compaction), batches round-robin over
-`--streams` HIP streams (the reference's per-thread streams,
-src/cudasp_gpu.cu:505).  Inputs are resident before the timed region; the
-PCIe-inclusive host path is measured separately.
+table at 1/2/4/8 MI355X", configs[3]): ONE 32.7M-row synthetic table, cut into
+the reference's batch_size = 300000-row batches; batch b is scanned by rank
+b mod N (the product's assignment, cudasp_assign_gpu; the reference
+round-robins its executor threads over GPUs, src/cudasp_extension.cu:523-529),
+so the total work is fixed as N grows (`--shard weak` gives every rank its own
+table instead).  Each rank's batches are resident in HBM, tweak limbs
+column-major per batch.  A step is one pass of the hot path over the rank's
+batches: every batch goes through the two kernels of cudasp_scan_device
+(stage A: d*T + tagged hash; stage B: t*G + B, labels, compare, flag + ballot
+compaction), batches round-robin over `--streams` HIP streams (the
+reference's per-thread streams, src/cudasp_gpu.cu:505).  No collective in the
+data path: torch.distributed carries the bracketing barrier and the max of the
+elapsed time.  After the timed steps, rank 0 at N = 1 also reports the
+PCIe-inclusive end-to-end rate of the table-function host (`e2e`,
+tools/host_e2e) -- never the `value`.
 
 Synthetic data: T_i = (s0 + g) G with s0 = SHA256("cudasp-synth-v1")
 mod n and g the global row index; 2 splitmix64 outputs per row (seed
-0xC0DA5EED); every 1000th row gets its true compare value planted, so the
+0xC0DA5EED); every 1000th row gets its true compare value planted, and with
+L labels the next row gets label j's value, j cycling over all L labels, so the
 expected match count is known exactly and checked after the run.
 
 Only the cpu_baseline leg touches oracle/ (the C restatement, timed on a
 bounded sample on this box's host cores, and checked against the GPU flags).
 """
 import argparse
-import ctypes
 import hashlib
 import json
 import os
@@ -121,28 +127,33 @@ def synth_s0():
 
 
 class Table:
-    """One rank's resident synthetic table, batch-major."""
+    """One rank's resident share of the synthetic table, batch-major.
 
-    def __init__(self, lib, device, rows, batch, k, labels, first_global, dev_stream, kmax=0):
+    batches: [(first global row, rows)] of the rank's batches (whole
+    batch_size-row batches of the global table, the last one possibly short)."""
+
+    def __init__(self, lib, device, batches, batch, k, labels, dev_stream, kmax=0):
         """k: fixed outputs per row; kmax > 0: variable lengths uniform in [1, kmax]."""
-        self.rows, self.batch, self.k, self.kmax = rows, batch, k, kmax
+        self.batch, self.k, self.kmax = batch, k, kmax
         cap = kmax if kmax else k
-        self.nb = (rows + batch - 1) // batch
-        self.sizes = [min(batch, rows - b * batch) for b in range(self.nb)]
+        self.first = [g0 for g0, _ in batches]
+        self.sizes = [m for _, m in batches]
+        self.nb = len(batches)
+        self.rows = sum(self.sizes)
         dev = torch.device("cuda", device)
-        self.tx = torch.empty((self.nb, 8, batch), dtype=torch.int32, device=dev)
-        self.ty = torch.empty((self.nb, 8, batch), dtype=torch.int32, device=dev)
-        self.outs = torch.empty((self.nb, batch * cap), dtype=torch.int64, device=dev)
-        self.offs = torch.empty((self.nb, batch), dtype=torch.int32, device=dev)
-        self.lens = torch.empty((self.nb, batch), dtype=torch.int32, device=dev)
-        self.flags = torch.zeros((self.nb, batch), dtype=torch.uint8, device=dev)
-        self.match_rows = torch.zeros((self.nb, batch), dtype=torch.int32, device=dev)
-        self.match_count = torch.zeros((self.nb,), dtype=torch.int32, device=dev)
+        nb = max(1, self.nb)
+        self.tx = torch.empty((nb, 8, batch), dtype=torch.int32, device=dev)
+        self.ty = torch.empty((nb, 8, batch), dtype=torch.int32, device=dev)
+        self.outs = torch.empty((nb, batch * cap), dtype=torch.int64, device=dev)
+        self.offs = torch.empty((nb, batch), dtype=torch.int32, device=dev)
+        self.lens = torch.empty((nb, batch), dtype=torch.int32, device=dev)
+        self.flags = torch.zeros((nb, batch), dtype=torch.uint8, device=dev)
+        self.match_rows = torch.zeros((nb, batch), dtype=torch.int32, device=dev)
+        self.match_count = torch.zeros((nb,), dtype=torch.int32, device=dev)
         s0 = synth_s0()
         st = _native.stream_arg(dev_stream)
         for b in range(self.nb):
-            m = self.sizes[b]
-            g0 = first_global + b * batch
+            m, g0 = self.sizes[b], self.first[b]
             _native.check(lib.cudasp_synth_tweak_columns(device, s0, g0, m, self.tx[b].data_ptr(),
                                                          self.ty[b].data_ptr(), st))
             if kmax:
@@ -157,18 +168,22 @@ class Table:
                                                        self.offs[b].data_ptr(), self.lens[b].data_ptr(), st))
         torch.cuda.synchronize(dev)
         # Plant true values (computed by the product's own stage outputs; the
-        # test suite checks those against the oracle): base value every 1000th
-        # global row, label-0 value on the row after it when labels exist.
-        self.total_outputs = int(self.lens.sum().item()) if kmax else rows * k
+        # test suite checks those against the oracle): the base value on every
+        # global row g = 0 mod 1000 and, with L labels, label j's value on row
+        # g = 1 mod 1000 with j = (g // 1000) mod L, so every label index of
+        # the label loop (src/cudasp_gpu.cu:153-172) is planted and must be found.
+        self.total_outputs = sum(int(self.lens[b][:self.sizes[b]].to(torch.int64).sum().item())
+                                 for b in range(self.nb)) if kmax else self.rows * k
         self.expected = 0
         self.expected_per_batch = [0] * self.nb
+        self.planted_labels = set()
+        L = len(labels)
         per_batch = 2 * ((batch + PLANT_EVERY - 1) // PLANT_EVERY) + 2
         planter = Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=per_batch, device=device)
         for b in range(self.nb):
-            m = self.sizes[b]
-            g0 = first_global + b * batch
+            m, g0 = self.sizes[b], self.first[b]
             base_idx = [i for i in range((-g0) % PLANT_EVERY, m, PLANT_EVERY)]
-            lab_idx = [i for i in range((1 - g0) % PLANT_EVERY, m, PLANT_EVERY)] if labels else []
+            lab_idx = [i for i in range((1 - g0) % PLANT_EVERY, m, PLANT_EVERY)] if L else []
             idx = base_idx + lab_idx
             if not idx:
                 continue
@@ -176,14 +191,18 @@ class Table:
             gx = self.cols(self.tx, b).index_select(1, it).contiguous()
             gy = self.cols(self.ty, b).index_select(1, it).contiguous()
             t = torch.empty((8, len(idx)), dtype=torch.int32, device=dev)
-            vals = torch.empty((1 + len(labels), len(idx)), dtype=torch.int64, device=dev)
+            vals = torch.empty((1 + L, len(idx)), dtype=torch.int64, device=dev)
             planter.row_values_device(gx, gy, t, vals)
             planter.sync()
             nbase = len(base_idx)
             pos = self.offs[b][:m].index_select(0, it).to(torch.int64)  # slot 0 of each planted list
             self.outs[b].index_copy_(0, pos[:nbase], vals[0, :nbase])
             if lab_idx:
-                self.outs[b].index_copy_(0, pos[nbase:], vals[1, nbase:])
+                js = [((g0 + i) // PLANT_EVERY) % L for i in lab_idx]
+                self.planted_labels.update(js)
+                jt = torch.tensor(js, dtype=torch.int64, device=dev)
+                cols = torch.arange(nbase, len(idx), dtype=torch.int64, device=dev)
+                self.outs[b].index_copy_(0, pos[nbase:], vals[1 + jt, cols])
             self.expected += len(idx)
             self.expected_per_batch[b] = len(idx)
         planter.close()
@@ -220,11 +239,28 @@ def shard_first_row(rank, rows_per_rank):
     return rank * rows_per_rank
 
 
+def rank_batches(shard, rows, batch, rank, world, assign):
+    """The (first global row, rows) batches a rank scans.
+
+    roundrobin (config 4, the default): ONE table of `rows` rows cut into
+    batch_size-row batches; batch b goes to rank assign(b, world), the
+    product's own assignment (cudasp_assign_gpu: b mod N, as the reference
+    round-robins its executor threads over GPUs, src/cudasp_extension.cu:523-529).
+    weak: every rank scans its own `rows`-row table (global rows
+    [rank * rows, (rank + 1) * rows))."""
+    if shard == "roundrobin":
+        nb = (rows + batch - 1) // batch
+        return [(b * batch, min(batch, rows - b * batch)) for b in range(nb) if assign(b, world) == rank]
+    first = shard_first_row(rank, rows)
+    return [(first + b * batch, min(batch, rows - b * batch)) for b in range((rows + batch - 1) // batch)]
+
+
 def run_step(tab, scanners, streams, events=None):
     """One pass over the rank's table.  Each batch is the two kernels of
     cudasp_scan_device (stage A then stage B on the batch's stream); when
-    `events` is a list, HIP events bracket each launch on its stream (the
-    per-launch kernel durations of the roofline)."""
+    `events` is a list, HIP events bracket each launch on its stream (with
+    several streams a launch's span includes the time it shares the GPU with
+    the other streams' kernels)."""
     tab.match_count.zero_()
     cur = torch.cuda.current_stream()
     for st in streams:
@@ -247,6 +283,36 @@ def run_step(tab, scanners, streams, events=None):
                 events.append((e0, e1, e2))
 
 
+def exclusive_launches(tab, scanner, stream, max_batches):
+    """Per-launch kernel durations with each launch ALONE on the GPU: after
+    the timed steps, up to `max_batches` full batches go through one stream
+    (so no two kernels overlap), HIP events recorded on that stream around
+    each stage.  These are the durations a rocprofv3 kernel trace reports for
+    the same dispatches (tools/prof_summary.py: `exclusive` = dispatches that
+    overlap no other dispatch).  Also re-checks those batches' match counts."""
+    full = [b for b in range(tab.nb) if tab.sizes[b] == tab.batch][:max_batches]
+    ev = []
+    tab.match_count.zero_()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        for b in full:
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(stream)
+            scanner.stage_shared_secret(tab.tx[b], tab.ty[b], tab.sizes[b], stream)
+            e1.record(stream)
+            scanner.stage_match(tab.outs[b], tab.offs[b], tab.lens[b], tab.sizes[b], tab.flags[b],
+                                tab.match_rows[b], tab.match_count[b:b + 1], stream)
+            e2.record(stream)
+            ev.append((e0, e1, e2))
+    stream.synchronize()
+    counts = tab.match_count.tolist()
+    ok = all(counts[b] == tab.expected_per_batch[b] for b in full)
+    a = [e0.elapsed_time(e1) for e0, e1, _ in ev]
+    m = [e1.elapsed_time(e2) for _, e1, e2 in ev]
+    return dict(launches=len(full), stage_a_ms=float(np.mean(a)) if a else None,
+                stage_b_ms=float(np.mean(m)) if m else None, matches_equal_planted=ok)
+
+
 def layout_probe(lib, tab, reps=5):
     """HBM cost of the data layout alone: k_layout_probe (cudasp_layout_probe)
     over the whole rank table as one column-major launch, reading exactly the
@@ -254,7 +320,6 @@ def layout_probe(lib, tab, reps=5):
     mapping and no arithmetic.  Timed with HIP events on the current stream,
     after (and outside) the timed bench steps."""
     m = tab.sizes
-    k = tab.kmax if tab.kmax else tab.k
     x = torch.cat([tab.cols(tab.tx, b) for b in range(tab.nb)], dim=1).contiguous()
     y = torch.cat([tab.cols(tab.ty, b) for b in range(tab.nb)], dim=1).contiguous()
     lens = torch.cat([tab.lens[b][:m[b]] for b in range(tab.nb)]).contiguous()
@@ -291,6 +356,51 @@ def layout_probe(lib, tab, reps=5):
                 frac=gbs / HBM_PEAK_GBS,
                 note="the scan's algorithmic HBM bytes (73 + 8k per row) moved with the kernels' thread "
                      "mapping and no arithmetic: the layout's own HBM roofline, one launch over the rank table")
+
+
+def host_cores():
+    """Host CPUs this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS when the environment sets it (on the GPU pool the box's
+    CPU share is set there, while the mask shows the whole machine)."""
+    visible = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    use = min(visible, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else visible
+    return use, visible
+
+
+def e2e_leg(args, mean_k):
+    """PCIe-inclusive end-to-end rate through the table-function host
+    (include/cudasp_host.h, the calls DuckDB's executor makes): tools/host_e2e
+    as a child process, the same global table shape in host memory, fed as
+    DuckDB-style 2048-row chunks by --e2e-threads executor threads; its first
+    query warms the process (scanner creation, table build), the second is
+    timed.  The child gets GPU_MAX_HW_QUEUES=16, what the DuckDB extension sets
+    at load when the environment leaves it unset
+    (duckdb_ext/cudasp_extension.cpp)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "host_e2e")
+    if not os.path.exists(exe):
+        return dict(error="tools/host_e2e not built (make -C duckdb-cudasp-extension_amd)")
+    k = max(1, int(round(mean_k)))
+    env = dict(os.environ, CUDASP_FB_BITS=str(args.fb_bits), GPU_MAX_HW_QUEUES=str(args.e2e_hw_queues))
+    cmd = [exe, str(args.rows), str(args.e2e_threads), str(args.batch_size), str(args.labels), str(k), "rows"]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.e2e_timeout, env=env)
+    except subprocess.TimeoutExpired:
+        return dict(error="timed out after %d s" % args.e2e_timeout, cmd=" ".join(cmd[1:]))
+    line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else ""
+    try:
+        res = json.loads(line)
+    except ValueError:
+        return dict(error="exit %d: %s" % (r.returncode, (r.stderr or r.stdout)[-400:]), cmd=" ".join(cmd[1:]))
+    res["exit_code"] = r.returncode
+    res["wall_s"] = round(time.perf_counter() - t0, 2)
+    res["args"] = " ".join(cmd[1:])
+    res["fixed_base_bits"] = args.fb_bits
+    if args.outputs_max:
+        res["note"] = "fixed %d outputs per row (host_e2e has no variable-length lists)" % k
+    return res
 
 
 def cpu_baseline(tab, labels, sample_rows, threads, output_count=1, label_negation=False):
@@ -332,12 +442,55 @@ def cpu_baseline(tab, labels, sample_rows, threads, output_count=1, label_negati
                 sample_matches=int(flags.sum()))
 
 
+def sq_profile_path(args):
+    """The PMC instruction-count summary matching this run's shape (labels,
+    outputs per row, fixed-base width, variants):
+    profiles/r02_pmc_sq_L<labels>_k<outputs>_w<bits>[_neg][_K<k>].json."""
+    kdesc = "1-%d" % args.outputs_max if args.outputs_max else str(args.outputs_per_row)
+    name = "r02_pmc_sq_L%d_k%s_w%d" % (args.labels, kdesc, args.fb_bits)
+    if args.label_negation:
+        name += "_neg"
+    if args.output_count != 1:
+        name += "_K%d" % args.output_count
+    return os.path.join(ROOT, "profiles", name + ".json")
+
+
+def alu_roofline(path, value_per_gpu):
+    """Integer-VALU roofline of the whole path: VALU wave-instructions per row
+    of both kernels (rocprofv3 SQ_INSTS_VALU of the same shape of run,
+    profiles/) x rows/s per GPU, against the nominal VALU issue rate and the
+    measured VOP3 rate."""
+    if not path or not os.path.exists(path):
+        return dict(error="no PMC summary for this shape: %s" % os.path.relpath(path, ROOT) if path else "none")
+    with open(path) as f:
+        sq = json.load(f)
+    per = sq["per_kernel"]
+    rpl = float(sq.get("rows_per_launch", 300000))
+    a = per.get("k_shared_secret", {}).get("SQ_INSTS_VALU")
+    bm = per.get("void k_match<false>", {}).get("SQ_INSTS_VALU")
+    if not (a and bm):
+        return dict(error="%s lacks the stage kernels" % os.path.relpath(path, ROOT))
+    wi_per_row = (a + bm) / rpl
+    achieved_wi = wi_per_row * value_per_gpu
+    return dict(bound="valu", unit="wave-instr/s per GPU", achieved=achieved_wi, peak=VALU_WAVE_INSTR_PEAK,
+                frac=achieved_wi / VALU_WAVE_INSTR_PEAK, measured_vop3_issue_rate=VOP3_WAVE_INSTR_MEASURED,
+                frac_of_measured_vop3_rate=achieved_wi / VOP3_WAVE_INSTR_MEASURED,
+                valu_wave_instr_per_64_rows=dict(k_shared_secret=a / rpl * 64, k_match=bm / rpl * 64),
+                source=os.path.relpath(path, ROOT),
+                note="SQ_INSTS_VALU per row of a run of this shape (%s); peak = nominal VALU issue rate; VOP3 "
+                     "integer ops issue at about half of it on gfx950" % sq.get("shape", "see source"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--rows", type=int, default=32_700_000, help="rows per rank")
+    ap.add_argument("--rows", type=int, default=32_700_000,
+                    help="rows of the table (roundrobin) or of each rank's table (weak)")
+    ap.add_argument("--shard", choices=["roundrobin", "weak"], default="roundrobin",
+                    help="roundrobin: ONE table, batch b on rank b mod N (BASELINE configs[3], strong scaling); "
+                         "weak: every rank scans its own table")
     ap.add_argument("--batch-size", type=int, default=300_000)
     ap.add_argument("--labels", type=int, default=0)
     ap.add_argument("--output-count", type=int, default=1,
@@ -346,13 +499,21 @@ def main():
     ap.add_argument("--outputs-per-row", type=int, default=2)
     ap.add_argument("--outputs-max", type=int, default=0,
                     help="variable outputs per row, uniform in [1, N] (15 -> mean 8, config 5); 0 = fixed")
+    ap.add_argument("--fb-bits", type=int, default=26, choices=[22, 26],
+                    help="fixed-base window width (26: 21.5 GB table, 22: 1.5 GiB; same results)")
     ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--exclusive-batches", type=int, default=16,
+                    help="full batches timed alone on one stream after the timed steps (roofline kernel_ms)")
     ap.add_argument("--cpu-rows", type=int, default=1200000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this process may use")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layout-probe", action="store_true")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_k_shared_secret.json"))
-    ap.add_argument("--pmc-sq", default=os.path.join(ROOT, "profiles", "r01_pmc_sq_counters.json"))
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--e2e-threads", type=int, default=8)
+    ap.add_argument("--e2e-hw-queues", type=int, default=16)
+    ap.add_argument("--e2e-timeout", type=int, default=420)
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02_pmc_hbm_k_shared_secret.json"))
+    ap.add_argument("--pmc-sq", default="", help="SQ counter summary (default: the file matching this run's shape)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) for the barrier/max; gloo to rehearse "
                     "several ranks on one GPU")
     args = ap.parse_args()
@@ -360,6 +521,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # The window width is the process default for every scanner and the
+    # synthetic-table generator (read once by the library).
+    os.environ["CUDASP_FB_BITS"] = str(args.fb_bits)
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     if world > 1:
@@ -368,17 +532,20 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
     lib = _native.load()
+    from cudasp_amd import assign_gpu
 
     labels = label_keys(args.labels)
     gen_stream = torch.cuda.Stream(device)
     t_setup = time.perf_counter()
-    tab = Table(lib, device, args.rows, args.batch_size, args.outputs_per_row, labels,
-                first_global=shard_first_row(rank, args.rows), dev_stream=gen_stream, kmax=args.outputs_max)
+    batches = rank_batches(args.shard, args.rows, args.batch_size, rank, world, assign_gpu)
+    tab = Table(lib, device, batches, args.batch_size, args.outputs_per_row, labels, dev_stream=gen_stream,
+                kmax=args.outputs_max)
     streams = [torch.cuda.Stream(device) for _ in range(args.streams)]
     scanners = [Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=args.batch_size, device=device)
                 for _ in range(args.streams)]
-    if args.output_count != 1 or args.label_negation:
-        for s in scanners:
+    for s in scanners:
+        s.set_fixed_base_bits(args.fb_bits)
+        if args.output_count != 1 or args.label_negation:
             s.set_options(args.output_count, args.label_negation)
     setup_s = time.perf_counter() - t_setup
 
@@ -403,87 +570,76 @@ def main():
         barrier()
         times.append(time.perf_counter() - t0)
         step_found.append(int(tab.match_count.sum().item()))
-    step_s = float(np.mean(times))
     total_s = float(np.sum(times))
     found = int(tab.match_count.sum().item())
     flagged = int(tab.flags.sum().item())
     if found != tab.expected or flagged != tab.expected:
         per = tab.match_count.tolist()
         bad = [(b, per[b], tab.expected_per_batch[b]) for b in range(tab.nb) if per[b] != tab.expected_per_batch[b]]
+        # Diagnostic only: the reported `matches` are the timed steps' counts above.
         print("rank %d: %d found, %d flagged, %d planted; found per step %s; batches (index, found, planted) "
               "that differ: %s" % (rank, found, flagged, tab.expected, step_found, bad[:16]), file=sys.stderr, flush=True)
-        # Re-scan the differing batches alone: a transient error finds them all again.
-        for b, _, _ in bad[:4]:
-            tab.match_count[b].zero_()
-            with torch.cuda.stream(streams[0]):
-                streams[0].wait_stream(torch.cuda.current_stream())
-                scanners[0].stage_shared_secret(tab.tx[b], tab.ty[b], tab.sizes[b], streams[0])
-                scanners[0].stage_match(tab.outs[b], tab.offs[b], tab.lens[b], tab.sizes[b], tab.flags[b],
-                                        tab.match_rows[b], tab.match_count[b:b + 1], streams[0])
-            torch.cuda.synchronize(device)
-            print("rank %d: batch %d re-scanned alone: %d found of %d planted"
-                  % (rank, b, int(tab.match_count[b].item()), tab.expected_per_batch[b]), file=sys.stderr, flush=True)
     total_s, found, flagged, expected = aggregate(world, args.dist_backend, total_s, found, flagged, tab.expected)
 
-    # Per-launch kernel durations over the timed region (HIP events on each
-    # launch's stream; with several streams a launch's span includes the time
-    # it shares the GPU with the other streams' kernels).
+    # Per-launch kernel durations.  The timed steps run 4 streams at once, so a
+    # launch's event span there includes time shared with the other streams'
+    # kernels (launch_span_ms_concurrent); kernel_ms is the duration of a launch
+    # alone on the GPU (exclusive_launches, after the timed region).
     ka = [e0.elapsed_time(e1) for e0, e1, _ in events]
     kb = [e1.elapsed_time(e2) for _, e1, e2 in events]
-    ka_ms, kb_ms = float(np.mean(ka)), float(np.mean(kb))
-    rows_per_launch = float(np.mean(tab.sizes))
-    mean_k = tab.total_outputs / args.rows
+    excl = exclusive_launches(tab, scanners[0], streams[0], args.exclusive_batches)
+    rows_per_launch = float(args.batch_size)
+    mean_k = tab.total_outputs / max(1, tab.rows)
     algo_bytes = bytes_per_row(mean_k) * rows_per_launch
-    achieved_gbs = algo_bytes / (ka_ms * 1e-3) / 1e9
+    kernel_ms = excl["stage_a_ms"] or float(np.mean(ka))
+    achieved_gbs = algo_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.pmc_summary):
         with open(args.pmc_summary) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
-    rows_total = args.rows * world * args.steps
-    value = rows_total / total_s
-
-    # Integer-VALU roofline of the whole path: VALU wave-instructions per row
-    # of both kernels (rocprofv3 SQ_INSTS_VALU, profiles/) x this run's rows/s
-    # per GPU, against the measured VOP3 issue rate.
-    alu = None
-    if os.path.exists(args.pmc_sq):
-        with open(args.pmc_sq) as f:
-            sq = json.load(f)
-        per = sq["per_kernel"]
-        rpl = float(sq.get("rows_per_launch", 300000))
-        a = per.get("k_shared_secret", {}).get("SQ_INSTS_VALU")
-        bm = per.get("void k_match<false>", {}).get("SQ_INSTS_VALU")
-        if a and bm:
-            wi_per_row = (a + bm) / rpl
-            achieved_wi = wi_per_row * value / world
-            alu = dict(bound="valu", unit="wave-instr/s per GPU", achieved=achieved_wi, peak=VALU_WAVE_INSTR_PEAK,
-                       frac=achieved_wi / VALU_WAVE_INSTR_PEAK, measured_vop3_issue_rate=VOP3_WAVE_INSTR_MEASURED,
-                       frac_of_measured_vop3_rate=achieved_wi / VOP3_WAVE_INSTR_MEASURED,
-                       valu_wave_instr_per_64_rows=dict(k_shared_secret=a / rpl * 64, k_match=bm / rpl * 64),
-                       note="SQ_INSTS_VALU per row from %s (0 labels, 2 outputs/row); peak = nominal VALU "
-                            "issue rate; VOP3 integer ops issue at about half of it on gfx950" % os.path.basename(args.pmc_sq))
+    rows_job = args.rows * (world if args.shard == "weak" else 1)  # rows all ranks scan per step
+    value = rows_job * args.steps / total_s
+    ms_per_step = total_s / args.steps * 1e3
+    rows_gpu_step = rows_job / world
+    step_gbs = bytes_per_row(mean_k) * rows_gpu_step / (ms_per_step * 1e-3) / 1e9
+    launches = tab.nb
+    sq_path = args.pmc_sq or sq_profile_path(args)
+    alu = alu_roofline(sq_path, value / world)
 
     result = dict(
         metric=METRIC, value=value, unit="tx/s", n_gpus=world, steps=args.steps, warmup=args.warmup,
-        ms_per_step=total_s / args.steps * 1e3, higher_is_better=True, scaling="weak", vs_baseline=None,
+        ms_per_step=ms_per_step, higher_is_better=True,
+        scaling="strong" if args.shard == "roundrobin" else "weak", vs_baseline=None,
         dtype="u32", data="synthetic",
-        config=dict(workload="%.1fM-row synthetic tweak table per rank, %d labels, %s outputs/row, "
-                             "batch_size %d, device-resident (BASELINE.json configs[3] shape; each rank "
-                             "scans its own table)" % (args.rows / 1e6, args.labels,
-                                                       ("1..%d (mean %.2f)" % (args.outputs_max, mean_k))
-                                                       if args.outputs_max else str(args.outputs_per_row),
-                                                       args.batch_size),
-                    rows_per_rank=args.rows, batch_size=args.batch_size, labels=args.labels,
+        config=dict(workload="%.1fM-row synthetic tweak table%s, %d labels, %s outputs/row, batch_size %d, "
+                             "device-resident; %s" % (
+                                 args.rows / 1e6, "" if args.shard == "roundrobin" else " per rank", args.labels,
+                                 ("1..%d (mean %.2f)" % (args.outputs_max, mean_k)) if args.outputs_max
+                                 else str(args.outputs_per_row), args.batch_size,
+                                 "batches round-robin over the ranks (BASELINE.json configs[3])"
+                                 if args.shard == "roundrobin" else "every rank scans its own table (weak)"),
+                    rows=args.rows, shard=args.shard, batch_size=args.batch_size, labels=args.labels,
                     output_count=args.output_count, label_negation=args.label_negation,
-                    outputs_per_row=round(mean_k, 3), streams=args.streams, parallelism="dp%d" % world),
+                    outputs_per_row=round(mean_k, 3), fixed_base_bits=args.fb_bits, streams=args.streams,
+                    batches_rank0=launches, parallelism="dp%d" % world),
         roofline=dict(bound="hbm", achieved=achieved_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                       frac=achieved_gbs / HBM_PEAK_GBS, traffic=traffic,
-                      kernel="k_shared_secret", kernel_ms=ka_ms, match_kernel_ms=kb_ms,
+                      kernel="k_shared_secret", kernel_ms=kernel_ms,
+                      kernel_ms_how="stage-A launch alone on the GPU: %d full batches on one stream after the "
+                                    "timed steps, HIP events on that stream" % excl["launches"],
+                      match_kernel_ms=excl["stage_b_ms"],
+                      launch_span_ms_concurrent=float(np.mean(ka)) if ka else None,
+                      match_launch_span_ms_concurrent=float(np.mean(kb)) if kb else None,
                       algorithmic_bytes_per_launch=algo_bytes, rows_per_launch=rows_per_launch,
+                      launches_per_step_rank0=launches, streams=args.streams,
+                      step_achieved=step_gbs, step_frac=step_gbs / HBM_PEAK_GBS,
+                      step_note="whole step: rows x (73 + 8k) B per GPU / ms_per_step",
                       note="integer-VALU-bound path; see alu_roofline"),
         alu_roofline=alu,
-        matches=dict(found=found, flagged=flagged, expected_planted=expected),
+        matches=dict(found=found, flagged=flagged, expected_planted=expected,
+                     label_indices_planted=sorted(tab.planted_labels) if labels else [],
+                     exclusive_pass_matches_equal_planted=excl["matches_equal_planted"]),
         setup_s=round(setup_s, 2),
     )
     if not args.no_layout_probe:
@@ -497,12 +653,21 @@ def main():
                 result["layout_probe"]["traffic_ratio"] = probe_traffic / (result["layout_probe"]["algorithmic_bytes"]
                                                                            / result["layout_probe"]["rows"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(tab, labels, args.cpu_rows, args.cpu_threads, args.output_count,
+        use, visible = host_cores()
+        threads = args.cpu_threads or use
+        result["cpu_baseline"] = cpu_baseline(tab, labels, args.cpu_rows, threads, args.output_count,
                                               args.label_negation)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+        result["cpu_baseline"]["host_cpus_visible"] = visible
     for s in scanners:
         s.close()
+    if rank == 0 and world == 1 and not args.no_e2e and args.output_count == 1 and not args.label_negation:
+        # after the device-resident legs, with this process's GPU work drained
+        torch.cuda.synchronize(device)
+        e2e = e2e_leg(args, mean_k)
+        result["e2e"] = e2e
+        result["e2e_tx_s"] = e2e.get("tx_per_s")
+    if rank == 0:
+        print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

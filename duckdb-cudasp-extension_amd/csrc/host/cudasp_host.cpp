@@ -28,6 +28,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -79,6 +80,8 @@ struct cudasp_tf_global {
   std::atomic<bool> output_thread_claimed{false};
   int num_gpus = 0;
   std::atomic<int> next_gpu_assignment{0};
+  // logical GPU -> HIP device; the identity unless CUDASP_TF_DEVICE_MAP is set
+  std::vector<int> device_map;
 };
 
 // One accumulation/launch buffer set of a thread (double-buffered).
@@ -114,7 +117,8 @@ struct HostSlot {
 struct cudasp_tf_local {
   bool finalized = false;
   bool is_output_thread = false;
-  int assigned_gpu = -1;
+  int assigned_gpu = -1;  // logical GPU (round-robin over num_gpus)
+  int device = -1;        // the HIP device it runs on
   uint32_t cap_rows = 0;
   HostSlot slots[2];
   int cur = 0;
@@ -256,13 +260,13 @@ void ctx_to_local(GpuCtx* c, cudasp_tf_local& l) {
 
 int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
   if (l.scanner) return CUDASP_OK;
-  DeviceSet dg(l.assigned_gpu);
+  DeviceSet dg(l.device);
   const uint32_t cap_rows = (uint32_t)(b.batch_size + CUDASP_TF_VECTOR_SIZE);
   const auto* scan = (const uint8_t*)b.scan_private_key_data.data();
   const auto* spend = (const uint8_t*)b.spend_public_key_data.data();
   const auto* labels = (const uint8_t*)b.label_keys_flat.data();
   const auto nlabels = (uint32_t)b.label_keys_data.size();
-  if (GpuCtx* c = pool_take(l.assigned_gpu, cap_rows)) {
+  if (GpuCtx* c = pool_take(l.device, cap_rows)) {
     int rc = cudasp_scanner_set_keys(c->scanner, scan, spend, labels, nlabels);
     if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(c->scanner, &b.opt);
     if (rc != CUDASP_OK) {
@@ -273,7 +277,7 @@ int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
     return CUDASP_OK;
   }
   l.cap_rows = cap_rows;
-  int rc = cudasp_scanner_create(l.assigned_gpu, scan, spend, labels, nlabels, l.cap_rows, &l.scanner);
+  int rc = cudasp_scanner_create(l.device, scan, spend, labels, nlabels, l.cap_rows, &l.scanner);
   if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(l.scanner, &b.opt);
   if (rc != CUDASP_OK)
     return host_fail(rc, "Failed to create scanner on GPU %d: %s", l.assigned_gpu, cudasp_last_error());
@@ -301,7 +305,7 @@ int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
 void free_local_gpu(cudasp_tf_local& l) {
   if (!l.scanner && !l.stream) return;
   GpuCtx* c = new GpuCtx();
-  c->device = l.assigned_gpu;
+  c->device = l.device;
   c->cap_rows = l.cap_rows;
   c->scanner = l.scanner;
   c->stream = l.stream;
@@ -489,7 +493,7 @@ int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const c
 int harvest(cudasp_tf_global& g, cudasp_tf_local& l, HostSlot& s) {
   if (!s.in_flight) return CUDASP_OK;
   {
-    DeviceSet dg(l.assigned_gpu);
+    DeviceSet dg(l.device);
     HOST_HIP(hipEventSynchronize(s.done));
   }
   s.in_flight = false;
@@ -519,7 +523,7 @@ int launch_batch(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_lo
   HostSlot& s = l.slots[l.cur];
   uint32_t n = s.rows;
   if (n > 0) {
-    DeviceSet dg(l.assigned_gpu);
+    DeviceSet dg(l.device);
     hipStream_t st = l.stream;
     const size_t words = s.n_outputs * out_words(b);
     if (words > s.d_outputs_cap) {
@@ -655,6 +659,28 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
   // Reference: cudaGetDeviceCount, falling back to 1 (:129-132).
   g->num_gpus = cudasp_device_count();
   if (g->num_gpus <= 0) g->num_gpus = 1;
+  for (int d = 0; d < g->num_gpus; d++) g->device_map.push_back(d);
+  // Test hook: CUDASP_TF_DEVICE_MAP="0,0" makes the host see 2 logical GPUs
+  // that both run on device 0, so the num_gpus > 1 round-robin can be
+  // exercised on a one-GPU box.
+  if (const char* m = getenv("CUDASP_TF_DEVICE_MAP")) {
+    std::vector<int> map;
+    const int ndev = cudasp_device_count();
+    for (const char* p = m; *p;) {
+      char* end = nullptr;
+      const long d = strtol(p, &end, 10);
+      if (end == p || d < 0 || (ndev > 0 && d >= ndev)) {
+        delete g;
+        return host_fail(CUDASP_ERR_INVALID_ARG, "CUDASP_TF_DEVICE_MAP: bad device list \"%s\"", m);
+      }
+      map.push_back((int)d);
+      p = *end == ',' ? end + 1 : end;
+    }
+    if (!map.empty()) {
+      g->device_map = map;
+      g->num_gpus = (int)map.size();
+    }
+  }
   *out = g;
   return CUDASP_OK;
 }
@@ -667,7 +693,11 @@ int cudasp_tf_local_init(cudasp_tf_global* g, cudasp_tf_local** out) {
   if (!g || !out) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
   g->currently_adding++;
   auto* l = new cudasp_tf_local();
-  l->assigned_gpu = g->num_gpus > 1 ? g->next_gpu_assignment.fetch_add(1) % g->num_gpus : 0;
+  // Round-robin per thread (src/cudasp_extension.cu:523-529).
+  l->assigned_gpu = g->num_gpus > 1 ? (int)cudasp_assign_gpu((uint64_t)g->next_gpu_assignment.fetch_add(1),
+                                                             (uint32_t)g->num_gpus)
+                                    : 0;
+  l->device = g->device_map.empty() ? l->assigned_gpu : g->device_map[l->assigned_gpu];
   *out = l;
   return CUDASP_OK;
 }
@@ -679,6 +709,12 @@ void cudasp_tf_local_free(cudasp_tf_local* l) {
 }
 
 int cudasp_tf_local_gpu(const cudasp_tf_local* l) { return l ? l->assigned_gpu : -1; }
+
+int cudasp_tf_local_device(const cudasp_tf_local* l) { return l ? l->device : -1; }
+
+uint32_t cudasp_assign_gpu(uint64_t ordinal, uint32_t num_gpus) {
+  return num_gpus > 1 ? (uint32_t)(ordinal % num_gpus) : 0u;
+}
 
 void cudasp_tf_release_pool(void) {
   std::vector<GpuCtx*> all;

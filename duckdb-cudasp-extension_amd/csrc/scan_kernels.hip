@@ -4,8 +4,9 @@
 // Kernel pipeline for one batch of n rows (all device-resident):
 //   k_shared_secret   stage A of scan_rows.hpp: reads tweak columns (8 x n u32
 //                     each, column-major), writes t (8 x n u32).
-//   k_match           stage B: reads t, gathers from the 32 MiB fixed-base
-//                     table, compares with the outputs CSR, writes one flag per
+//   k_match           stage B: reads t, gathers from the per-device fixed-base
+//                     table (22-bit windows: 1.5 GiB, 26-bit: 21.5 GB; a
+//                     per-scanner choice, scan_rows.hpp), compares with the outputs CSR, writes one flag per
 //                     row and (optionally) the compacted row indices via a
 //                     per-wavefront ballot + one atomic per wave.
 // Replaces the reference's ec_pmul + serialize + hash + host round trip +
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
 // consecutive rows of full waves.  n counts virtual rows kk * n_rows + row
 // (K output indices per input row; n == n_rows when K = 1): t, flags and
 // values are indexed by the virtual row, the outputs lists by the input row.
-template <bool VALUES, int R>
+template <bool VALUES, int R, int FBB>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t* __restrict__ t_in, uint32_t n,
                                                  uint32_t n_rows,
                                                  const uint32_t* __restrict__ fb, ScanConsts k,
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
 #pragma unroll
         for (int w = 0; w < 8; w++) t[w] = t_in[(size_t)w * n + row];
         gej P;
-        row_match_point(P, t, fb, k);
+        row_match_point<FBB>(P, t, fb, k);
         pend_store(sc, PB, j, P);
         count = j + 1;
       }
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
         const uint32_t orow = n == n_rows ? row : row % n_rows;
         uint32_t off = VALUES ? 0u : offs[orow];
         uint32_t len = VALUES ? 0u : lens[orow];
-        hit = row_match(t, fb, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
+        hit = row_match<FBB>(t, fb, k, labels, outputs, off, len, sc, VALUES ? values + row : nullptr, n);
         if (!VALUES) flags[row] = hit ? 1 : 0;
       } else if (j < count) {
         hit = (hits >> j) & 1u;
@@ -281,11 +282,13 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_fb_build(const uint32_t* __restrict__ bases,
-                                                    uint32_t* __restrict__ table) {
+// One entry per thread of a table with `windows` windows of `entries` odd
+// multiples each (the width's FbWidth), from the windows' bases.
+__global__ __launch_bounds__(BLOCK) void k_fb_build(const uint32_t* __restrict__ bases, uint32_t windows,
+                                                    uint32_t entries, uint32_t* __restrict__ table) {
   const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (uint32_t)(FB_WINDOWS * FB_ENTRIES)) return;
-  const uint32_t window = idx / FB_ENTRIES, j = idx % FB_ENTRIES;
+  if (idx >= windows * entries) return;
+  const uint32_t window = idx / entries, j = idx % entries;
   ge Q;
   ge_from_words(Q, bases + window * 16);
   uint32_t out[16];
@@ -384,6 +387,7 @@ __device__ __forceinline__ void add_index_mod_n(uint32_t s[8], const uint32_t s0
   }
 }
 
+template <int FBB>
 __global__ __launch_bounds__(BLOCK) void k_synth_tweaks(SynthConsts c, uint64_t first, uint32_t n,
                                                         const uint32_t* __restrict__ fb, uint32_t* __restrict__ x,
                                                         uint32_t* __restrict__ y) {
@@ -392,7 +396,7 @@ __global__ __launch_bounds__(BLOCK) void k_synth_tweaks(SynthConsts c, uint64_t 
     uint32_t s[8];
     add_index_mod_n(s, c.s0, first + row);
     gej R;
-    fixed_base_mul(R, s, fb);
+    fixed_base_mul<FBB>(R, s, fb);
     fe zi;
     fe_inv(zi, R.z);
     ge A;
@@ -493,39 +497,81 @@ __global__ __launch_bounds__(BLOCK) void k_debug_field_ops(int op, const uint32_
 namespace {
 
 // ------------------------------------------------ per-device fixed-base table
+// One table per (device, window width), built on first use and kept for the
+// process.  Each table has its own once-guard, so the first scanners of
+// several devices (one DuckDB executor thread per GPU) build their tables in
+// parallel; the map itself is only locked for the lookup.
 struct DeviceTable {
+  std::mutex mu;  // held while building
   uint32_t* table = nullptr;
 };
-std::mutex g_table_mutex;
-std::map<int, DeviceTable> g_tables;
+std::mutex g_table_map_mutex;
+std::map<std::pair<int, int>, DeviceTable> g_tables;
 
-int ensure_device_table(int device, const uint32_t** out) {
-  std::lock_guard<std::mutex> lock(g_table_mutex);
-  auto it = g_tables.find(device);
-  if (it != g_tables.end()) {
-    *out = it->second.table;
+// Prebuilt widths (k_match / k_synth_tweaks instances).
+bool fb_bits_supported(int bits) { return bits == 22 || bits == 26; }
+
+int g_default_fb_bits = 0;  // 0: not read yet
+std::once_flag g_default_fb_once;
+
+// The process default width: CUDASP_FB_BITS (22 or 26) from the environment,
+// else the build's FB_BITS.
+int default_fb_bits() {
+  std::call_once(g_default_fb_once, [] {
+    g_default_fb_bits = FB_BITS;
+    if (const char* e = getenv("CUDASP_FB_BITS")) {
+      const int b = atoi(e);
+      if (fb_bits_supported(b)) g_default_fb_bits = b;
+    }
+  });
+  return g_default_fb_bits;
+}
+
+size_t fb_table_bytes(int bits) {
+  const size_t windows = (256 + bits - 1) / bits;
+  return windows * ((size_t)1 << (bits - 1)) * FB_WORDS * 4;
+}
+
+int ensure_device_table(int device, int bits, const uint32_t** out) {
+  if (!fb_bits_supported(bits))
+    return set_error(CUDASP_ERR_INVALID_ARG, "fixed-base window width %d not supported (22 or 26)", bits);
+  DeviceTable* dt;
+  {
+    std::lock_guard<std::mutex> lock(g_table_map_mutex);
+    dt = &g_tables[std::make_pair(device, bits)];  // std::map: stable address
+  }
+  std::lock_guard<std::mutex> lock(dt->mu);
+  if (dt->table) {
+    *out = dt->table;
     return CUDASP_OK;
   }
-  std::vector<uint32_t> bases = fb_window_bases();
+  const uint32_t windows = (256 + bits - 1) / bits, entries = 1u << (bits - 1);
+  std::vector<uint32_t> bases = fb_window_bases(bits);
   uint32_t* d_bases = nullptr;
   uint32_t* d_table = nullptr;
   HIP_TRY(hipMalloc(&d_bases, bases.size() * 4));
-  const size_t table_bytes = (size_t)FB_WINDOWS * FB_ENTRIES * FB_WORDS * 4;
+  const size_t table_bytes = fb_table_bytes(bits);
   if (hipMalloc(&d_table, table_bytes) != hipSuccess) {
     (void)hipGetLastError();
     (void)hipFree(d_bases);
     return set_error(CUDASP_ERR_HIP,
                      "device %d: cannot allocate the %.1f GB fixed-base table (%d-bit windows); free device memory "
-                     "or build with a smaller CUDASP_FB_BITS (22: 1.5 GiB, 16: 32 MiB)",
-                     device, table_bytes / 1e9, FB_BITS);
+                     "or choose 22-bit windows (1.5 GiB; CUDASP_FB_BITS=22)",
+                     device, table_bytes / 1e9, bits);
   }
-  HIP_TRY(hipMemcpy(d_bases, bases.data(), bases.size() * 4, hipMemcpyHostToDevice));
-  const uint32_t total = FB_WINDOWS * FB_ENTRIES;
-  hipLaunchKernelGGL(k_fb_build, dim3((total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, 0, d_bases, d_table);
+  // The build runs on a stream of its own, so other threads' work on the
+  // device is not serialized behind it (no device-wide synchronize).
+  hipStream_t st = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  HIP_TRY(hipMemcpyAsync(d_bases, bases.data(), bases.size() * 4, hipMemcpyHostToDevice, st));
+  const uint32_t total = windows * entries;
+  hipLaunchKernelGGL(k_fb_build, dim3((total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, d_bases, windows, entries,
+                     d_table);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipStreamSynchronize(st));
+  HIP_TRY(hipStreamDestroy(st));
   HIP_TRY(hipFree(d_bases));
-  g_tables[device].table = d_table;
+  dt->table = d_table;
   *out = d_table;
   return CUDASP_OK;
 }
@@ -538,6 +584,7 @@ struct cudasp_scanner {
   hipStream_t stream = nullptr;
   ScanConsts consts{};
   const uint32_t* d_fb = nullptr;
+  int fb_bits = 0;  // window width of d_fb (22 or 26)
   int8_t* d_naf = nullptr;
   uint32_t* d_labels = nullptr;
   uint32_t label_count = 0;  // label keys in d_labels (x2 with label_negation)
@@ -669,8 +716,11 @@ int launch_match(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t
   const uint32_t N = K * n;
   const int r = rows_b_for(s, N);
   const uint32_t blocks_b = grid_b(s, N, r);
-  auto kv = r == ROWS_B ? k_match<true, ROWS_B> : k_match<true, 2>;
-  auto kf = r == ROWS_B ? k_match<false, ROWS_B> : k_match<false, 2>;
+  const bool w26 = s->fb_bits == 26;
+  auto kv = r == ROWS_B ? (w26 ? k_match<true, ROWS_B, 26> : k_match<true, ROWS_B, 22>)
+                        : (w26 ? k_match<true, 2, 26> : k_match<true, 2, 22>);
+  auto kf = r == ROWS_B ? (w26 ? k_match<false, ROWS_B, 26> : k_match<false, ROWS_B, 22>)
+                        : (w26 ? k_match<false, 2, 26> : k_match<false, 2, 22>);
   if (values) {
     hipLaunchKernelGGL(kv, dim3(blocks_b), dim3(BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels, nullptr,
                        nullptr, nullptr, s->d_lscratch, nullptr, nullptr, nullptr, values);
@@ -750,7 +800,8 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
 
   // --- device state --------------------------------------------------------
   DeviceGuard g(device);
-  int rc = ensure_device_table(device, &s->d_fb);
+  s->fb_bits = default_fb_bits();
+  int rc = ensure_device_table(device, s->fb_bits, &s->d_fb);
   if (rc != CUDASP_OK) {
     delete s;
     return rc;
@@ -904,6 +955,27 @@ int cudasp_scanner_set_options(cudasp_scanner* s, const cudasp_scan_options* opt
   return rc;
 }
 
+int cudasp_default_fixed_base_bits(void) { return default_fb_bits(); }
+
+uint64_t cudasp_fixed_base_table_bytes(int bits) { return fb_bits_supported(bits) ? (uint64_t)fb_table_bytes(bits) : 0; }
+
+int cudasp_scanner_set_fixed_base_bits(cudasp_scanner* s, int bits) {
+  g_last_error.clear();
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  if (bits == 0) bits = default_fb_bits();
+  if (bits == s->fb_bits) return CUDASP_OK;
+  DeviceGuard g(s->device);
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  const uint32_t* fb = nullptr;
+  int rc = ensure_device_table(s->device, bits, &fb);
+  if (rc != CUDASP_OK) return rc;
+  s->d_fb = fb;
+  s->fb_bits = bits;
+  return CUDASP_OK;
+}
+
+int cudasp_scanner_fixed_base_bits(const cudasp_scanner* s) { return s ? s->fb_bits : 0; }
+
 int cudasp_scanner_sync(cudasp_scanner* s) {
   if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
   DeviceGuard g(s->device);
@@ -1037,15 +1109,16 @@ int cudasp_synth_tweak_columns(int device, const uint8_t s0_le[32], uint64_t fir
   if (!s0_le || !d_x || !d_y) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
   DeviceGuard g(device);
   const uint32_t* fb = nullptr;
-  int rc = ensure_device_table(device, &fb);
+  const int bits = default_fb_bits();
+  int rc = ensure_device_table(device, bits, &fb);
   if (rc != CUDASP_OK) return rc;
   SynthConsts c;
   host::Big<8> s0 = host::big_zero<8>();
   for (int i = 0; i < 32; i++) s0.w[i / 4] |= (uint32_t)s0_le[i] << (8 * (i % 4));
   s0 = host::scalar_reduce(s0);
   for (int i = 0; i < 8; i++) c.s0[i] = s0.w[i];
-  hipLaunchKernelGGL(k_synth_tweaks, dim3(grid_for(n)), dim3(BLOCK), 0, plain_stream(stream), c, first_index, n, fb,
-                     d_x, d_y);
+  hipLaunchKernelGGL(bits == 26 ? k_synth_tweaks<26> : k_synth_tweaks<22>, dim3(grid_for(n)), dim3(BLOCK), 0,
+                     plain_stream(stream), c, first_index, n, fb, d_x, d_y);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
 }

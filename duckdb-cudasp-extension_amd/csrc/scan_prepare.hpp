@@ -95,25 +95,6 @@ HPoint hp_generator() {
   return hp_from_bytes(gbytes);
 }
 
-// 2^(FB_BITS i) G for i = 0..FB_WINDOWS (the bases of the fixed-base
-// windows, and one more), computed once.
-struct GenPowers {
-  HPoint q[FB_WINDOWS + 1];
-  GenPowers() {
-    HPoint cur = hp_generator();
-    for (int i = 0; i <= FB_WINDOWS; i++) {
-      q[i] = cur;
-      if (i == FB_WINDOWS) break;
-      for (int d = 0; d < FB_BITS; d++) cur = hp_add(cur, cur);
-    }
-  }
-};
-
-const GenPowers& gen_powers() {
-  static GenPowers g;
-  return g;
-}
-
 void sha256_bytes(uint8_t out[32], const uint8_t* msg, size_t len) {
   uint32_t s[8];
   sha256_init(s);
@@ -153,11 +134,16 @@ void bip352_midstate(uint32_t mid[8]) {
 }
 
 
-// Fixed-base window bases 2^(16 i) G, i = 0..15, as 16 normalized words each.
-inline std::vector<uint32_t> fb_window_bases() {
-  const GenPowers& gp = gen_powers();
-  std::vector<uint32_t> bases(FB_WINDOWS * 16);
-  for (int i = 0; i < FB_WINDOWS; i++) hp_words(&bases[i * 16], gp.q[i]);
+// Fixed-base window bases 2^(bits i) G, i = 0 .. windows - 1, as 16
+// normalized words each (host, once per table build).
+inline std::vector<uint32_t> fb_window_bases(int bits = FB_BITS) {
+  const int windows = (256 + bits - 1) / bits;
+  std::vector<uint32_t> bases((size_t)windows * 16);
+  HPoint cur = hp_generator();
+  for (int i = 0; i < windows; i++) {
+    hp_words(&bases[(size_t)i * 16], cur);
+    for (int d = 0; d < bits; d++) cur = hp_add(cur, cur);
+  }
   return bases;
 }
 

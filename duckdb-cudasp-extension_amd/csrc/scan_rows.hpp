@@ -18,21 +18,29 @@ namespace cudasp {
 // Variable-base window: odd multiples 1,3,...,15 of T (width-5 NAF digits).
 constexpr int VB_ENTRIES = 8;
 constexpr int NAF_MAX = 136;
-// Fixed-base table: FB_WINDOWS windows of FB_BITS-bit odd digits, each with
-// FB_ENTRIES odd multiples (2j+1) 2^(FB_BITS i) G, 64 bytes per entry.  The odd
-// representative t' of t mod n is sum_i d_i 2^(FB_BITS i) (fixed_base_mul), so
-// P0 = t G costs FB_WINDOWS gathers and FB_WINDOWS - 1 mixed additions.
-// Default 26 bits: 10 windows, 21.5 GB per device (22 bits: 12 windows, 1.5 GiB; 16 bits:
-// 16 windows, 32 MiB).  Chosen by A/B (profiles/r01_stage_ab_fb_windows26.txt):
-// 22 -> 24 -> 26 bits measured 158.4 -> 160.2 -> 160.9 M tx/s, stage B
-// -13%, for a 0.9 s one-time build per device; MI355X has 288 GB.
+// Fixed-base table: W windows of w-bit odd digits, each with 2^(w-1) odd
+// multiples (2j+1) 2^(w i) G, 64 bytes per entry.  The odd representative t'
+// of t mod n is sum_i d_i 2^(w i) (fixed_base_mul), so P0 = t G costs W
+// gathers and W - 1 mixed additions.  The width is a per-scanner runtime
+// choice among the prebuilt widths (FbWidth below; cudasp_scanner_set_fixed_base_bits):
+//   22 bits: 12 windows, 1.5 GiB per device  (the default, CUDASP_FB_BITS)
+//   26 bits: 10 windows, 21.5 GB per device  (~1.5% faster end to end,
+//            profiles/r01_stage_ab_fb_windows26.txt: 22 -> 24 -> 26 bits
+//            158.4 -> 160.2 -> 160.9 M tx/s, stage B -13%)
+// FB_BITS / FB_WINDOWS / FB_ENTRIES name the default width.
 #ifndef CUDASP_FB_BITS
-#define CUDASP_FB_BITS 26
+#define CUDASP_FB_BITS 22
 #endif
+template <int BITS>
+struct FbWidth {
+  static_assert(BITS >= 8 && BITS <= 27, "fixed-base window width");
+  static constexpr int WINDOWS = (256 + BITS - 1) / BITS;
+  static constexpr uint32_t ENTRIES = 1u << (BITS - 1);
+};
 constexpr int FB_BITS = CUDASP_FB_BITS;
-static_assert(FB_BITS >= 8 && FB_BITS <= 27, "fixed-base window width");
-constexpr int FB_WINDOWS = (256 + FB_BITS - 1) / FB_BITS;
-constexpr uint32_t FB_ENTRIES = 1u << (FB_BITS - 1);
+static_assert(FB_BITS == 22 || FB_BITS == 26, "default fixed-base width must be a prebuilt one (22 or 26)");
+constexpr int FB_WINDOWS = FbWidth<FB_BITS>::WINDOWS;
+constexpr uint32_t FB_ENTRIES = FbWidth<FB_BITS>::ENTRIES;
 constexpr int FB_WORDS = 16;
 
 // Per-query constants, passed to the kernels by value.
@@ -419,12 +427,14 @@ CUDASP_HD bool outputs_match(const ScanConsts& k, const int64_t* outputs, uint32
 // no x coordinate exists, the row cannot match through it.
 constexpr int64_t LABEL_INFINITY = (int64_t)0x8000000000000000ull;
 
-// Entry for the digit d = 2 b + 1 - 2^FB_BITS of window `window` (b = the
-// window's FB_BITS bits): |d| = 2j + 1, negated when b < 2^(FB_BITS-1).
+// Entry for the digit d = 2 b + 1 - 2^BITS of window `window` (b = the
+// window's BITS bits): |d| = 2j + 1, negated when b < 2^(BITS-1).
+template <int BITS = FB_BITS>
 CUDASP_HD void fb_entry(ge& P, const uint32_t* table, int window, uint32_t bits) {
-  bool neg = (bits & FB_ENTRIES) == 0;
-  uint32_t j = (bits ^ (neg ? FB_ENTRIES - 1 : 0u)) & (FB_ENTRIES - 1);
-  const uint32_t* e = table + ((size_t)window * FB_ENTRIES + j) * FB_WORDS;
+  constexpr uint32_t ENTRIES = FbWidth<BITS>::ENTRIES;
+  bool neg = (bits & ENTRIES) == 0;
+  uint32_t j = (bits ^ (neg ? ENTRIES - 1 : 0u)) & (ENTRIES - 1);
+  const uint32_t* e = table + ((size_t)window * ENTRIES + j) * FB_WORDS;
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t w[16];
   const uint4* e4 = reinterpret_cast<const uint4*>(e);
@@ -479,14 +489,17 @@ CUDASP_HD bool scalar_odd_rep(uint32_t t[8], const uint32_t in[8]) {
 
 // P = t*G (Jacobian) from the fixed-base table.  t: 8 LE words, any 256-bit
 // value (not reduced mod n, like the reference, src/cudasp_gpu.cu:862-877;
-// n*G = O makes that irrelevant).  FB_WINDOWS gathers and FB_WINDOWS - 1 mixed
-// additions, no constant term.
+// n*G = O makes that irrelevant).  W gathers and W - 1 mixed additions (W the
+// windows of the BITS-bit table), no constant term.
+template <int BITS = FB_BITS>
 CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb_table) {
+  constexpr int WINDOWS = FbWidth<BITS>::WINDOWS;
+  constexpr uint32_t ENTRIES = FbWidth<BITS>::ENTRIES;
   uint32_t t[9];
   const bool negate = scalar_odd_rep(t, t_in);
   t[8] = 0;
   // odd t' < n = 1 + sum_{i<W} 2 b_i 2^(w i), b_i = bits [w i + 1, w i + w] of
-  // t' (w = FB_BITS, W = FB_WINDOWS), written with signed odd digits
+  // t' (w = BITS, W = WINDOWS), written with signed odd digits
   // d_i = 2 b_i + 1 - 2^w below the top window and the positive top digit
   // d_(W-1) = 2 b_(W-1) + 1: the (1 - 2^w) 2^(w i) terms telescope to
   // 1 - 2^(w (W-1)), which the top digit's + 2^(w (W-1)) cancels, so
@@ -496,16 +509,16 @@ CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb
   // instruction cache), so t is consumed by shifting instead of indexing a
   // register array with the loop counter (that would spill to scratch).
 #pragma unroll 1
-  for (int i = 0; i < FB_WINDOWS; i++) {
-    uint32_t bits = (t[0] >> 1) & ((FB_ENTRIES << 1) - 1);
+  for (int i = 0; i < WINDOWS; i++) {
+    uint32_t bits = (t[0] >> 1) & ((ENTRIES << 1) - 1);
 #pragma unroll
-    for (int q = 0; q < 8; q++) t[q] = (t[q] >> FB_BITS) | (t[q + 1] << (32 - FB_BITS));
-    t[8] >>= FB_BITS;
+    for (int q = 0; q < 8; q++) t[q] = (t[q] >> BITS) | (t[q + 1] << (32 - BITS));
+    t[8] >>= BITS;
     ge P;
-    if (i < FB_WINDOWS - 1)
-      fb_entry(P, fb_table, i, bits);
+    if (i < WINDOWS - 1)
+      fb_entry<BITS>(P, fb_table, i, bits);
     else
-      fb_entry(P, fb_table, i, bits | FB_ENTRIES);  // positive digit 2 bits + 1: entry bits
+      fb_entry<BITS>(P, fb_table, i, bits | ENTRIES);  // positive digit 2 bits + 1: entry bits
     if (i == 0) {
       gej_set_ge(R, P);
     } else {
@@ -521,8 +534,9 @@ CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb
 }
 
 // Stage B, first half: F = t G + B as a Jacobian point.
+template <int BITS = FB_BITS>
 CUDASP_HD void row_match_point(gej& R, const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k) {
-  fixed_base_mul(R, t_in, fb_table);  // P0 = t*G
+  fixed_base_mul<BITS>(R, t_in, fb_table);  // P0 = t*G
   // B is added on its own (not folded into the table), so F = P0 + B is the same
   // single chord addition as the reference's even for a spend key that is not
   // on the curve.
@@ -702,19 +716,20 @@ CUDASP_HD uint32_t match_labels_rows(const ScanConsts& k, const uint32_t* labels
 }
 
 // Stage B for one row (one inversion per row).
+template <int BITS = FB_BITS>
 CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k,
                          const uint32_t* labels, const int64_t* outputs, uint32_t off, uint32_t len,
                          const Scratch& sc, int64_t* values, uint32_t vstride) {
   gej R;
-  row_match_point(R, t_in, fb_table, k);
+  row_match_point<BITS>(R, t_in, fb_table, k);
   fe zi;
   fe_inv(zi, R.z);
   return row_match_finish(R, zi, k, labels, outputs, off, len, sc, values, vstride);
 }
 
-// Fixed-base table entry (2j+1) * 2^(16 window) * G from the window base Q.
+// Fixed-base table entry (2j+1) Q of a window with base Q = 2^(w window) G.
 CUDASP_HD void fb_build_entry(uint32_t out[16], const ge& Q, uint32_t j) {
-  uint32_t m = 2 * j + 1;  // 1 .. 2^FB_BITS - 1
+  uint32_t m = 2 * j + 1;  // 1 .. 2^w - 1
   int top = 31 - __builtin_clz(m);
   gej R;
   gej_set_ge(R, Q);

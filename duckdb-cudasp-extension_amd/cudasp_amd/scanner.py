@@ -66,6 +66,16 @@ class Scanner:
         self.full_x = bool(full_x)
         self._t = None
 
+    def set_fixed_base_bits(self, bits=0):
+        """Fixed-base window width of stage B (22 or 26; 0 = the process
+        default, cudasp_default_fixed_base_bits).  Same results at every
+        width; builds the device's table for that width on first use."""
+        _native.check(self._lib.cudasp_scanner_set_fixed_base_bits(self._h, int(bits)))
+
+    @property
+    def fixed_base_bits(self):
+        return int(self._lib.cudasp_scanner_fixed_base_bits(self._h))
+
     @property
     def value_rows(self):
         """Compare values per virtual row: the base value and one per label

@@ -103,6 +103,8 @@ _HOST_SIGNATURES = {
     "cudasp_tf_local_init": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     "cudasp_tf_local_free": (None, [_P]),
     "cudasp_tf_local_gpu": (ctypes.c_int, [_P]),
+    "cudasp_tf_local_device": (ctypes.c_int, [_P]),
+    "cudasp_assign_gpu": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32]),
     "cudasp_tf_release_pool": (None, []),
     "cudasp_tf_pool_size": (ctypes.c_uint32, []),
     "cudasp_tf_function": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Chunk)]),
@@ -236,6 +238,14 @@ def _make_chunk(rows, full_x=False):
     return keep, c
 
 
+def assign_gpu(ordinal, num_gpus):
+    """The product's multi-GPU work assignment (cudasp_assign_gpu,
+    include/cudasp_host.h): unit `ordinal` -> GPU ordinal mod num_gpus, as
+    the host assigns executor threads (src/cudasp_extension.cu:523-529) and
+    bench.py assigns the batches of one table to ranks.  Host-only."""
+    return int(_lib().cudasp_assign_gpu(int(ordinal), int(num_gpus)))
+
+
 def pool_size():
     """GPU contexts parked in the host's cross-query pool (cudasp_tf_pool_size)."""
     return int(_lib().cudasp_tf_pool_size())
@@ -247,14 +257,15 @@ def release_pool():
 
 
 def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size=None, threads=1,
-                chunk_rows=VECTOR_SIZE, output_count=None, label_negation=None, full_x=None):
+                chunk_rows=VECTOR_SIZE, output_count=None, label_negation=None, full_x=None, assignments=None):
     """Run the table function over `rows` with `threads` executor threads.
     Chunks are dealt round-robin to the threads, as DuckDB's parallel scan
     would hand out morsels; each thread gets its own local state (and GPU,
     round-robin, CudaspScanLocalInit :523-529).  output_count /
     label_negation / full_x: the protocol-variant named parameters
     (cudasp_tf_bind_options); with full_x the outputs are lists of 32-byte
-    x-only keys."""
+    x-only keys.  assignments: if a list, receives (logical GPU, HIP device)
+    of each thread's local state."""
     lib = _lib()
     bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size, output_count=output_count,
                       label_negation=label_negation, full_x=full_x)
@@ -266,6 +277,8 @@ def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size
             l = _P()
             _native.check(lib.cudasp_tf_local_init(g, ctypes.byref(l)))
             locals_.append(l)
+            if assignments is not None:
+                assignments.append((int(lib.cudasp_tf_local_gpu(l)), int(lib.cudasp_tf_local_device(l))))
         chunks = [rows[i:i + chunk_rows] for i in range(0, len(rows), chunk_rows)]
         errors = []
         results = []

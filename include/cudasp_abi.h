@@ -61,7 +61,10 @@ typedef struct cudasp_scanner cudasp_scanner;
 /* Create a scanner on `device` for one query's keys.  label_keys holds
  * label_count 64-byte keys back to back (may be NULL when label_count is 0).
  * max_rows bounds the rows of any later batch.  The first scanner on a device
- * also builds that device's fixed-base table (32 MiB, kept for the process).
+ * also builds that device's fixed-base table for the default window width
+ * (cudasp_default_fixed_base_bits: 22-bit windows, 1.5 GiB, unless the
+ * environment sets CUDASP_FB_BITS=26, 21.5 GB), kept for the process; tables
+ * of different devices build in parallel.
  * Fails with CUDASP_ERR_INVALID_ARG for a scan key that is 0 mod n. */
 int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const uint8_t spend_public_key[64],
                           const uint8_t* label_keys, uint32_t label_count, uint32_t max_rows,
@@ -74,6 +77,19 @@ void cudasp_scanner_destroy(cudasp_scanner* s);
  * solver state per batch, src/cudasp_gpu.cu:445-669). */
 int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32],
                             const uint8_t spend_public_key[64], const uint8_t* label_keys, uint32_t label_count);
+
+/* Fixed-base window width of stage B's t*G (the reference's gECC d_mul_table,
+ * src/cudasp_gpu.cu:317-354).  Prebuilt widths: 22 bits (12 windows, 1.5 GiB
+ * table per device) and 26 bits (10 windows, 21.5 GB; one mixed addition
+ * fewer per window saved, ~1.5% faster end to end).  Same results at every
+ * width.  The process default is CUDASP_FB_BITS from the environment (22 or
+ * 26), else 22.  set_fixed_base_bits (0 = the default) switches a scanner's
+ * table, building it on first use; not concurrent with work in flight on the
+ * scanner.  table_bytes returns 0 for an unsupported width. */
+int cudasp_default_fixed_base_bits(void);
+uint64_t cudasp_fixed_base_table_bytes(int bits);
+int cudasp_scanner_set_fixed_base_bits(cudasp_scanner* s, int bits);
+int cudasp_scanner_fixed_base_bits(const cudasp_scanner* s);
 
 /* Protocol variants, off by default.  With the
  * defaults a scanner computes exactly the reference's flags.

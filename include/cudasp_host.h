@@ -78,10 +78,18 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out);
 void cudasp_tf_global_free(cudasp_tf_global* g);
 int cudasp_tf_num_gpus(const cudasp_tf_global* g);
 
-/* Local state (one per executor thread): round-robin GPU. */
+/* Local state (one per executor thread): round-robin GPU.  local_gpu is the
+ * logical GPU index (0 .. num_gpus-1), local_device the HIP device it runs on
+ * (the same unless the test hook CUDASP_TF_DEVICE_MAP="d0,d1,..." maps the
+ * logical GPUs to devices, e.g. "0,0" for two logical GPUs on one card). */
 int cudasp_tf_local_init(cudasp_tf_global* g, cudasp_tf_local** out);
 void cudasp_tf_local_free(cudasp_tf_local* l);
 int cudasp_tf_local_gpu(const cudasp_tf_local* l);
+int cudasp_tf_local_device(const cudasp_tf_local* l);
+/* The work assignment used for multi-GPU sharding: unit `ordinal` (an
+ * executor thread in the host, src/cudasp_extension.cu:523-529; a batch of
+ * the table in bench.py) goes to GPU ordinal mod num_gpus.  Host-only. */
+uint32_t cudasp_assign_gpu(uint64_t ordinal, uint32_t num_gpus);
 /* The GPU state of a freed local state (scanner, stream, pinned and device
  * batch buffers) is kept in a process-wide pool (at most 64 entries) and
  * reused by later queries with the same device and batch capacity.

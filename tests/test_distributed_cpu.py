@@ -1,10 +1,17 @@
-"""CPU, world_size 2 over gloo: the benchmark's sharding and cross-rank
-reduction (bench.shard_first_row / bench.aggregate), with the C oracle standing
-in for the GPU scan of each rank's shard.  The union of the shards must equal a
-single-process scan of the whole table, and the job time must be the max."""
-import hashlib
+"""CPU, world_size 2 over gloo: the benchmark's multi-GPU sharding and
+cross-rank reduction, with the C oracle standing in for each rank's GPU scan.
+
+* roundrobin (BASELINE configs[3], the N > 1 headline): ONE table cut into
+  batch_size-row batches, batch b scanned by rank cudasp_assign_gpu(b, N) --
+  the product's own assignment function from libcudasp_amd.so (host-only
+  code, the round-robin of src/cudasp_extension.cu:523-529).  The ranks'
+  batches must partition the table, and the union of their matches must equal
+  a single-process scan of the whole table.
+* weak: every rank scans its own table (bench.shard_first_row).
+The job time is the max over ranks, match counts the sum (bench.aggregate)."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -12,40 +19,56 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
-ROWS_PER_RANK = 24
+PKG = os.path.join(ROOT, "duckdb-cudasp-extension_amd")
+ROWS = 46          # global table (roundrobin): 6 batches of 8, the last one short
+BATCH = 8
+ROWS_PER_RANK = 24  # weak
 
 
-def _table(first, rows):
-    import sys
-    sys.path.insert(0, ROOT)
+def _paths():
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _scan_rows(global_rows):
+    """Oracle scan of the given global row indices of the synthetic table:
+    every 5th global row carries its true value.  -> (flags, planted)."""
+    _paths()
     import bench
     from oracle import oracle
     s0 = bench.synth_s0()
-    tweaks = np.frombuffer(b"".join(oracle.synth_tweak(s0, first + i) for i in range(rows)),
-                           dtype=np.uint8).reshape(rows, 64)
+    n = len(global_rows)
+    if n == 0:
+        return np.zeros(0, dtype=np.uint8), 0
+    tweaks = np.frombuffer(b"".join(oracle.synth_tweak(s0, g) for g in global_rows),
+                           dtype=np.uint8).reshape(n, 64)
     _, vals = oracle.scan(bench.SCAN_KEY, bench.SPEND_KEY, [], tweaks, want_values=True)
-    outs = np.array([[i * 7 + 1, 0] for i in range(rows)], dtype=np.int64)
-    planted = [i for i in range(rows) if (first + i) % 5 == 0]
+    outs = np.array([[g * 7 + 1, 0] for g in global_rows], dtype=np.int64)
+    planted = [i for i, g in enumerate(global_rows) if g % 5 == 0]
     for i in planted:
         outs[i, 1] = vals[i, 0]
     flags, _ = oracle.scan(bench.SCAN_KEY, bench.SPEND_KEY, [], tweaks, outs.reshape(-1),
-                           np.arange(rows, dtype=np.uint32) * 2, np.full(rows, 2, dtype=np.uint32))
+                           np.arange(n, dtype=np.uint32) * 2, np.full(n, 2, dtype=np.uint32))
     return flags, len(planted)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, shard, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    import sys
-    sys.path.insert(0, ROOT)
+    _paths()
     import bench
-    first = bench.shard_first_row(rank, ROWS_PER_RANK)
-    flags, planted = _table(first, ROWS_PER_RANK)
+    from cudasp_amd import assign_gpu
+    rows = ROWS if shard == "roundrobin" else ROWS_PER_RANK
+    batches = bench.rank_batches(shard, rows, BATCH, rank, world, assign_gpu)
+    global_rows = [g0 + i for g0, m in batches for i in range(m)]
+    flags, planted = _scan_rows(global_rows)
     t, found, flagged, expected = bench.aggregate(world, "gloo", 1.0 + rank, int(flags.sum()), int(flags.sum()),
                                                   planted)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, global_rows)
     if rank == 0:
-        q.put((t, found, flagged, expected))
+        q.put((t, found, flagged, expected, gathered))
     dist.destroy_process_group()
 
 
@@ -57,19 +80,58 @@ def _free_port():
     return p
 
 
-def test_two_rank_shards_equal_single_scan():
-    world = 2
+def _run(shard, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shard, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs)
-    t, found, flagged, expected = q.get(timeout=5)
-    flags_all, planted_all = _table(0, world * ROWS_PER_RANK)
+    return q.get(timeout=5)
+
+
+def test_assignment_is_round_robin():
+    _paths()
+    from cudasp_amd import assign_gpu
+    assert [assign_gpu(b, 3) for b in range(7)] == [0, 1, 2, 0, 1, 2, 0]
+    assert [assign_gpu(b, 1) for b in range(3)] == [0, 0, 0]
+    assert assign_gpu(2**40 + 5, 8) == 5
+
+
+def test_two_rank_roundrobin_equals_single_scan():
+    t, found, flagged, expected, gathered = _run("roundrobin")
+    # the ranks' batches partition the one table: rank r holds batches b = r mod 2
+    assert sorted(r for rows in gathered for r in rows) == list(range(ROWS))
+    assert gathered[0][:BATCH] == list(range(0, BATCH)) and gathered[1][:BATCH] == list(range(BATCH, 2 * BATCH))
+    flags_all, planted_all = _scan_rows(list(range(ROWS)))
     assert t == 2.0  # max over ranks
     assert found == flagged == int(flags_all.sum()) == planted_all == expected
 
+
+def test_two_rank_weak_shards_equal_single_scan():
+    t, found, flagged, expected, gathered = _run("weak")
+    assert gathered[0] == list(range(ROWS_PER_RANK))
+    assert gathered[1] == list(range(ROWS_PER_RANK, 2 * ROWS_PER_RANK))
+    flags_all, planted_all = _scan_rows(list(range(2 * ROWS_PER_RANK)))
+    assert t == 2.0
+    assert found == flagged == int(flags_all.sum()) == planted_all == expected
+
+
+def test_rank_batches_cover_config4_table():
+    """The default bench shape: 32.7M rows in 300000-row batches (109 full
+    batches) over 1, 2, 4 and 8 ranks: every batch on exactly one rank, rank
+    loads differ by at most one batch."""
+    _paths()
+    import bench
+    from cudasp_amd import assign_gpu
+    rows, batch = 32_700_000, 300_000
+    for world in (1, 2, 4, 8):
+        per = [bench.rank_batches("roundrobin", rows, batch, r, world, assign_gpu) for r in range(world)]
+        firsts = sorted(g0 for p in per for g0, _ in p)
+        assert firsts == list(range(0, rows, batch))
+        assert sum(m for p in per for _, m in p) == rows
+        loads = [len(p) for p in per]
+        assert max(loads) - min(loads) <= 1

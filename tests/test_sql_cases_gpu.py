@@ -142,3 +142,40 @@ def test_scanner_set_keys(gpu):
         assert (values(s, len(labels)) == want).all()
         s.set_keys(scan, spend, labels[:1])
         assert (values(s, 1) == want[:2]).all()
+
+
+def test_multi_gpu_round_robin_host(gpu, monkeypatch):
+    """The host's num_gpus > 1 path (CudaspScanLocalInit's round-robin,
+    src/cudasp_extension.cu:523-529) on a one-GPU box: the test hook
+    CUDASP_TF_DEVICE_MAP="0,0" gives the host two logical GPUs that both run
+    on device 0.  Executor threads alternate logical GPUs 0, 1, 0, 1, each
+    with its own scanner and stream, and the results equal the one-GPU run
+    (as multisets) on the SQL file's queries and on 128 random rows with
+    planted base and label matches repeated over several batches."""
+    from cudasp_amd import cudasp_scan, release_pool
+    sc = golden_io.load("sql_cases.json")
+    rr = golden_io.load("random_rows.json")
+    rows = [(bytes.fromhex(r["txid"]), 800000 + i,
+             bytes.fromhex(r["tweak"]), r["outputs"]) for i, r in enumerate(rr["rows"])] * 40
+    keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]),
+            [bytes.fromhex(l) for l in rr["label_keys"]])
+
+    def run_all(threads):
+        outs, assign = [], []
+        for q in sc["queries"]:
+            outs.append(sorted(cudasp_scan(_table(sc, q), bytes.fromhex(q["scan_key"]), bytes.fromhex(q["spend_key"]),
+                                           [bytes.fromhex(l) for l in q["label_keys"]], batch_size=q["batch_size"],
+                                           threads=threads)))
+        outs.append(sorted(cudasp_scan(rows, *keys, batch_size=1000, threads=threads, assignments=assign)))
+        return outs, assign
+
+    monkeypatch.delenv("CUDASP_TF_DEVICE_MAP", raising=False)
+    one, assign1 = run_all(4)
+    assert {g for g, _ in assign1} == {0}
+    release_pool()
+    monkeypatch.setenv("CUDASP_TF_DEVICE_MAP", "0,0")
+    two, assign2 = run_all(4)
+    release_pool()
+    assert assign2 == [(0, 0), (1, 0), (0, 0), (1, 0)]
+    assert two == one
+    assert len(one[-1]) > 0

@@ -34,9 +34,9 @@ def kernel_key(name):
     m = re.fullmatch(r"void k_shared_secret<(\d+)>", k)
     if m:
         k = "k_shared_secret" if m.group(1) == "4" else "k_shared_secret<%s>" % m.group(1)
-    m = re.fullmatch(r"void k_match<(true|false), (\d+)>", k)
-    if m:  # stage B: 6 rows per thread (CUDASP_ROWS_B) for full batches
-        k = "void k_match<%s>" % m.group(1) if m.group(2) == "6" else "void k_match<%s, %s>" % m.groups()
+    m = re.fullmatch(r"void k_match<(true|false), (\d+)(?:, (\d+))?>", k)
+    if m:  # stage B: 6 rows per thread (CUDASP_ROWS_B) for full batches; any fixed-base width
+        k = "void k_match<%s>" % m.group(1) if m.group(2) == "6" else "void k_match<%s, %s>" % m.groups()[:2]
     return k
 
 
@@ -74,12 +74,13 @@ def main():
     ap.add_argument("csvs", nargs="+")
     ap.add_argument("--rows", type=int, default=300000)
     ap.add_argument("--source", default="")
+    ap.add_argument("--shape", default="", help="the run's shape (labels, outputs per row, window width)")
     ap.add_argument("--algorithmic-bytes-per-row", type=float, default=89.0)
     ap.add_argument("--probe-rows", type=int, default=0)
     ap.add_argument("--probe-outputs-per-row", type=float, default=2.0)
     a = ap.parse_args()
     if a.mode == "sq":
-        res = dict(source=a.source, rows_per_launch=a.rows, per_kernel=averages(load(a.csvs)))
+        res = dict(source=a.source, shape=a.shape, rows_per_launch=a.rows, per_kernel=averages(load(a.csvs)))
     else:
         fetch = averages(load([a.csvs[0]]))
         write = averages(load([a.csvs[1]]))
