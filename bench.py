@@ -403,13 +403,10 @@ def e2e_leg(args, mean_k):
     return res
 
 
-def cpu_baseline(tab, labels, sample_rows, threads, output_count=1, label_negation=False):
-    """The CPU oracle (oracle/cudasp_oracle.c, `port`) timed on this box's host
-    cores over the first `sample_rows` rows of the rank table (whole batches,
-    so several scanners/streams are covered), and its flags compared row by
-    row with the GPU's flags of the last timed step."""
-    sys.path.insert(0, ROOT)
-    from oracle import oracle  # the C restatement: baseline + checker only
+def cpu_sample(tab, sample_rows):
+    """The first `sample_rows` rows of the rank table (whole batches, so
+    several scanners/streams are covered) in host memory: tweak blobs, the
+    outputs CSR and the GPU's flags of the last pass."""
     tw, outs, offs, lens, gflags = [], [], [], [], []
     base, m = 0, 0
     for b in range(tab.nb):
@@ -428,17 +425,58 @@ def cpu_baseline(tab, labels, sample_rows, threads, output_count=1, label_negati
         gflags.append(tab.flags[b][:mb].cpu().numpy())
         base += used
         m += mb
-    tweaks = np.concatenate(tw)
-    outs, offs, lens, gflags = np.concatenate(outs), np.concatenate(offs), np.concatenate(lens), np.concatenate(gflags)
+    return dict(tweaks=np.concatenate(tw), outs=np.concatenate(outs), offs=np.concatenate(offs),
+                lens=np.concatenate(lens), gpu_flags=np.concatenate(gflags), rows=m, batches=len(tw))
+
+
+def cpu_baseline(smp, labels, threads, output_count=1, label_negation=False):
+    """The CPU oracle (oracle/cudasp_oracle.c, `port`: a plain restatement of
+    the reference's algorithm -- 4x64-bit limbs, 4-bit Jacobian windows, no
+    endomorphism) timed on this box's host cores over the sample, its flags
+    compared row by row with the GPU's."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle  # the C restatement: baseline + checker only
     t0 = time.perf_counter()
-    flags, _ = oracle.scan_ex(SCAN_KEY, SPEND_KEY, labels, tweaks, outs, offs, lens, output_count=output_count,
-                              label_negation=label_negation, threads=threads)
+    flags, _ = oracle.scan_ex(SCAN_KEY, SPEND_KEY, labels, smp["tweaks"], smp["outs"], smp["offs"], smp["lens"],
+                              output_count=output_count, label_negation=label_negation, threads=threads)
     dt = time.perf_counter() - t0
-    nb = len(tw)
-    return dict(value=m / dt, unit="tx/s", cores=threads, kind="port",
+    return dict(value=smp["rows"] / dt, unit="tx/s", cores=threads, kind="port",
                 sample="first %d rows (%d batches) of the rank-0 table, %d labels, oracle/cudasp_oracle.c with %d "
-                       "pthreads" % (m, nb, len(labels), threads),
-                seconds=round(dt, 3), flags_match_gpu=bool(np.array_equal(flags, gflags)),
+                       "pthreads" % (smp["rows"], smp["batches"], len(labels), threads),
+                seconds=round(dt, 3), flags_match_gpu=bool(np.array_equal(flags, smp["gpu_flags"])),
+                sample_matches=int(flags.sum()))
+
+
+def cpu_baseline_optimized(smp, labels, threads):
+    """`port-optimized`: the product's own row pipeline (GLV + wNAF, co-Z,
+    shared inversions, one-compression SHA-256, batched label inversions)
+    compiled for the host at -O3 (tools/cpu_port, 8-bit fixed-base windows
+    sized for the CPU cache), timed on the same sample and cores; flags
+    compared with the GPU's."""
+    import ctypes
+    lib_path = os.path.join(ROOT, "tools", "cpu_port", "libcudasp_cpu_port.so")
+    if not os.path.exists(lib_path):
+        return dict(error="tools/cpu_port not built")
+    lib = ctypes.CDLL(lib_path)
+    P = ctypes.c_void_p
+    lib.cudasp_cpu_port_scan.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint32, P, P, P, P, ctypes.c_int]
+    lib.cudasp_cpu_port_scan.restype = ctypes.c_int
+    n = smp["rows"]
+    flags = np.zeros(n, dtype=np.uint8)
+    outs = np.ascontiguousarray(smp["outs"], dtype=np.int64)
+    lab = b"".join(labels) if labels else None
+    t0 = time.perf_counter()
+    rc = lib.cudasp_cpu_port_scan(SCAN_KEY, SPEND_KEY, lab, len(labels), smp["tweaks"].ctypes.data, n,
+                                  outs.ctypes.data if outs.size else None, smp["offs"].ctypes.data,
+                                  smp["lens"].ctypes.data, flags.ctypes.data, threads)
+    dt = time.perf_counter() - t0
+    if rc != 0:
+        return dict(error="cudasp_cpu_port_scan returned %d" % rc)
+    return dict(value=n / dt, unit="tx/s", cores=threads, kind="port-optimized",
+                sample="first %d rows (%d batches) of the rank-0 table, %d labels, the product's row pipeline "
+                       "compiled for the host (tools/cpu_port) on %d threads" % (n, smp["batches"], len(labels),
+                                                                                 threads),
+                seconds=round(dt, 3), flags_match_gpu=bool(np.array_equal(flags, smp["gpu_flags"])),
                 sample_matches=int(flags.sum()))
 
 
@@ -655,9 +693,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         use, visible = host_cores()
         threads = args.cpu_threads or use
-        result["cpu_baseline"] = cpu_baseline(tab, labels, args.cpu_rows, threads, args.output_count,
-                                              args.label_negation)
+        smp = cpu_sample(tab, args.cpu_rows)
+        result["cpu_baseline"] = cpu_baseline(smp, labels, threads, args.output_count, args.label_negation)
         result["cpu_baseline"]["host_cpus_visible"] = visible
+        if args.output_count == 1 and not args.label_negation:
+            result["cpu_baseline_optimized"] = cpu_baseline_optimized(smp, labels, threads)
+        del smp
     for s in scanners:
         s.close()
     if rank == 0 and world == 1 and not args.no_e2e and args.output_count == 1 and not args.label_negation:
