@@ -255,7 +255,7 @@ def rank_batches(shard, rows, batch, rank, world, assign):
     return [(first + b * batch, min(batch, rows - b * batch)) for b in range((rows + batch - 1) // batch)]
 
 
-def run_step(tab, scanners, streams, events=None):
+def run_step(tab, scanners, streams, events=None, tail_rows=(0, 0)):
     """One pass over the rank's table.  Each batch is the two kernels of
     cudasp_scan_device (stage A then stage B on the batch's stream); when
     `events` is a list, HIP events bracket each launch on its stream (with
@@ -265,10 +265,13 @@ def run_step(tab, scanners, streams, events=None):
     cur = torch.cuda.current_stream()
     for st in streams:
         st.wait_stream(cur)  # the counters are zeroed before any batch counts into them
+    tail_from = tab.nb - len(streams) if any(tail_rows) else tab.nb
     for b in range(tab.nb):
         s = b % len(scanners)
         st = streams[s]
         m = tab.sizes[b]
+        if b >= tail_from:
+            scanners[s].set_rows_per_thread(*tail_rows)  # the last round of launches: shorter drain
         with torch.cuda.stream(st):
             if events is not None:
                 e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
@@ -281,6 +284,9 @@ def run_step(tab, scanners, streams, events=None):
             if events is not None:
                 e2.record(st)
                 events.append((e0, e1, e2))
+    if any(tail_rows):
+        for sc in scanners:
+            sc.set_rows_per_thread(0, 0)
 
 
 def exclusive_launches(tab, scanner, stream, max_batches):
@@ -540,6 +546,9 @@ def main():
     ap.add_argument("--fb-bits", type=int, default=26, choices=[22, 26],
                     help="fixed-base window width (26: 21.5 GB table, 22: 1.5 GiB; same results)")
     ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--tail-rows-a", type=int, default=0, help="stage-A rows per thread of the last round of "
+                    "launches (one per stream); 0 = automatic")
+    ap.add_argument("--tail-rows-b", type=int, default=0)
     ap.add_argument("--exclusive-batches", type=int, default=16,
                     help="full batches timed alone on one stream after the timed steps (roofline kernel_ms)")
     ap.add_argument("--cpu-rows", type=int, default=1200000)
@@ -593,7 +602,7 @@ def main():
 
     step_found = []
     for _ in range(args.warmup):
-        run_step(tab, scanners, streams)
+        run_step(tab, scanners, streams, tail_rows=(args.tail_rows_a, args.tail_rows_b))
         torch.cuda.synchronize(device)
         step_found.append(int(tab.match_count.sum().item()))
 
@@ -603,7 +612,7 @@ def main():
         barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
-        run_step(tab, scanners, streams, events=events)
+        run_step(tab, scanners, streams, events=events, tail_rows=(args.tail_rows_a, args.tail_rows_b))
         torch.cuda.synchronize(device)
         barrier()
         times.append(time.perf_counter() - t0)

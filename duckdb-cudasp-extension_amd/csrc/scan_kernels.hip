@@ -61,6 +61,22 @@ constexpr int BLOCK = 256;
 #ifndef CUDASP_WAVES_B
 #define CUDASP_WAVES_B 3
 #endif
+// Measurement-only A/B (never in a product build): CUDASP_AB_SCRATCH_ALIAS=S
+// maps every thread's scratch slot onto slot mod S, so the per-row scratch of
+// both stages (odd-multiple table, Z ratios, pending rows, label prefix
+// products) stays inside an L2-sized region: the HBM traffic of the scratch
+// disappears while the instruction stream is unchanged.  Threads then race on
+// shared slots, so results are wrong -- the build only times the kernels.
+#ifdef CUDASP_AB_SCRATCH_ALIAS
+__device__ __forceinline__ Scratch ab_scratch(uint32_t* s, uint32_t stride, uint32_t slot) {
+  // never more slots than the buffer holds (stride = the launch's thread count)
+  const uint32_t a = stride < CUDASP_AB_SCRATCH_ALIAS ? stride : CUDASP_AB_SCRATCH_ALIAS;
+  return make_scratch(s, a, slot % a);
+}
+#define SCAN_SCRATCH ab_scratch
+#else
+#define SCAN_SCRATCH make_scratch
+#endif
 // Grid cap for the grid-stride kernels; also bounds the per-slot scratch.
 constexpr uint32_t MAX_BLOCKS = 4096;
 // Rows per thread in stage A / stage B: the rows of a thread share one field
@@ -113,7 +129,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
                                                          uint32_t* __restrict__ t_out) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  const Scratch sc = make_scratch(vscr, stride, slot);
+  const Scratch sc = SCAN_SCRATCH(vscr, stride, slot);
   if constexpr (R == 1) {
     for (uint32_t row = slot; row < n; row += stride) {
       uint32_t x[8], y[8];
@@ -186,7 +202,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
                                                  int64_t* __restrict__ values) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  const Scratch sc = make_scratch(lscr, stride, slot);
+  const Scratch sc = SCAN_SCRATCH(lscr, stride, slot);
   const uint32_t G = (n + R - 1) / R;
   const int PB = FW * (int)k.label_count * R;
   for (uint32_t g0 = blockIdx.x * blockDim.x; g0 < G; g0 += stride) {
@@ -975,6 +991,17 @@ int cudasp_scanner_set_fixed_base_bits(cudasp_scanner* s, int bits) {
 }
 
 int cudasp_scanner_fixed_base_bits(const cudasp_scanner* s) { return s ? s->fb_bits : 0; }
+
+int cudasp_scanner_set_rows_per_thread(cudasp_scanner* s, int rows_a, int rows_b) {
+  g_last_error.clear();
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  if (!(rows_a == 0 || rows_a == 1 || rows_a == 2 || rows_a == ROWS_A) || !(rows_b == 0 || rows_b == 2 || rows_b == ROWS_B))
+    return set_error(CUDASP_ERR_INVALID_ARG, "rows per thread: stage A 0, 1, 2 or %d; stage B 0, 2 or %d", ROWS_A,
+                     ROWS_B);
+  s->rows_a_force = rows_a;
+  s->rows_b_force = rows_b;
+  return CUDASP_OK;
+}
 
 int cudasp_scanner_sync(cudasp_scanner* s) {
   if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");

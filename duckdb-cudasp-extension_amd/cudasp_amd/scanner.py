@@ -72,6 +72,11 @@ class Scanner:
         width; builds the device's table for that width on first use."""
         _native.check(self._lib.cudasp_scanner_set_fixed_base_bits(self._h, int(bits)))
 
+    def set_rows_per_thread(self, rows_a=0, rows_b=0):
+        """Launch shape of the next launches (cudasp_scanner_set_rows_per_thread):
+        rows per thread of stage A (1, 2, 4) and stage B (2, 6); 0 = automatic."""
+        _native.check(self._lib.cudasp_scanner_set_rows_per_thread(self._h, int(rows_a), int(rows_b)))
+
     @property
     def fixed_base_bits(self):
         return int(self._lib.cudasp_scanner_fixed_base_bits(self._h))

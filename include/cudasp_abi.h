@@ -91,6 +91,15 @@ uint64_t cudasp_fixed_base_table_bytes(int bits);
 int cudasp_scanner_set_fixed_base_bits(cudasp_scanner* s, int bits);
 int cudasp_scanner_fixed_base_bits(const cudasp_scanner* s);
 
+/* Launch shape of the scanner's next launches: rows per thread of stage A
+ * (1, 2 or 4) and stage B (2 or 6); 0 = automatic (the default: 4 and 6, or
+ * fewer for launches too small to fill the device).  Rows of a thread run in
+ * sequence and share one inversion, so fewer rows per thread shorten a launch
+ * at a few percent more instructions per row: a host that knows a launch is
+ * the tail of its work (the last batches of a rank or executor thread) can
+ * trade that for a shorter drain.  Results do not depend on it. */
+int cudasp_scanner_set_rows_per_thread(cudasp_scanner* s, int rows_a, int rows_b);
+
 /* Protocol variants, off by default.  With the
  * defaults a scanner computes exactly the reference's flags.
  *   output_count   K >= 1: each row is tested for the output indices
