@@ -543,8 +543,9 @@ def main():
     ap.add_argument("--outputs-per-row", type=int, default=2)
     ap.add_argument("--outputs-max", type=int, default=0,
                     help="variable outputs per row, uniform in [1, N] (15 -> mean 8, config 5); 0 = fixed")
-    ap.add_argument("--fb-bits", type=int, default=26, choices=[22, 26],
-                    help="fixed-base window width (26: 21.5 GB table, 22: 1.5 GiB; same results)")
+    ap.add_argument("--fb-bits", type=int, default=26, choices=[7, 22, 26],
+                    help="fixed-base window width (26: 21.5 GB HBM table, 22: 1.5 GiB, 7: 151.5 KB staged in LDS; "
+                         "same results)")
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--tail-rows-a", type=int, default=0, help="stage-A rows per thread of the last round of "
                     "launches (one per stream); 0 = automatic")
@@ -570,7 +571,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # The window width is the process default for every scanner and the
     # synthetic-table generator (read once by the library).
-    os.environ["CUDASP_FB_BITS"] = str(args.fb_bits)
+    os.environ["CUDASP_FB_BITS"] = str(args.fb_bits if args.fb_bits in (22, 26) else 22)
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     if world > 1:

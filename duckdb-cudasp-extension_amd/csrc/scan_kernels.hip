@@ -189,17 +189,16 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
 // (K output indices per input row; n == n_rows when K = 1): t, flags and
 // values are indexed by the virtual row, the outputs lists by the input row.
 template <bool VALUES, int R, int FBB>
-__global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t* __restrict__ t_in, uint32_t n,
-                                                 uint32_t n_rows,
-                                                 const uint32_t* __restrict__ fb, ScanConsts k,
-                                                 const uint32_t* __restrict__ labels,
-                                                 const int64_t* __restrict__ outputs,
-                                                 const uint32_t* __restrict__ offs,
-                                                 const uint32_t* __restrict__ lens,
-                                                 uint32_t* __restrict__ lscr, uint8_t* __restrict__ flags,
-                                                 uint32_t* __restrict__ match_rows,
-                                                 uint32_t* __restrict__ match_count,
-                                                 int64_t* __restrict__ values) {
+__device__ __forceinline__ void match_body(const uint32_t* __restrict__ t_in, uint32_t n, uint32_t n_rows,
+                                           const uint32_t* __restrict__ fb, const ScanConsts& k,
+                                           const uint32_t* __restrict__ labels,
+                                           const int64_t* __restrict__ outputs,
+                                           const uint32_t* __restrict__ offs,
+                                           const uint32_t* __restrict__ lens,
+                                           uint32_t* __restrict__ lscr, uint8_t* __restrict__ flags,
+                                           uint32_t* __restrict__ match_rows,
+                                           uint32_t* __restrict__ match_count,
+                                           int64_t* __restrict__ values) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
   const Scratch sc = SCAN_SCRATCH(lscr, stride, slot);
@@ -270,6 +269,40 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(const uint32_t*
       }
     }
   }
+}
+
+#define MATCH_PARAMS                                                                                        \
+  const uint32_t *__restrict__ t_in, uint32_t n, uint32_t n_rows, const uint32_t *__restrict__ fb, ScanConsts k, \
+      const uint32_t *__restrict__ labels, const int64_t *__restrict__ outputs, const uint32_t *__restrict__ offs, \
+      const uint32_t *__restrict__ lens, uint32_t *__restrict__ lscr, uint8_t *__restrict__ flags,               \
+      uint32_t *__restrict__ match_rows, uint32_t *__restrict__ match_count, int64_t *__restrict__ values
+#define MATCH_ARGS t_in, n, n_rows, fb, k, labels, outputs, offs, lens, lscr, flags, match_rows, match_count, values
+
+// Stage B with the fixed-base table in HBM (22- or 26-bit windows).
+template <bool VALUES, int R, int FBB>
+__global__ __launch_bounds__(BLOCK, CUDASP_WAVES_B) void k_match(MATCH_PARAMS) {
+  match_body<VALUES, R, FBB>(MATCH_ARGS);
+}
+
+// Stage B with LDS-staged fixed-base windows (the north star's layout): the
+// 7-bit table (37 windows x 64 odd multiples x 64 B = 151.5 KB) is copied from
+// HBM into the workgroup's LDS, then t*G reads its 37 entries per row from
+// LDS.  One 768-thread workgroup per CU (12 waves, 3 per SIMD).  Selected by
+// a scanner's fixed-base width 7; measured against the HBM tables:
+// 36 mixed additions per row instead of 9 cost far more than the 10 HBM
+// gathers they replace.
+constexpr int LDS_BLOCK = 768;
+constexpr int LDS_FB_BITS = 7;
+constexpr uint32_t LDS_FB_WORDS = FbWidth<LDS_FB_BITS>::WINDOWS * FbWidth<LDS_FB_BITS>::ENTRIES * FB_WORDS;
+template <bool VALUES, int R>
+__global__ __launch_bounds__(LDS_BLOCK, 1) void k_match_lds(MATCH_PARAMS) {
+  __shared__ uint4 tab[LDS_FB_WORDS / 4];
+  const uint4* src = reinterpret_cast<const uint4*>(fb);
+  for (uint32_t i = threadIdx.x; i < LDS_FB_WORDS / 4; i += blockDim.x) tab[i] = src[i];
+  __syncthreads();
+  const uint32_t* lfb = reinterpret_cast<const uint32_t*>(tab);
+  match_body<VALUES, R, LDS_FB_BITS>(t_in, n, n_rows, lfb, k, labels, outputs, offs, lens, lscr, flags, match_rows,
+                                     match_count, values);
 }
 
 // K > 1 output indices: a row matches when any of its K virtual rows does;
@@ -524,8 +557,9 @@ struct DeviceTable {
 std::mutex g_table_map_mutex;
 std::map<std::pair<int, int>, DeviceTable> g_tables;
 
-// Prebuilt widths (k_match / k_synth_tweaks instances).
-bool fb_bits_supported(int bits) { return bits == 22 || bits == 26; }
+// Prebuilt widths (k_match / k_synth_tweaks instances): 22 and 26 (HBM), 7
+// (LDS-staged, stage B only).
+bool fb_bits_supported(int bits) { return bits == 22 || bits == 26 || bits == LDS_FB_BITS; }
 
 int g_default_fb_bits = 0;  // 0: not read yet
 std::once_flag g_default_fb_once;
@@ -537,7 +571,7 @@ int default_fb_bits() {
     g_default_fb_bits = FB_BITS;
     if (const char* e = getenv("CUDASP_FB_BITS")) {
       const int b = atoi(e);
-      if (fb_bits_supported(b)) g_default_fb_bits = b;
+      if (b == 22 || b == 26) g_default_fb_bits = b;  // the HBM widths (the synthetic generator uses it too)
     }
   });
   return g_default_fb_bits;
@@ -550,7 +584,7 @@ size_t fb_table_bytes(int bits) {
 
 int ensure_device_table(int device, int bits, const uint32_t** out) {
   if (!fb_bits_supported(bits))
-    return set_error(CUDASP_ERR_INVALID_ARG, "fixed-base window width %d not supported (22 or 26)", bits);
+    return set_error(CUDASP_ERR_INVALID_ARG, "fixed-base window width %d not supported (22, 26, or 7 = LDS)", bits);
   DeviceTable* dt;
   {
     std::lock_guard<std::mutex> lock(g_table_map_mutex);
@@ -723,6 +757,43 @@ void free_scanner(cudasp_scanner* s) {
   delete s;
 }
 
+// Stage B with the LDS-staged 7-bit table (k_match_lds): 768-thread
+// workgroups, 2 rows per thread (6 for launches large enough to fill the
+// device at 6), within the label scratch's slots.
+int launch_match_lds(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t* outputs, const uint32_t* offs,
+                     const uint32_t* lens, uint8_t* flags, uint32_t* match_rows, uint32_t* match_count,
+                     int64_t* values, hipStream_t st) {
+  const uint32_t K = s->consts.output_count;
+  const uint32_t N = K * n;
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+  const int r = s->rows_b_force ? s->rows_b_force
+                                : ((N + ROWS_B - 1) / ROWS_B >= (uint32_t)cus * LDS_BLOCK ? ROWS_B : 2);
+  uint64_t blocks = ((N + r - 1) / (uint32_t)r + LDS_BLOCK - 1) / LDS_BLOCK;
+  const uint64_t cap = (uint64_t)s->slots_b * lscratch_words(s->label_cap) /
+                       ((uint64_t)lscratch_words(s->label_count, r) * LDS_BLOCK);
+  if (blocks > cap) blocks = cap;
+  if (blocks > MAX_BLOCKS) blocks = MAX_BLOCKS;
+  if (blocks == 0) blocks = 1;
+  auto kv = r == ROWS_B ? k_match_lds<true, ROWS_B> : k_match_lds<true, 2>;
+  auto kf = r == ROWS_B ? k_match_lds<false, ROWS_B> : k_match_lds<false, 2>;
+  if (values) {
+    hipLaunchKernelGGL(kv, dim3((uint32_t)blocks), dim3(LDS_BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels,
+                       nullptr, nullptr, nullptr, s->d_lscratch, nullptr, nullptr, nullptr, values);
+  } else if (K == 1) {
+    hipLaunchKernelGGL(kf, dim3((uint32_t)blocks), dim3(LDS_BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels,
+                       outputs, offs, lens, s->d_lscratch, flags, match_rows, match_count, nullptr);
+  } else {
+    hipLaunchKernelGGL(kf, dim3((uint32_t)blocks), dim3(LDS_BLOCK), 0, st, t, N, n, s->d_fb, s->consts, s->d_labels,
+                       outputs, offs, lens, s->d_lscratch, s->d_vflags, nullptr, nullptr, nullptr);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_or_flags, dim3(grid_for(n)), dim3(BLOCK), 0, st, s->d_vflags, n, K, flags, match_rows,
+                       match_count);
+  }
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
 // Stage B over the K n virtual rows of n input rows (t: 8 x (K n)); with
 // K > 1 the per-index flags are ORed per input row before the compaction.
 int launch_match(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t* outputs, const uint32_t* offs,
@@ -732,6 +803,8 @@ int launch_match(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t
   const uint32_t N = K * n;
   const int r = rows_b_for(s, N);
   const uint32_t blocks_b = grid_b(s, N, r);
+  if (s->fb_bits == LDS_FB_BITS) return launch_match_lds(s, t, n, outputs, offs, lens, flags, match_rows, match_count,
+                                                         values, st);
   const bool w26 = s->fb_bits == 26;
   auto kv = r == ROWS_B ? (w26 ? k_match<true, ROWS_B, 26> : k_match<true, ROWS_B, 22>)
                         : (w26 ? k_match<true, 2, 26> : k_match<true, 2, 22>);

@@ -33,7 +33,7 @@ constexpr int NAF_MAX = 136;
 #endif
 template <int BITS>
 struct FbWidth {
-  static_assert(BITS >= 8 && BITS <= 27, "fixed-base window width");
+  static_assert(BITS >= 4 && BITS <= 27, "fixed-base window width");
   static constexpr int WINDOWS = (256 + BITS - 1) / BITS;
   static constexpr uint32_t ENTRIES = 1u << (BITS - 1);
 };

@@ -80,10 +80,11 @@ int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32
 
 /* Fixed-base window width of stage B's t*G (the reference's gECC d_mul_table,
  * src/cudasp_gpu.cu:317-354).  Prebuilt widths: 22 bits (12 windows, 1.5 GiB
- * table per device) and 26 bits (10 windows, 21.5 GB; one mixed addition
- * fewer per window saved, ~1.5% faster end to end).  Same results at every
- * width.  The process default is CUDASP_FB_BITS from the environment (22 or
- * 26), else 22.  set_fixed_base_bits (0 = the default) switches a scanner's
+ * table per device in HBM), 26 bits (10 windows, 21.5 GB in HBM; two mixed
+ * additions fewer per row, ~1.5% faster end to end) and 7 bits (37 windows,
+ * 151.5 KB, staged into each workgroup's LDS -- measured slower: 36 mixed
+ * additions per row).  Same results at every width.  The process default is
+ * CUDASP_FB_BITS from the environment (22 or 26), else 22.  set_fixed_base_bits (0 = the default) switches a scanner's
  * table, building it on first use; not concurrent with work in flight on the
  * scanner.  table_bytes returns 0 for an unsupported width. */
 int cudasp_default_fixed_base_bits(void);

@@ -1,0 +1,86 @@
+"""GPU: stage B's fixed-base window widths give identical results.
+
+The width of the t*G table is a per-scanner runtime choice
+(cudasp_scanner_set_fixed_base_bits): 22-bit windows (1.5 GiB HBM table, the
+library default), 26-bit (21.5 GB HBM) and 7-bit staged into LDS
+(k_match_lds).  All must produce the oracle's compare values and flags
+bit for bit, with labels and at a launch large enough to use the 6-rows-per-
+thread shapes."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def test_widths_equal_oracle(torch):
+    from test_labels16_gpu import rows_of, synth_var
+    from cudasp_amd import Scanner
+    from oracle import oracle
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    labels = bench.label_keys(3)
+    n = 5003
+    x, y, outs, offs, lens = synth_var(torch, 123456, n)
+    rows = rows_of(x, y)
+    _, ov = oracle.scan(bench.SCAN_KEY, bench.SPEND_KEY, labels, rows, threads=16, want_values=True)
+    o = outs.cpu().numpy()
+    of = offs.cpu().numpy().view(np.uint32)
+    for i in range(0, n, 5):
+        o[of[i]] = ov[i, (i // 5) % 4]
+    od = torch.from_numpy(o).cuda()
+    want, _ = oracle.scan(bench.SCAN_KEY, bench.SPEND_KEY, labels, rows, o, of, lens.cpu().numpy().view(np.uint32),
+                          threads=16)
+    with Scanner(bench.SCAN_KEY, bench.SPEND_KEY, labels, max_rows=n) as s:
+        assert s.fixed_base_bits in (22, 26)
+        for bits in (22, 26, 7):
+            s.set_fixed_base_bits(bits)
+            assert s.fixed_base_bits == bits
+            t = torch.empty((8, n), dtype=torch.int32, device="cuda")
+            v = torch.empty((4, n), dtype=torch.int64, device="cuda")
+            s.row_values_device(x, y, t, v)
+            flags = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            s.scan_device(x, y, od, offs, lens, flags)
+            s.sync()
+            assert (v.cpu().numpy().T == ov).all(), bits
+            assert (flags.cpu().numpy() == want).all(), bits
+        with pytest.raises(Exception):
+            s.set_fixed_base_bits(24)
+
+
+def test_lds_width_full_batch(torch):
+    """A full 300000-row batch through the LDS-staged stage B equals the
+    default width's flags and compacted rows (both 2- and 6-row shapes)."""
+    from test_gpu_synth import _plant, synth
+    from cudasp_amd import Scanner
+    import bench
+    n = 300000
+    x, y, outs, offs, lens = synth(torch, 42, n)
+    planted = _plant(torch, x, y, outs, [])
+    res = []
+    with Scanner(bench.SCAN_KEY, bench.SPEND_KEY, [], max_rows=n) as s:
+        for bits, rb in ((22, 0), (7, 0), (7, 6), (7, 2)):
+            s.set_fixed_base_bits(bits)
+            s.set_rows_per_thread(0, rb)
+            flags = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            rows = torch.zeros(n, dtype=torch.int32, device="cuda")
+            cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+            s.scan_device(x, y, outs, offs, lens, flags, rows, cnt)
+            s.sync()
+            c = int(cnt.item())
+            assert sorted(rows[:c].cpu().tolist()) == planted.cpu().tolist()
+            res.append(flags.cpu().numpy())
+    for r in res[1:]:
+        assert (r == res[0]).all()
