@@ -130,6 +130,16 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
   const Scratch sc = SCAN_SCRATCH(vscr, stride, slot);
+  // A/B builds may fold only the odd-multiple table or only the pending rows
+  // (the two regions never overlap: table words < VB_SCRATCH_WORDS).
+#if defined(CUDASP_AB_ALIAS_TABLE_ONLY)
+  const Scratch sc_tab = SCAN_SCRATCH(vscr, stride, slot), sc_pend = make_scratch(vscr, stride, slot);
+#elif defined(CUDASP_AB_ALIAS_PEND_ONLY)
+  const Scratch sc_tab = make_scratch(vscr, stride, slot), sc_pend = SCAN_SCRATCH(vscr, stride, slot);
+#else
+  const Scratch& sc_tab = sc;
+  const Scratch& sc_pend = sc;
+#endif
   if constexpr (R == 1) {
     for (uint32_t row = slot; row < n; row += stride) {
       uint32_t x[8], y[8];
@@ -163,18 +173,18 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
         y[w] = ty[(size_t)w * n + row];
       }
       gej P;
-      row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
-      pend_store(sc, PB, j, P);
+      row_shared_secret_point(P, x, y, naf, k.naf_len, sc_tab);
+      pend_store(sc_pend, PB, j, P);
       count = j + 1;
     }
-    pend_invert<R>(sc, PB, count);
+    pend_invert<R>(sc_pend, PB, count);
 #pragma unroll 1
     for (int j = 0; j < count; j++) {
       const uint32_t row = g + (uint32_t)j * G;
       gej P;
       fe zi;
-      pend_load(P, sc, PB, j);
-      scr_load(zi, sc, PEND_ZI(PB, j));
+      pend_load(P, sc_pend, PB, j);
+      scr_load(zi, sc_pend, PEND_ZI(PB, j));
       uint32_t sx[8];
       const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
       store_t(t_out, n, k.output_count, row, sx, y_odd, k.mid);

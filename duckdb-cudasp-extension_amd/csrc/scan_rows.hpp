@@ -229,6 +229,48 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
   // entry with its digit's sign times sgn (wave-uniform, like the digits).
   bool inf = true;
   bool sgn_neg = false;
+#if LADDER_YH && CUDASP_PHI_TABLE && CUDASP_PREFETCH_ENTRY
+  // The table entry of an iteration's first addition is loaded BEFORE its
+  // doubling, so the load's latency runs under the doubling's ~900
+  // instructions (the digits are wave-uniform, so is the choice).
+  for (int i = (int)naf_len - 1; i >= 0; --i) {
+    const int d0 = uniform_digit(naf, i), d1 = uniform_digit(naf, NAF_MAX + i);
+    const int hf = d0 != 0 ? 0 : (d1 != 0 ? 1 : -1);
+    ge Pn;
+    if (hf >= 0) {
+      const int d = hf ? d1 : d0;
+      const int e = (d < 0 ? -d : d) >> 1;
+      scr_load(Pn.x, sc, hf ? VB_ENTRY_XB(e) : VB_ENTRY_X(e));
+      scr_load(Pn.y, sc, VB_ENTRY_Y(e));
+    }
+    if (!inf) {
+      gej_double_neg_yh(R, R);
+      sgn_neg = !sgn_neg;
+    }
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      const int d = half ? d1 : d0;
+      if (d != 0) {
+        ge P;
+        if (half == hf) {
+          P = Pn;
+        } else {
+          const int e = (d < 0 ? -d : d) >> 1;
+          scr_load(P.x, sc, VB_ENTRY_XB(e));
+          scr_load(P.y, sc, VB_ENTRY_Y(e));
+        }
+        if ((d < 0) != sgn_neg) fe_negate<2>(P.y, P.y);
+        if (inf) {
+          gej_set_ge(R, P);
+          fe_normalize_weak(R.y);
+          inf = false;
+        } else {
+          gej_add_ge_yh(R, R, P);
+        }
+      }
+    }
+  }
+#else
   for (int i = (int)naf_len - 1; i >= 0; --i) {
 #if LADDER_YH
     if (!inf) {
@@ -272,6 +314,7 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
       }
     }
   }
+#endif  // CUDASP_PREFETCH_ENTRY
 #if LADDER_YH
   fe_half(R.y, R.y);                              // Y = Yh / 2
   if (sgn_neg) fe_negate<2>(R.y, R.y);            // R_true
