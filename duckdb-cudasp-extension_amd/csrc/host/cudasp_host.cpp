@@ -733,6 +733,11 @@ uint32_t cudasp_tf_pool_size(void) {
 int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
                        const cudasp_tf_chunk* chunk) {
   if (!b || !g || !l || !chunk) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
+  // The batch slots hold batch_size + one vector of rows (the >= batch_size
+  // trigger runs after each chunk), so a chunk may not exceed one vector.
+  if (chunk->count > CUDASP_TF_VECTOR_SIZE)
+    return host_fail(CUDASP_ERR_INVALID_ARG, "chunk of %u rows exceeds the vector size %d", chunk->count,
+                     CUDASP_TF_VECTOR_SIZE);
   if (chunk->count > 0) {
     int rc = accumulate(*b, *l, *chunk);
     if (rc != CUDASP_OK) return rc;

@@ -98,7 +98,8 @@ uint32_t cudasp_assign_gpu(uint64_t ordinal, uint32_t num_gpus);
 void cudasp_tf_release_pool(void);
 uint32_t cudasp_tf_pool_size(void);
 
-/* One input chunk (<= 2048 rows) of the input table, columns by position:
+/* One input chunk (<= CUDASP_TF_VECTOR_SIZE = 2048 rows; a larger count is
+ * rejected with CUDASP_ERR_INVALID_ARG) of the input table, columns by position:
  * 0 txid BLOB, 1 height INTEGER, 2 tweak_key BLOB, 3 outputs BIGINT[]
  * (src/cudasp_extension.cu:159-163), in DuckDB's unified form.  Validity
  * arrays may be NULL (= all valid).  outputs: per-row list entries

@@ -50,3 +50,25 @@ def test_variant_parameter_errors(k, msg):
         bind(SCAN, SPEND, [], output_count=k)
     assert str(e.value) == msg
     assert bind(SCAN, SPEND, [], output_count=64, label_negation=True, full_x=True).full_x
+
+
+def test_chunk_larger_than_a_vector_is_rejected():
+    """A chunk may hold at most CUDASP_TF_VECTOR_SIZE rows: the batch slots
+    are sized batch_size + one vector (include/cudasp_host.h), so a larger
+    chunk is an argument error, raised before any GPU work."""
+    import ctypes
+
+    from cudasp_amd import _native
+    from cudasp_amd import table_function as tf
+    lib = tf._lib()
+    bound = bind(SCAN, SPEND, [])
+    g, loc = ctypes.c_void_p(), ctypes.c_void_p()
+    assert lib.cudasp_tf_init(bound._h, ctypes.byref(g)) == 0
+    assert lib.cudasp_tf_local_init(g, ctypes.byref(loc)) == 0
+    try:
+        keep, c = tf._make_chunk([(None, None, None, None)] * (tf.VECTOR_SIZE + 1))
+        assert lib.cudasp_tf_function(bound._h, g, loc, ctypes.byref(c)) == _native.CUDASP_ERR_INVALID_ARG
+        assert b"exceeds the vector size" in _native.load().cudasp_last_error()
+    finally:
+        lib.cudasp_tf_local_free(loc)
+        lib.cudasp_tf_global_free(g)
