@@ -289,6 +289,29 @@ def run_step(tab, scanners, streams, events=None, tail_rows=(0, 0)):
             sc.set_rows_per_thread(0, 0)
 
 
+def multi_descs(tab):
+    """The rank's batches as cudasp_scan_device_batches descriptors."""
+    return [dict(tweak_x=tab.cols(tab.tx, b), tweak_y=tab.cols(tab.ty, b), outputs=tab.outs[b], offsets=tab.offs[b],
+                 lengths=tab.lens[b], flags=tab.flags[b][:tab.sizes[b]], match_rows=tab.match_rows[b],
+                 match_count=tab.match_count[b:b + 1]) for b in range(tab.nb)]
+
+
+def run_step_multi(tab, scanner, stream, descs, events=None):
+    """One pass over the rank's table through cudasp_scan_device_batches: one
+    persistent kernel runs both stages over every row of every batch, with
+    per-batch flags and match lists (the results of run_step)."""
+    tab.match_count.zero_()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        if events is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        scanner.scan_device_batches(descs, stream)
+        if events is not None:
+            e1.record(stream)
+            events.append((e0, e1))
+
+
 def exclusive_launches(tab, scanner, stream, max_batches):
     """Per-launch kernel durations with each launch ALONE on the GPU: after
     the timed steps, up to `max_batches` full batches go through one stream
@@ -499,27 +522,36 @@ def sq_profile_path(args):
     return os.path.join(ROOT, "profiles", name + ".json")
 
 
-def alu_roofline(path, value_per_gpu):
+def alu_roofline(path, value_per_gpu, multi=False):
     """Integer-VALU roofline of the whole path: VALU wave-instructions per row
-    of both kernels (rocprofv3 SQ_INSTS_VALU of the same shape of run,
-    profiles/) x rows/s per GPU, against the nominal VALU issue rate and the
-    measured VOP3 rate."""
+    (rocprofv3 SQ_INSTS_VALU of the same shape of run, profiles/: both stage
+    kernels per batch, or k_scan_multi per row with --launch multi) x rows/s
+    per GPU, against the nominal VALU issue rate and the measured VOP3 rate."""
     if not path or not os.path.exists(path):
         return dict(error="no PMC summary for this shape: %s" % os.path.relpath(path, ROOT) if path else "none")
     with open(path) as f:
         sq = json.load(f)
     per = sq["per_kernel"]
-    rpl = float(sq.get("rows_per_launch", 300000))
-    a = per.get("k_shared_secret", {}).get("SQ_INSTS_VALU")
-    bm = per.get("void k_match<false>", {}).get("SQ_INSTS_VALU")
-    if not (a and bm):
-        return dict(error="%s lacks the stage kernels" % os.path.relpath(path, ROOT))
-    wi_per_row = (a + bm) / rpl
+    if multi:
+        m = per.get("k_scan_multi", {}).get("SQ_INSTS_VALU")
+        rows = sq.get("multi_rows_per_launch")
+        if not (m and rows):
+            return dict(error="%s lacks k_scan_multi" % os.path.relpath(path, ROOT))
+        wi_per_row = m / float(rows)
+        per64 = dict(k_scan_multi=wi_per_row * 64)
+    else:
+        rpl = float(sq.get("rows_per_launch", 300000))
+        a = per.get("k_shared_secret", {}).get("SQ_INSTS_VALU")
+        bm = per.get("void k_match<false>", {}).get("SQ_INSTS_VALU")
+        if not (a and bm):
+            return dict(error="%s lacks the stage kernels" % os.path.relpath(path, ROOT))
+        wi_per_row = (a + bm) / rpl
+        per64 = dict(k_shared_secret=a / rpl * 64, k_match=bm / rpl * 64)
     achieved_wi = wi_per_row * value_per_gpu
     return dict(bound="valu", unit="wave-instr/s per GPU", achieved=achieved_wi, peak=VALU_WAVE_INSTR_PEAK,
                 frac=achieved_wi / VALU_WAVE_INSTR_PEAK, measured_vop3_issue_rate=VOP3_WAVE_INSTR_MEASURED,
                 frac_of_measured_vop3_rate=achieved_wi / VOP3_WAVE_INSTR_MEASURED,
-                valu_wave_instr_per_64_rows=dict(k_shared_secret=a / rpl * 64, k_match=bm / rpl * 64),
+                valu_wave_instr_per_64_rows=per64,
                 source=os.path.relpath(path, ROOT),
                 note="SQ_INSTS_VALU per row of a run of this shape (%s); peak = nominal VALU issue rate; VOP3 "
                      "integer ops issue at about half of it on gfx950" % sq.get("shape", "see source"))
@@ -546,6 +578,9 @@ def main():
     ap.add_argument("--fb-bits", type=int, default=26, choices=[7, 22, 26],
                     help="fixed-base window width (26: 21.5 GB HBM table, 22: 1.5 GiB, 7: 151.5 KB staged in LDS; "
                          "same results)")
+    ap.add_argument("--launch", choices=["multi", "batches"], default="multi",
+                    help="multi: the rank's batches in one cudasp_scan_device_batches call (one persistent kernel "
+                         "for both stages); batches: cudasp_scan_device per batch, round-robin over --streams")
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--tail-rows-a", type=int, default=0, help="stage-A rows per thread of the last round of "
                     "launches (one per stream); 0 = automatic")
@@ -601,9 +636,18 @@ def main():
         if world > 1:
             dist.barrier()
 
+    multi = args.launch == "multi"
+    descs = multi_descs(tab) if multi else None
+
+    def step(events=None):
+        if multi:
+            run_step_multi(tab, scanners[0], streams[0], descs, events)
+        else:
+            run_step(tab, scanners, streams, events=events, tail_rows=(args.tail_rows_a, args.tail_rows_b))
+
     step_found = []
     for _ in range(args.warmup):
-        run_step(tab, scanners, streams, tail_rows=(args.tail_rows_a, args.tail_rows_b))
+        step()
         torch.cuda.synchronize(device)
         step_found.append(int(tab.match_count.sum().item()))
 
@@ -613,7 +657,7 @@ def main():
         barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
-        run_step(tab, scanners, streams, events=events, tail_rows=(args.tail_rows_a, args.tail_rows_b))
+        step(events)
         torch.cuda.synchronize(device)
         barrier()
         times.append(time.perf_counter() - t0)
@@ -629,31 +673,49 @@ def main():
               "that differ: %s" % (rank, found, flagged, tab.expected, step_found, bad[:16]), file=sys.stderr, flush=True)
     total_s, found, flagged, expected = aggregate(world, args.dist_backend, total_s, found, flagged, tab.expected)
 
-    # Per-launch kernel durations.  The timed steps run 4 streams at once, so a
-    # launch's event span there includes time shared with the other streams'
-    # kernels (launch_span_ms_concurrent); kernel_ms is the duration of a launch
-    # alone on the GPU (exclusive_launches, after the timed region).
-    ka = [e0.elapsed_time(e1) for e0, e1, _ in events]
-    kb = [e1.elapsed_time(e2) for _, e1, e2 in events]
+    # Per-launch kernel durations.  multi: the step is ONE k_scan_multi launch,
+    # timed by the HIP events around it on its stream (it runs alone), so
+    # kernel_ms is that launch's duration.  batches: the timed steps run 4
+    # streams at once, so a launch's event span there includes time shared with
+    # the other streams' kernels (launch_span_ms_concurrent); kernel_ms is the
+    # duration of a stage-A launch alone on the GPU (exclusive_launches, after
+    # the timed region).  Both modes also report the per-batch kernels alone.
     excl = exclusive_launches(tab, scanners[0], streams[0], args.exclusive_batches)
-    rows_per_launch = float(args.batch_size)
     mean_k = tab.total_outputs / max(1, tab.rows)
-    algo_bytes = bytes_per_row(mean_k) * rows_per_launch
-    kernel_ms = excl["stage_a_ms"] or float(np.mean(ka))
-    achieved_gbs = algo_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = None
+    pmc = {}
     if os.path.exists(args.pmc_summary):
         with open(args.pmc_summary) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            pmc = json.load(f)
+    if multi:
+        spans = [e0.elapsed_time(e1) for e0, e1 in events]
+        kernel, kernel_ms, rows_per_launch, launches = "k_scan_multi", float(np.mean(spans)), float(tab.rows), 1
+        kernel_ms_how = ("the step's one k_scan_multi launch (both stages, all %d batches), HIP events on its stream "
+                         "around each timed step's call (descriptor upload and counter reset included)" % tab.nb)
+        per_row = pmc.get("multi_hbm_bytes_per_row")
+        traffic = per_row * rows_per_launch if per_row else None
+        extra = dict(per_batch_stage_a_ms_alone=excl["stage_a_ms"], per_batch_stage_b_ms_alone=excl["stage_b_ms"])
+    else:
+        ka = [e0.elapsed_time(e1) for e0, e1, _ in events]
+        kb = [e1.elapsed_time(e2) for _, e1, e2 in events]
+        kernel, rows_per_launch, launches = "k_shared_secret", float(args.batch_size), tab.nb
+        kernel_ms = excl["stage_a_ms"] or float(np.mean(ka))
+        kernel_ms_how = ("stage-A launch alone on the GPU: %d full batches on one stream after the timed steps, HIP "
+                         "events on that stream" % excl["launches"])
+        traffic = pmc.get("hbm_bytes_per_launch")
+        extra = dict(match_kernel_ms=excl["stage_b_ms"],
+                     launch_span_ms_concurrent=float(np.mean(ka)) if ka else None,
+                     match_launch_span_ms_concurrent=float(np.mean(kb)) if kb else None, streams=args.streams)
+    algo_bytes = bytes_per_row(mean_k) * rows_per_launch
+    achieved_gbs = algo_bytes / (kernel_ms * 1e-3) / 1e9
 
     rows_job = args.rows * (world if args.shard == "weak" else 1)  # rows all ranks scan per step
     value = rows_job * args.steps / total_s
     ms_per_step = total_s / args.steps * 1e3
     rows_gpu_step = rows_job / world
     step_gbs = bytes_per_row(mean_k) * rows_gpu_step / (ms_per_step * 1e-3) / 1e9
-    launches = tab.nb
     sq_path = args.pmc_sq or sq_profile_path(args)
-    alu = alu_roofline(sq_path, value / world)
+    alu = alu_roofline(sq_path, value / world, multi)
 
     result = dict(
         metric=METRIC, value=value, unit="tx/s", n_gpus=world, steps=args.steps, warmup=args.warmup,
@@ -669,21 +731,16 @@ def main():
                                  if args.shard == "roundrobin" else "every rank scans its own table (weak)"),
                     rows=args.rows, shard=args.shard, batch_size=args.batch_size, labels=args.labels,
                     output_count=args.output_count, label_negation=args.label_negation,
-                    outputs_per_row=round(mean_k, 3), fixed_base_bits=args.fb_bits, streams=args.streams,
-                    batches_rank0=launches, parallelism="dp%d" % world),
+                    outputs_per_row=round(mean_k, 3), fixed_base_bits=args.fb_bits, launch=args.launch,
+                    streams=1 if multi else args.streams, batches_rank0=tab.nb, parallelism="dp%d" % world),
         roofline=dict(bound="hbm", achieved=achieved_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                       frac=achieved_gbs / HBM_PEAK_GBS, traffic=traffic,
-                      kernel="k_shared_secret", kernel_ms=kernel_ms,
-                      kernel_ms_how="stage-A launch alone on the GPU: %d full batches on one stream after the "
-                                    "timed steps, HIP events on that stream" % excl["launches"],
-                      match_kernel_ms=excl["stage_b_ms"],
-                      launch_span_ms_concurrent=float(np.mean(ka)) if ka else None,
-                      match_launch_span_ms_concurrent=float(np.mean(kb)) if kb else None,
+                      kernel=kernel, kernel_ms=kernel_ms, kernel_ms_how=kernel_ms_how,
                       algorithmic_bytes_per_launch=algo_bytes, rows_per_launch=rows_per_launch,
-                      launches_per_step_rank0=launches, streams=args.streams,
+                      launches_per_step_rank0=launches,
                       step_achieved=step_gbs, step_frac=step_gbs / HBM_PEAK_GBS,
                       step_note="whole step: rows x (73 + 8k) B per GPU / ms_per_step",
-                      note="integer-VALU-bound path; see alu_roofline"),
+                      note="integer-VALU-bound path; see alu_roofline", **extra),
         alu_roofline=alu,
         matches=dict(found=found, flagged=flagged, expected_planted=expected,
                      label_indices_planted=sorted(tab.planted_labels) if labels else [],

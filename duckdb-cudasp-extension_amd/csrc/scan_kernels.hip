@@ -14,6 +14,7 @@
 // twice per batch; here nothing leaves the device between the two kernels.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -336,6 +337,166 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
         if (lane == 0) base = atomicAdd(match_count, (uint32_t)__popcll(m));
         base = __shfl(base, 0);
         if (hit) match_rows[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = row;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------ multi-batch persistent scan
+// cudasp_scan_device_batches: both stages of every row of several resident
+// batches in ONE persistent kernel.  The batches' rows form a virtual row
+// space in 64-row "wave-rows" (batch b starts at wave-row first_wr; its last
+// wave-row is padded, padding lanes compute batch row 0 and store nothing).
+// Each wavefront takes R consecutive wave-rows from a device counter (one
+// atomic per piece): R = RMAX rows per thread while more than g2 wave-rows
+// remain, then 2, then 1 below g1 -- guided self-scheduling, so the last
+// pieces are short and the GPU stays full to the end.  A thread's R rows share
+// one Z inversion in stage A (t stays in the thread), then one Z inversion and
+// one label inversion in stage B.  Exit: every wave leaves when the counter
+// passes the last wave-row.
+struct MultiBatch {
+  const uint32_t* tx;
+  const uint32_t* ty;
+  const int64_t* outputs;
+  const uint32_t* offs;
+  const uint32_t* lens;
+  uint8_t* flags;
+  uint32_t* match_rows;
+  uint32_t* match_count;
+  uint32_t n;
+  uint32_t first_wr;
+};
+
+// The batch holding wave-row w (w wave-uniform): the last batch with
+// first_wr <= w.
+__device__ __forceinline__ uint32_t multi_batch_of(const MultiBatch* __restrict__ bd, uint32_t nb, uint32_t w) {
+  uint32_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (bd[mid].first_wr <= w) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// Row of this lane in wave-row w of batch `b`; *active = false for the padding
+// of the batch's last wave-row (which then reads batch row 0).
+__device__ __forceinline__ uint32_t multi_row(const MultiBatch& b, uint32_t w, uint32_t lane, bool* active) {
+  const uint32_t r = (w - b.first_wr) * 64u + lane;
+  *active = r < b.n;
+  return *active ? r : 0u;
+}
+
+#ifndef CUDASP_MULTI_RMAX
+#define CUDASP_MULTI_RMAX 6
+#endif
+constexpr int MULTI_RMAX = CUDASP_MULTI_RMAX;  // rows per thread while much work remains (tuned)
+static_assert(MULTI_RMAX >= 2 && MULTI_RMAX <= 16, "multi-batch rows per thread");
+constexpr uint32_t multi_scratch_words(uint32_t label_count) {
+  return VB_SCRATCH_WORDS + PEND_WORDS * MULTI_RMAX + FW * label_count * MULTI_RMAX;
+}
+
+template <int FBB>
+__global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const MultiBatch* __restrict__ bd, uint32_t nb,
+                                                                   uint32_t total_wr, const int8_t* __restrict__ naf,
+                                                                   ScanConsts k, const uint32_t* __restrict__ fb,
+                                                                   const uint32_t* __restrict__ labels,
+                                                                   uint32_t* __restrict__ scr,
+                                                                   uint32_t* __restrict__ counter, uint32_t g1,
+                                                                   uint32_t g2) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const Scratch sc = make_scratch(scr, gridDim.x * blockDim.x, slot);
+  const uint32_t lane = threadIdx.x & 63u;
+  constexpr int PB = VB_SCRATCH_WORDS;                      // pending rows
+  constexpr int LB = VB_SCRATCH_WORDS + PEND_WORDS * MULTI_RMAX;  // label prefix products
+  for (;;) {
+    uint32_t base = 0, R = 1;
+    if (lane == 0) {
+      const uint32_t prev = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t rem = prev < total_wr ? total_wr - prev : 0u;
+      R = rem > g2 ? (uint32_t)MULTI_RMAX : (rem > g1 ? 2u : 1u);
+      base = atomicAdd(counter, R);
+    }
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+    R = (uint32_t)__builtin_amdgcn_readfirstlane((int)R);
+    if (base >= total_wr) break;
+    const int count = (int)(R < total_wr - base ? R : total_wr - base);
+    // stage A: S = d T of the thread's rows, one shared inversion
+#pragma unroll 1
+    for (int j = 0; j < count; j++) {
+      const uint32_t w = base + (uint32_t)j;
+      const MultiBatch& b = bd[multi_batch_of(bd, nb, w)];
+      bool active;
+      const uint32_t r = multi_row(b, w, lane, &active);
+      uint32_t x[8], y[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        x[q] = b.tx[(size_t)q * b.n + r];
+        y[q] = b.ty[(size_t)q * b.n + r];
+      }
+      gej P;
+      row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
+      pend_store(sc, PB, j, P);
+    }
+    pend_invert<MULTI_RMAX>(sc, PB, count);
+    // t of each row, then stage B's F = t G + B in the same pending slot
+#pragma unroll 1
+    for (int j = 0; j < count; j++) {
+      gej P;
+      fe zi;
+      pend_load(P, sc, PB, j);
+      scr_load(zi, sc, PEND_ZI(PB, j));
+      uint32_t sx[8], t[8];
+      const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
+      bip352_shared_secret_hash(t, k.mid, sx, y_odd);
+      gej F;
+      row_match_point<FBB>(F, t, fb, k);
+      pend_store(sc, PB, j, F);
+    }
+    pend_invert<MULTI_RMAX>(sc, PB, count);
+    uint32_t hits = 0;
+#pragma unroll 1
+    for (int j = 0; j < count; j++) {
+      const uint32_t w = base + (uint32_t)j;
+      const MultiBatch& b = bd[multi_batch_of(bd, nb, w)];
+      bool active;
+      const uint32_t r = multi_row(b, w, lane, &active);
+      gej P;
+      fe zi;
+      pend_load(P, sc, PB, j);
+      scr_load(zi, sc, PEND_ZI(PB, j));
+      if (row_match_base(P, zi, k, b.outputs, b.offs[r], b.lens[r], sc, PB, j, nullptr)) hits |= 1u << j;
+    }
+    if (k.label_count)
+      hits |= match_labels_core(k, labels, count, sc, PB, LB,
+                                [&](int j, const int64_t*& o, uint32_t& off, uint32_t& len, int64_t*& vrow,
+                                    uint32_t& vstride) {
+                                  const uint32_t w = base + (uint32_t)j;
+                                  const MultiBatch& b = bd[multi_batch_of(bd, nb, w)];
+                                  bool active;
+                                  const uint32_t r = multi_row(b, w, lane, &active);
+                                  o = b.outputs;
+                                  off = b.offs[r];
+                                  len = b.lens[r];
+                                  vrow = nullptr;
+                                  vstride = 0;
+                                });
+    // flags and compaction, one wave-row (= one batch) at a time
+#pragma unroll 1
+    for (int j = 0; j < count; j++) {
+      const uint32_t w = base + (uint32_t)j;
+      const MultiBatch& b = bd[multi_batch_of(bd, nb, w)];
+      bool active;
+      const uint32_t r = multi_row(b, w, lane, &active);
+      const bool hit = active && ((hits >> j) & 1u);
+      if (active) b.flags[r] = hit ? 1 : 0;
+      if (b.match_rows != nullptr) {
+        const uint64_t m = __ballot(hit);
+        if (m) {
+          uint32_t at = 0;
+          if (lane == 0) at = atomicAdd(b.match_count, (uint32_t)__popcll(m));
+          at = __shfl(at, 0);
+          if (hit) b.match_rows[at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = r;
+        }
       }
     }
   }
@@ -672,6 +833,16 @@ struct cudasp_scanner {
   uint32_t* d_lens = nullptr;
   int64_t* d_outputs = nullptr;
   size_t outputs_cap = 0;
+  // multi-batch persistent path (cudasp_scan_device_batches)
+  MultiBatch* d_multi = nullptr;   // batch descriptors on the device
+  MultiBatch* h_multi = nullptr;   // pinned staging of the descriptors
+  uint32_t multi_cap = 0;          // descriptors the two buffers hold
+  hipEvent_t multi_copied = nullptr;  // the last descriptor upload has been read
+  bool multi_pending = false;
+  uint32_t* d_counter = nullptr;   // the persistent kernel's work counter
+  uint32_t* d_mscratch = nullptr;  // mscratch_words u32
+  uint64_t mscratch_words = 0;
+  int cus = 0;
 };
 
 namespace {
@@ -759,10 +930,13 @@ void free_scanner(cudasp_scanner* s) {
   if (!s) return;
   DeviceGuard g(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  void* ptrs[] = {s->d_naf, s->d_labels, s->d_t,    s->d_vscratch, s->d_lscratch, s->d_rows, s->d_tx,
-                  s->d_ty,  s->d_flags,  s->d_offs, s->d_lens,     s->d_outputs,   s->d_vflags};
+  void* ptrs[] = {s->d_naf,  s->d_labels, s->d_t,       s->d_vscratch, s->d_lscratch, s->d_rows,
+                  s->d_tx,   s->d_ty,     s->d_flags,   s->d_offs,     s->d_lens,     s->d_outputs,
+                  s->d_vflags, s->d_multi, s->d_counter, s->d_mscratch};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (s->h_multi) (void)hipHostFree(s->h_multi);
+  if (s->multi_copied) (void)hipEventDestroy(s->multi_copied);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -1106,6 +1280,123 @@ int cudasp_scan_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint3
   return launch_pipeline(s, d_tweak_x, d_tweak_y, d_outputs, d_output_offsets, d_output_lengths, n, d_match_flags,
                          (d_match_rows && d_match_count) ? d_match_rows : nullptr,
                          (d_match_rows && d_match_count) ? d_match_count : nullptr, nullptr, nullptr, st);
+}
+
+// Guided-scheduling thresholds of k_scan_multi in units of the grid's waves:
+// 6 rows per thread while more than G2 x waves wave-rows remain, 2 while more
+// than G1 x waves, then 1 (CUDASP_MULTI_G1 / CUDASP_MULTI_G2 in hundredths
+// override them for tuning).
+static uint32_t multi_threshold(const char* env, uint32_t dflt_x100, uint32_t waves) {
+  uint32_t x = dflt_x100;
+  if (const char* e = getenv(env)) {
+    const long v = atol(e);
+    if (v >= 0 && v <= 100000) x = (uint32_t)v;
+  }
+  return (uint32_t)((uint64_t)waves * x / 100);
+}
+
+int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* batches, uint32_t count, void* stream) {
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  if (count == 0) return CUDASP_OK;
+  if (!batches) return set_error(CUDASP_ERR_INVALID_ARG, "null batch array");
+  for (uint32_t i = 0; i < count; i++) {
+    const cudasp_device_batch& b = batches[i];
+    if (b.n && (!b.tweak_x || !b.tweak_y || !b.output_offsets || !b.output_lengths || !b.match_flags))
+      return set_error(CUDASP_ERR_INVALID_ARG, "batch %u: null device buffer", i);
+  }
+  const bool persistent = s->consts.output_count == 1 && (s->fb_bits == 22 || s->fb_bits == 26);
+  if (!persistent) {  // the per-batch path (protocol variants, the LDS width)
+    for (uint32_t i = 0; i < count; i++) {
+      const cudasp_device_batch& b = batches[i];
+      int rc = cudasp_scan_device(s, b.tweak_x, b.tweak_y, b.outputs, b.output_offsets, b.output_lengths, b.n,
+                                  b.match_flags, b.match_rows, b.match_count, stream);
+      if (rc != CUDASP_OK) return rc;
+    }
+    return CUDASP_OK;
+  }
+  DeviceGuard g(s->device);
+  hipStream_t st = scanner_stream(s, stream);
+  // descriptors: batches with rows only, each starting at a fresh wave-row
+  std::vector<MultiBatch> md;
+  md.reserve(count);
+  uint64_t total_wr = 0;
+  for (uint32_t i = 0; i < count; i++) {
+    const cudasp_device_batch& b = batches[i];
+    if (b.n == 0) continue;
+    MultiBatch m;
+    m.tx = b.tweak_x;
+    m.ty = b.tweak_y;
+    m.outputs = b.outputs;
+    m.offs = b.output_offsets;
+    m.lens = b.output_lengths;
+    m.flags = b.match_flags;
+    const bool compact = b.match_rows && b.match_count;
+    m.match_rows = compact ? b.match_rows : nullptr;
+    m.match_count = compact ? b.match_count : nullptr;
+    m.n = b.n;
+    m.first_wr = (uint32_t)total_wr;
+    total_wr += (b.n + 63u) / 64u;
+    md.push_back(m);
+  }
+  if (md.empty()) return CUDASP_OK;
+  if (total_wr >= (1ull << 31)) return set_error(CUDASP_ERR_CAPACITY, "too many rows in one multi-batch call");
+  const uint32_t nb = (uint32_t)md.size();
+  if (s->multi_pending) {  // the previous upload must have been read before the staging is reused
+    HIP_TRY(hipEventSynchronize(s->multi_copied));
+    s->multi_pending = false;
+  }
+  if (nb > s->multi_cap) {
+    if (s->d_multi) HIP_TRY(hipFree(s->d_multi));
+    if (s->h_multi) HIP_TRY(hipHostFree(s->h_multi));
+    s->d_multi = nullptr;
+    s->h_multi = nullptr;
+    s->multi_cap = 0;
+    const uint32_t cap = nb < 256 ? 256 : nb;
+    HIP_TRY(hipMalloc(&s->d_multi, (size_t)cap * sizeof(MultiBatch)));
+    HIP_TRY(hipHostMalloc((void**)&s->h_multi, (size_t)cap * sizeof(MultiBatch), hipHostMallocDefault));
+    s->multi_cap = cap;
+  }
+  if (!s->multi_copied) HIP_TRY(hipEventCreateWithFlags(&s->multi_copied, hipEventDisableTiming));
+  if (!s->d_counter) HIP_TRY(hipMalloc(&s->d_counter, sizeof(uint32_t)));
+  if (!s->cus) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus <= 0)
+      cus = 256;
+    s->cus = cus;
+  }
+  // persistent grid: CUDASP_WAVES_A waves per SIMD (one 256-thread block = one
+  // wave per SIMD of a CU), no more waves than wave-rows, within 4 GiB of scratch
+  const uint64_t words = multi_scratch_words(s->consts.label_count);
+  uint64_t blocks = (uint64_t)s->cus * CUDASP_WAVES_A;
+  const uint64_t need_blocks = (total_wr + 3) / 4;
+  if (blocks > need_blocks) blocks = need_blocks;
+  const uint64_t cap_blocks = ((1ull << 32) - 1) / 4 / (words * BLOCK);
+  if (blocks > cap_blocks) blocks = cap_blocks;
+  if (blocks == 0) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the multi-batch path");
+  const uint64_t need_words = blocks * BLOCK * words;
+  if (need_words > s->mscratch_words) {
+    HIP_TRY(hipStreamSynchronize(st));  // no kernel of this scanner still uses the old scratch
+    if (s->d_mscratch) HIP_TRY(hipFree(s->d_mscratch));
+    s->d_mscratch = nullptr;
+    s->mscratch_words = 0;
+    // sized for the full grid, so later calls with more rows reuse it
+    const uint64_t full = std::min<uint64_t>((uint64_t)s->cus * CUDASP_WAVES_A, cap_blocks) * BLOCK * words;
+    HIP_TRY(hipMalloc(&s->d_mscratch, (size_t)full * 4));
+    s->mscratch_words = full;
+  }
+  memcpy(s->h_multi, md.data(), (size_t)nb * sizeof(MultiBatch));
+  HIP_TRY(hipMemcpyAsync(s->d_multi, s->h_multi, (size_t)nb * sizeof(MultiBatch), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipEventRecord(s->multi_copied, st));
+  s->multi_pending = true;
+  HIP_TRY(hipMemsetAsync(s->d_counter, 0, sizeof(uint32_t), st));
+  const uint32_t waves = (uint32_t)blocks * (BLOCK / 64);
+  const uint32_t g1 = multi_threshold("CUDASP_MULTI_G1", 150, waves);
+  const uint32_t g2 = multi_threshold("CUDASP_MULTI_G2", 400, waves);
+  hipLaunchKernelGGL(s->fb_bits == 26 ? k_scan_multi<26> : k_scan_multi<22>, dim3((uint32_t)blocks), dim3(BLOCK), 0,
+                     st, s->d_multi, nb, (uint32_t)total_wr, s->d_naf, s->consts, s->d_fb, s->d_labels,
+                     s->d_mscratch, s->d_counter, g1, g2);
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
 }
 
 int cudasp_row_values_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint32_t* d_tweak_y, uint32_t n,

@@ -698,15 +698,16 @@ CUDASP_HD bool row_match_base(const gej& R, const fe& zi, const ScanConsts& k, c
   return outputs_match(k, outputs, off, len, F.x, v);
 }
 
-// Label sums F_j + L_l of a thread's pending rows j < count (rows g + j G),
-// all with ONE batched inversion over the count x L denominators (Montgomery's
-// trick; prefix products at scratch words (j L + l) FW) instead of one per
-// row.  Same values and hits as row_match_finish.  Returns the rows with a
-// label hit as a bit mask; with `values` (then outputs/offs/lens unused) the
-// label values go to values[(1 + l) n + row].
-CUDASP_HD uint32_t match_labels_rows(const ScanConsts& k, const uint32_t* labels, const int64_t* outputs,
-                                     const uint32_t* offs, const uint32_t* lens, uint32_t g, uint32_t G, uint32_t n,
-                                     uint32_t n_rows, int count, const Scratch& sc, int pb, int64_t* values) {
+// Label sums F_j + L_l of a thread's pending rows j < count, all with ONE
+// batched inversion over the count x L denominators (Montgomery's trick;
+// prefix products at scratch words lb + (j L + l) FW) instead of one per row.
+// Same values and hits as row_match_finish.  Returns the rows with a label hit
+// as a bit mask.  row_out(j, outputs, off, len, vrow, vstride) gives row j's
+// outputs list and, if vrow != nullptr, where its label values go
+// (vrow[(1 + l) vstride]).
+template <class RowOut>
+CUDASP_HD uint32_t match_labels_core(const ScanConsts& k, const uint32_t* labels, int count, const Scratch& sc, int pb,
+                                     int lb, const RowOut& row_out) {
   const int L = (int)k.label_count;
   fe acc;
   fe_set_int(acc, 1);
@@ -719,7 +720,7 @@ CUDASP_HD uint32_t match_labels_rows(const ScanConsts& k, const uint32_t* labels
       ge_from_words(Ll, labels + (size_t)l * 16);
       fe d;
       label_terms(d, nullptr, F, Ll);
-      scr_store(sc, (j * L + l) * FW, acc);
+      scr_store(sc, lb + (j * L + l) * FW, acc);
       fe_mul(acc, acc, d);
     }
   }
@@ -727,10 +728,10 @@ CUDASP_HD uint32_t match_labels_rows(const ScanConsts& k, const uint32_t* labels
   fe_inv(inv, acc);
   uint32_t hits = 0;
   for (int j = count - 1; j >= 0; j--) {
-    const uint32_t row = g + (uint32_t)j * G;
-    const uint32_t orow = n == n_rows ? row : row % n_rows;
-    const uint32_t off = values ? 0u : offs[orow];
-    const uint32_t len = values ? 0u : lens[orow];
+    const int64_t* outputs;
+    uint32_t off, len, vstride;
+    int64_t* vrow;
+    row_out(j, outputs, off, len, vrow, vstride);
     ge F;
     scr_load(F.x, sc, PEND_X(pb, j));
     scr_load(F.y, sc, PEND_Y(pb, j));
@@ -740,7 +741,7 @@ CUDASP_HD uint32_t match_labels_rows(const ScanConsts& k, const uint32_t* labels
       ge_from_words(Ll, labels + (size_t)l * 16);
       fe d, num, pre, dinv;
       const bool infinity = label_terms(d, &num, F, Ll);
-      scr_load(pre, sc, (j * L + l) * FW);
+      scr_load(pre, sc, lb + (j * L + l) * FW);
       fe_mul(dinv, inv, pre);
       fe_mul(inv, inv, d);
       fe lam, x3;
@@ -750,12 +751,32 @@ CUDASP_HD uint32_t match_labels_rows(const ScanConsts& k, const uint32_t* labels
       fe_sub<1>(x3, x3, Ll.x);
       fe_normalize(x3);
       const int64_t vl = infinity ? LABEL_INFINITY : fe_upper64(x3);
-      if (values) values[(size_t)(1 + l) * n + row] = vl;
+      if (vrow) vrow[(size_t)(1 + l) * vstride] = vl;
       if (!infinity) hit = hit || outputs_match(k, outputs, off, len, x3, vl);
     }
     if (hit) hits |= 1u << j;
   }
   return hits;
+}
+
+// match_labels_core for the rows g + j G of one batch (k_match, the
+// emulation): outputs lists by input row (virtual row mod n_rows), label
+// values (with `values`, then outputs/offs/lens unused) to
+// values[(1 + l) n + row]; label prefix products from scratch word 0.
+CUDASP_HD uint32_t match_labels_rows(const ScanConsts& k, const uint32_t* labels, const int64_t* outputs,
+                                     const uint32_t* offs, const uint32_t* lens, uint32_t g, uint32_t G, uint32_t n,
+                                     uint32_t n_rows, int count, const Scratch& sc, int pb, int64_t* values) {
+  return match_labels_core(k, labels, count, sc, pb, 0,
+                           [&](int j, const int64_t*& o, uint32_t& off, uint32_t& len, int64_t*& vrow,
+                               uint32_t& vstride) {
+                             const uint32_t row = g + (uint32_t)j * G;
+                             const uint32_t orow = n == n_rows ? row : row % n_rows;
+                             o = outputs;
+                             off = values ? 0u : offs[orow];
+                             len = values ? 0u : lens[orow];
+                             vrow = values ? values + row : nullptr;
+                             vstride = n;
+                           });
 }
 
 // Stage B for one row (one inversion per row).

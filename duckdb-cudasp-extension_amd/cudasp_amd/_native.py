@@ -37,6 +37,7 @@ SIGNATURES = {
     "cudasp_scan_device": (_I32, [_P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "cudasp_scan_host": (_I32, [_P, _P, _P, ctypes.c_size_t, _P, _P, _U32, _P]),
     "cudasp_row_values_device": (_I32, [_P, _P, _P, _U32, _P, _P, _P]),
+    "cudasp_scan_device_batches": (_I32, [_P, _P, _U32, _P]),
     "cudasp_scanner_sync": (_I32, [_P]),
     "cudasp_tweaks_to_columns": (_I32, [_P, _U32, _P, _P, _P]),
     "cudasp_stage_shared_secret_device": (_I32, [_P, _P, _P, _U32, _P, _P]),
@@ -93,6 +94,13 @@ def check(rc):
 
 CUDASP_STREAM_DEFAULT = 1  # include/cudasp_abi.h: the device's null stream
 CUDASP_MAX_OUTPUT_COUNT = 64
+
+
+class DeviceBatch(ctypes.Structure):
+    """cudasp_device_batch (include/cudasp_abi.h)."""
+    _fields_ = [("tweak_x", _P), ("tweak_y", _P), ("outputs", _P), ("output_offsets", _P),
+                ("output_lengths", _P), ("n", _U32), ("match_flags", _P), ("match_rows", _P),
+                ("match_count", _P)]
 
 
 class ScanOptions(ctypes.Structure):

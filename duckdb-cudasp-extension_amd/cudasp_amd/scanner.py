@@ -130,6 +130,21 @@ class Scanner:
             self._h, _ptr(tweak_x), _ptr(tweak_y), _ptr(outputs), _ptr(offsets), _ptr(lengths), n,
             _ptr(flags), _ptr(match_rows), _ptr(match_count), st))
 
+    def scan_device_batches(self, batches, stream=None):
+        """Asynchronous scan of several device-resident batches in one call
+        (cudasp_scan_device_batches: one persistent kernel for both stages).
+        batches: sequence of dicts with the keys of scan_device (tweak_x,
+        tweak_y, outputs, offsets, lengths, flags, optional match_rows /
+        match_count); n is flags.numel()."""
+        arr = (_native.DeviceBatch * max(1, len(batches)))()
+        for i, b in enumerate(batches):
+            arr[i] = _native.DeviceBatch(
+                _ptr(b["tweak_x"]), _ptr(b["tweak_y"]), _ptr(b.get("outputs")), _ptr(b["offsets"]),
+                _ptr(b["lengths"]), int(b["flags"].numel()), _ptr(b["flags"]), _ptr(b.get("match_rows")),
+                _ptr(b.get("match_count")))
+        st = self._stream(stream)
+        _native.check(self._lib.cudasp_scan_device_batches(self._h, arr, len(batches), st))
+
     def row_values_device(self, tweak_x, tweak_y, t_out, values, stream=None):
         n = int(tweak_x.numel() // 8)
         st = self._stream(stream)

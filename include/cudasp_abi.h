@@ -148,6 +148,32 @@ int cudasp_scan_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint3
                        const uint32_t* d_output_lengths, uint32_t n, uint8_t* d_match_flags,
                        uint32_t* d_match_rows, uint32_t* d_match_count, void* stream);
 
+/* Several device-resident batches in one call (e.g. a rank's share of a
+ * resident table): the same flags, and the same match rows and counts per
+ * batch, as cudasp_scan_device on each batch in turn.  With the default
+ * options (output_count 1) and an HBM fixed-base width (22 or 26 bits) one
+ * persistent kernel runs both stages over all rows of all batches: every
+ * wavefront takes 64-row pieces from a device work counter, up to 6 per thread
+ * (sharing one inversion) while much work remains and 2, then 1 as it runs out,
+ * so the GPU stays full to the end and t never leaves the thread.  Otherwise
+ * the batches go through cudasp_scan_device one after the other.  Batch sizes
+ * are not bounded by the scanner's capacity on the persistent path (the
+ * per-batch path needs n <= capacity).  Asynchronous on `stream`; the
+ * descriptor array is read before the call returns.  match_count words are
+ * added to (the caller zeroes them). */
+typedef struct {
+  const uint32_t* tweak_x;          /* 8 x n, column-major */
+  const uint32_t* tweak_y;
+  const int64_t* outputs;
+  const uint32_t* output_offsets;   /* n */
+  const uint32_t* output_lengths;   /* n */
+  uint32_t n;
+  uint8_t* match_flags;             /* n, required */
+  uint32_t* match_rows;             /* optional, with match_count */
+  uint32_t* match_count;
+} cudasp_device_batch;
+int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* batches, uint32_t count, void* stream);
+
 /* Host batch, synchronous: tweak keys as n 64-byte blobs back to back, the
  * outputs CSR in host memory; writes h_match_flags[n]. */
 int cudasp_scan_host(cudasp_scanner* s, const uint8_t* h_tweak_keys, const int64_t* h_outputs,

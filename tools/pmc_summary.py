@@ -22,7 +22,7 @@ import csv
 import json
 import re
 
-SCAN_KERNELS = ("k_shared_secret", "void k_match<false>", "void k_match<true>", "k_layout_probe")
+SCAN_KERNELS = ("k_shared_secret", "void k_match<false>", "void k_match<true>", "k_layout_probe", "k_scan_multi")
 
 
 def kernel_key(name):
@@ -31,6 +31,8 @@ def kernel_key(name):
     plain names bench.py looks up, the small-launch instances (rows_a_for,
     rows_b_for) stay separate."""
     k = name.split("(")[0]
+    if re.fullmatch(r"void k_scan_multi<\d+>", k):  # the multi-batch kernel, any fixed-base width
+        return "k_scan_multi"
     m = re.fullmatch(r"void k_shared_secret<(\d+)>", k)
     if m:
         k = "k_shared_secret" if m.group(1) == "4" else "k_shared_secret<%s>" % m.group(1)
@@ -78,9 +80,13 @@ def main():
     ap.add_argument("--algorithmic-bytes-per-row", type=float, default=89.0)
     ap.add_argument("--probe-rows", type=int, default=0)
     ap.add_argument("--probe-outputs-per-row", type=float, default=2.0)
+    ap.add_argument("--multi-rows", type=int, default=0,
+                    help="rows of one k_scan_multi launch (cudasp_scan_device_batches) in the profiled run")
     a = ap.parse_args()
     if a.mode == "sq":
         res = dict(source=a.source, shape=a.shape, rows_per_launch=a.rows, per_kernel=averages(load(a.csvs)))
+        if a.multi_rows:
+            res["multi_rows_per_launch"] = a.multi_rows
     else:
         fetch = averages(load([a.csvs[0]]))
         write = averages(load([a.csvs[1]]))
@@ -99,6 +105,9 @@ def main():
                    per_kernel=per, kernel="k_shared_secret", hbm_bytes_per_launch=hbm("k_shared_secret"),
                    match_kernel_hbm_bytes_per_launch=hbm("void k_match<false>"), rows_per_launch=a.rows,
                    algorithmic_bytes_per_launch=a.algorithmic_bytes_per_row * a.rows)
+        if a.multi_rows and hbm("k_scan_multi"):
+            res.update(multi_rows_per_launch=a.multi_rows,
+                       multi_hbm_bytes_per_row=hbm("k_scan_multi") / a.multi_rows)
         pv = per.get("k_layout_probe")
         if pv and a.probe_rows:
             read = a.probe_rows * (72 + 8 * a.probe_outputs_per_row)
