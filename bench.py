@@ -510,11 +510,11 @@ def cpu_baseline_optimized(smp, labels, threads):
 
 
 def sq_profile_path(args):
-    """The PMC instruction-count summary matching this run's shape (labels,
-    outputs per row, fixed-base width, variants):
-    profiles/r02_pmc_sq_L<labels>_k<outputs>_w<bits>[_neg][_K<k>].json."""
+    """The PMC instruction-count summary matching this run's shape (launch
+    mode, labels, outputs per row, fixed-base width, variants):
+    profiles/r02_pmc_sq_[multi_]L<labels>_k<outputs>_w<bits>[_neg][_K<k>].json."""
     kdesc = "1-%d" % args.outputs_max if args.outputs_max else str(args.outputs_per_row)
-    name = "r02_pmc_sq_L%d_k%s_w%d" % (args.labels, kdesc, args.fb_bits)
+    name = "r02_pmc_sq_%sL%d_k%s_w%d" % ("multi_" if args.launch == "multi" else "", args.labels, kdesc, args.fb_bits)
     if args.label_negation:
         name += "_neg"
     if args.output_count != 1:
@@ -595,11 +595,16 @@ def main():
     ap.add_argument("--e2e-threads", type=int, default=8)
     ap.add_argument("--e2e-hw-queues", type=int, default=16)
     ap.add_argument("--e2e-timeout", type=int, default=420)
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02_pmc_hbm_k_shared_secret.json"))
+    ap.add_argument("--pmc-summary", default="",
+                    help="HBM traffic summary (default: profiles/r02_pmc_hbm_multi.json with --launch multi, "
+                         "profiles/r02_pmc_hbm_k_shared_secret.json with --launch batches)")
     ap.add_argument("--pmc-sq", default="", help="SQ counter summary (default: the file matching this run's shape)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) for the barrier/max; gloo to rehearse "
                     "several ranks on one GPU")
     args = ap.parse_args()
+    if not args.pmc_summary:
+        args.pmc_summary = os.path.join(ROOT, "profiles", "r02_pmc_hbm_multi.json" if args.launch == "multi"
+                                        else "r02_pmc_hbm_k_shared_secret.json")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
