@@ -130,7 +130,14 @@ typedef struct {
  * Not concurrent with work in flight on the scanner. */
 int cudasp_scanner_set_options(cudasp_scanner* s, const cudasp_scan_options* options);
 
-/* Stream arguments: a hipStream_t; NULL = the scanner's own stream (for the
+/* Concurrency: a scanner's launches share its scratch and staging buffers, so
+ * two launches of ONE scanner must not run at the same time -- issue them on
+ * one stream (or order them).  Use one scanner per stream for concurrent
+ * batches (the table-function host keeps one per executor thread; bench.py
+ * one per stream).  Scanners of one device share only the read-only
+ * fixed-base table.
+ *
+ * Stream arguments: a hipStream_t; NULL = the scanner's own stream (for the
  * entry points without a scanner: the null stream); CUDASP_STREAM_DEFAULT =
  * the device's null stream, for callers whose current stream is the default
  * stream (its handle is 0, which would otherwise select the scanner's stream
