@@ -348,9 +348,10 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 // space in 64-row "wave-rows" (batch b starts at wave-row first_wr; its last
 // wave-row is padded, padding lanes compute batch row 0 and store nothing).
 // Each wavefront takes R consecutive wave-rows from a device counter (one
-// atomic per piece): R = RMAX rows per thread while more than g2 wave-rows
-// remain, then 2, then 1 below g1 -- guided self-scheduling, so the last
-// pieces are short and the GPU stays full to the end.  A thread's R rows share
+// atomic per piece): R = rmax (<= MULTI_RMAX) rows per thread while more than
+// g2 wave-rows remain, then 2, then 1 below g1 -- guided self-scheduling, so
+// the last pieces are short and the GPU stays full to the end (a fused
+// single-batch launch uses g1 = g2 = 0: rmax rows per thread throughout).  A thread's R rows share
 // one Z inversion in stage A (t stays in the thread), then one Z inversion and
 // one label inversion in stage B.  Exit: every wave leaves when the counter
 // passes the last wave-row.
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
                                                                    const uint32_t* __restrict__ labels,
                                                                    uint32_t* __restrict__ scr,
                                                                    uint32_t* __restrict__ counter, uint32_t g1,
-                                                                   uint32_t g2) {
+                                                                   uint32_t g2, uint32_t rmax) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = make_scratch(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
     if (lane == 0) {
       const uint32_t prev = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t rem = prev < total_wr ? total_wr - prev : 0u;
-      R = rem > g2 ? (uint32_t)MULTI_RMAX : (rem > g1 ? 2u : 1u);
+      R = rem > g2 ? rmax : (rem > g1 ? 2u : 1u);
       base = atomicAdd(counter, R);
     }
     base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
@@ -843,6 +844,11 @@ struct cudasp_scanner {
   uint32_t* d_mscratch = nullptr;  // mscratch_words u32
   uint64_t mscratch_words = 0;
   int cus = 0;
+  // cudasp_scan_device / cudasp_scan_host through one k_scan_multi launch
+  // (both stages fused, t kept in the thread) instead of the two stage kernels;
+  // CUDASP_FUSED_SINGLE=0 selects the two kernels (A/B; the stage entry points,
+  // the values path, forced launch shapes and the variants always use them)
+  bool fused_single = true;
 };
 
 namespace {
@@ -1011,11 +1017,117 @@ int launch_match(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t
   return CUDASP_OK;
 }
 
+// Guided-scheduling thresholds of k_scan_multi in hundredths of the grid's
+// waves: 6 rows per thread while more than G2 x waves wave-rows remain, 2
+// while more than G1 x waves, then 1 (CUDASP_MULTI_G1 / CUDASP_MULTI_G2
+// override the defaults for tuning).
+static uint32_t multi_threshold_x100(const char* env, uint32_t dflt_x100) {
+  if (const char* e = getenv(env)) {
+    const long v = atol(e);
+    if (v >= 0 && v <= 100000) return (uint32_t)v;
+  }
+  return dflt_x100;
+}
+
+static MultiBatch multi_desc(const uint32_t* tx, const uint32_t* ty, const int64_t* outputs, const uint32_t* offs,
+                             const uint32_t* lens, uint32_t n, uint8_t* flags, uint32_t* match_rows,
+                             uint32_t* match_count, uint64_t first_wr) {
+  MultiBatch m;
+  m.tx = tx;
+  m.ty = ty;
+  m.outputs = outputs;
+  m.offs = offs;
+  m.lens = lens;
+  m.flags = flags;
+  const bool compact = match_rows && match_count;
+  m.match_rows = compact ? match_rows : nullptr;
+  m.match_count = compact ? match_count : nullptr;
+  m.n = n;
+  m.first_wr = (uint32_t)first_wr;
+  return m;
+}
+
+// One k_scan_multi launch over the described batches (total_wr wave-rows):
+// uploads the descriptors, resets the work counter, launches on `st`.  rmax:
+// rows per thread of the bulk; g1/g2: guided thresholds (hundredths of the
+// grid's waves); blocks: 0 = the persistent grid (every wave slot), else a
+// grid of that many blocks.
+static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, uint64_t total_wr, hipStream_t st,
+                        uint32_t rmax, uint32_t g1_x100, uint32_t g2_x100, uint64_t blocks_req) {
+  if (total_wr >= (1ull << 31)) return set_error(CUDASP_ERR_CAPACITY, "too many rows in one multi-batch call");
+  const uint32_t nb = (uint32_t)md.size();
+  if (s->multi_pending) {  // the previous upload must have been read before the staging is reused
+    HIP_TRY(hipEventSynchronize(s->multi_copied));
+    s->multi_pending = false;
+  }
+  if (nb > s->multi_cap) {
+    if (s->d_multi) HIP_TRY(hipFree(s->d_multi));
+    if (s->h_multi) HIP_TRY(hipHostFree(s->h_multi));
+    s->d_multi = nullptr;
+    s->h_multi = nullptr;
+    s->multi_cap = 0;
+    const uint32_t cap = nb < 256 ? 256 : nb;
+    HIP_TRY(hipMalloc(&s->d_multi, (size_t)cap * sizeof(MultiBatch)));
+    HIP_TRY(hipHostMalloc((void**)&s->h_multi, (size_t)cap * sizeof(MultiBatch), hipHostMallocDefault));
+    s->multi_cap = cap;
+  }
+  if (!s->multi_copied) HIP_TRY(hipEventCreateWithFlags(&s->multi_copied, hipEventDisableTiming));
+  if (!s->d_counter) HIP_TRY(hipMalloc(&s->d_counter, sizeof(uint32_t)));
+  if (!s->cus) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus <= 0)
+      cus = 256;
+    s->cus = cus;
+  }
+  // grid: at most CUDASP_WAVES_A waves per SIMD (one 256-thread block = one
+  // wave per SIMD of a CU), no more waves than wave-rows, within 4 GiB of scratch
+  const uint64_t words = multi_scratch_words(s->consts.label_count);
+  const uint64_t full_blocks = (uint64_t)s->cus * CUDASP_WAVES_A;
+  const uint64_t cap_blocks = ((1ull << 32) - 1) / 4 / (words * BLOCK);
+  uint64_t blocks = blocks_req ? blocks_req : full_blocks;
+  if (blocks > full_blocks) blocks = full_blocks;
+  const uint64_t need_blocks = (total_wr + 3) / 4;
+  if (blocks > need_blocks) blocks = need_blocks;
+  if (blocks > cap_blocks) blocks = cap_blocks;
+  if (blocks == 0) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the multi-batch path");
+  const uint64_t need_words = blocks * BLOCK * words;
+  if (need_words > s->mscratch_words) {
+    HIP_TRY(hipStreamSynchronize(st));  // no kernel of this scanner still uses the old scratch
+    if (s->d_mscratch) HIP_TRY(hipFree(s->d_mscratch));
+    s->d_mscratch = nullptr;
+    s->mscratch_words = 0;
+    // sized for the full grid, so later calls with more rows reuse it
+    const uint64_t full = std::min<uint64_t>(full_blocks, cap_blocks) * BLOCK * words;
+    HIP_TRY(hipMalloc(&s->d_mscratch, (size_t)full * 4));
+    s->mscratch_words = full;
+  }
+  memcpy(s->h_multi, md.data(), (size_t)nb * sizeof(MultiBatch));
+  HIP_TRY(hipMemcpyAsync(s->d_multi, s->h_multi, (size_t)nb * sizeof(MultiBatch), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipEventRecord(s->multi_copied, st));
+  s->multi_pending = true;
+  HIP_TRY(hipMemsetAsync(s->d_counter, 0, sizeof(uint32_t), st));
+  const uint64_t waves = blocks * (BLOCK / 64);
+  const uint32_t g1 = (uint32_t)(waves * g1_x100 / 100), g2 = (uint32_t)(waves * g2_x100 / 100);
+  hipLaunchKernelGGL(s->fb_bits == 26 ? k_scan_multi<26> : k_scan_multi<22>, dim3((uint32_t)blocks), dim3(BLOCK), 0,
+                     st, s->d_multi, nb, (uint32_t)total_wr, s->d_naf, s->consts, s->d_fb, s->d_labels,
+                     s->d_mscratch, s->d_counter, g1, g2, rmax);
+  HIP_TRY(hipGetLastError());
+  return CUDASP_OK;
+}
+
 int launch_pipeline(cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, const int64_t* outputs,
                     const uint32_t* offs, const uint32_t* lens, uint32_t n, uint8_t* flags, uint32_t* match_rows,
                     uint32_t* match_count, int64_t* values, uint32_t* t_out, hipStream_t st) {
   if (n == 0) return CUDASP_OK;
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
+  if (s->fused_single && !values && !t_out && flags && s->consts.output_count == 1 &&
+      (s->fb_bits == 22 || s->fb_bits == 26) && !s->rows_a_force && !s->rows_b_force) {
+    // both stages in one k_scan_multi launch over this batch: ROWS_A rows per
+    // thread throughout, one wave per chunk
+    std::vector<MultiBatch> md(1, multi_desc(tx, ty, outputs, offs, lens, n, flags, match_rows, match_count, 0));
+    const uint64_t wr = (n + 63u) / 64u;
+    return launch_multi(s, md, wr, st, ROWS_A, 0, 0, (wr + ROWS_A * 4 - 1) / (ROWS_A * 4));
+  }
   uint32_t* t = t_out ? t_out : s->d_t;
   launch_a(s, tx, ty, n, t, st);
   HIP_TRY(hipGetLastError());
@@ -1097,6 +1209,7 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
     // a quarter of the wave slots (4 SIMDs per CU, CUDASP_WAVES_A waves each)
     s->fill_threads = (uint32_t)cus * 4 * CUDASP_WAVES_A * 64 / 4;
     s->fill_threads_b = (uint32_t)cus * 4 * CUDASP_WAVES_B * 64 / 4;
+    if (const char* f = getenv("CUDASP_FUSED_SINGLE")) s->fused_single = atoi(f) != 0;
     if (const char* f = getenv("CUDASP_ROWS_A_FORCE")) {
       const int r = atoi(f);
       if (r == 1 || r == 2 || r == ROWS_A) s->rows_a_force = r;
@@ -1282,19 +1395,6 @@ int cudasp_scan_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint3
                          (d_match_rows && d_match_count) ? d_match_count : nullptr, nullptr, nullptr, st);
 }
 
-// Guided-scheduling thresholds of k_scan_multi in units of the grid's waves:
-// 6 rows per thread while more than G2 x waves wave-rows remain, 2 while more
-// than G1 x waves, then 1 (CUDASP_MULTI_G1 / CUDASP_MULTI_G2 in hundredths
-// override them for tuning).
-static uint32_t multi_threshold(const char* env, uint32_t dflt_x100, uint32_t waves) {
-  uint32_t x = dflt_x100;
-  if (const char* e = getenv(env)) {
-    const long v = atol(e);
-    if (v >= 0 && v <= 100000) x = (uint32_t)v;
-  }
-  return (uint32_t)((uint64_t)waves * x / 100);
-}
-
 int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* batches, uint32_t count, void* stream) {
   if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
   if (count == 0) return CUDASP_OK;
@@ -1323,80 +1423,13 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
   for (uint32_t i = 0; i < count; i++) {
     const cudasp_device_batch& b = batches[i];
     if (b.n == 0) continue;
-    MultiBatch m;
-    m.tx = b.tweak_x;
-    m.ty = b.tweak_y;
-    m.outputs = b.outputs;
-    m.offs = b.output_offsets;
-    m.lens = b.output_lengths;
-    m.flags = b.match_flags;
-    const bool compact = b.match_rows && b.match_count;
-    m.match_rows = compact ? b.match_rows : nullptr;
-    m.match_count = compact ? b.match_count : nullptr;
-    m.n = b.n;
-    m.first_wr = (uint32_t)total_wr;
+    md.push_back(multi_desc(b.tweak_x, b.tweak_y, b.outputs, b.output_offsets, b.output_lengths, b.n, b.match_flags,
+                            b.match_rows, b.match_count, total_wr));
     total_wr += (b.n + 63u) / 64u;
-    md.push_back(m);
   }
   if (md.empty()) return CUDASP_OK;
-  if (total_wr >= (1ull << 31)) return set_error(CUDASP_ERR_CAPACITY, "too many rows in one multi-batch call");
-  const uint32_t nb = (uint32_t)md.size();
-  if (s->multi_pending) {  // the previous upload must have been read before the staging is reused
-    HIP_TRY(hipEventSynchronize(s->multi_copied));
-    s->multi_pending = false;
-  }
-  if (nb > s->multi_cap) {
-    if (s->d_multi) HIP_TRY(hipFree(s->d_multi));
-    if (s->h_multi) HIP_TRY(hipHostFree(s->h_multi));
-    s->d_multi = nullptr;
-    s->h_multi = nullptr;
-    s->multi_cap = 0;
-    const uint32_t cap = nb < 256 ? 256 : nb;
-    HIP_TRY(hipMalloc(&s->d_multi, (size_t)cap * sizeof(MultiBatch)));
-    HIP_TRY(hipHostMalloc((void**)&s->h_multi, (size_t)cap * sizeof(MultiBatch), hipHostMallocDefault));
-    s->multi_cap = cap;
-  }
-  if (!s->multi_copied) HIP_TRY(hipEventCreateWithFlags(&s->multi_copied, hipEventDisableTiming));
-  if (!s->d_counter) HIP_TRY(hipMalloc(&s->d_counter, sizeof(uint32_t)));
-  if (!s->cus) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus <= 0)
-      cus = 256;
-    s->cus = cus;
-  }
-  // persistent grid: CUDASP_WAVES_A waves per SIMD (one 256-thread block = one
-  // wave per SIMD of a CU), no more waves than wave-rows, within 4 GiB of scratch
-  const uint64_t words = multi_scratch_words(s->consts.label_count);
-  uint64_t blocks = (uint64_t)s->cus * CUDASP_WAVES_A;
-  const uint64_t need_blocks = (total_wr + 3) / 4;
-  if (blocks > need_blocks) blocks = need_blocks;
-  const uint64_t cap_blocks = ((1ull << 32) - 1) / 4 / (words * BLOCK);
-  if (blocks > cap_blocks) blocks = cap_blocks;
-  if (blocks == 0) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the multi-batch path");
-  const uint64_t need_words = blocks * BLOCK * words;
-  if (need_words > s->mscratch_words) {
-    HIP_TRY(hipStreamSynchronize(st));  // no kernel of this scanner still uses the old scratch
-    if (s->d_mscratch) HIP_TRY(hipFree(s->d_mscratch));
-    s->d_mscratch = nullptr;
-    s->mscratch_words = 0;
-    // sized for the full grid, so later calls with more rows reuse it
-    const uint64_t full = std::min<uint64_t>((uint64_t)s->cus * CUDASP_WAVES_A, cap_blocks) * BLOCK * words;
-    HIP_TRY(hipMalloc(&s->d_mscratch, (size_t)full * 4));
-    s->mscratch_words = full;
-  }
-  memcpy(s->h_multi, md.data(), (size_t)nb * sizeof(MultiBatch));
-  HIP_TRY(hipMemcpyAsync(s->d_multi, s->h_multi, (size_t)nb * sizeof(MultiBatch), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipEventRecord(s->multi_copied, st));
-  s->multi_pending = true;
-  HIP_TRY(hipMemsetAsync(s->d_counter, 0, sizeof(uint32_t), st));
-  const uint32_t waves = (uint32_t)blocks * (BLOCK / 64);
-  const uint32_t g1 = multi_threshold("CUDASP_MULTI_G1", 150, waves);
-  const uint32_t g2 = multi_threshold("CUDASP_MULTI_G2", 400, waves);
-  hipLaunchKernelGGL(s->fb_bits == 26 ? k_scan_multi<26> : k_scan_multi<22>, dim3((uint32_t)blocks), dim3(BLOCK), 0,
-                     st, s->d_multi, nb, (uint32_t)total_wr, s->d_naf, s->consts, s->d_fb, s->d_labels,
-                     s->d_mscratch, s->d_counter, g1, g2);
-  HIP_TRY(hipGetLastError());
-  return CUDASP_OK;
+  return launch_multi(s, md, total_wr, st, MULTI_RMAX, multi_threshold_x100("CUDASP_MULTI_G1", 150),
+                      multi_threshold_x100("CUDASP_MULTI_G2", 400), 0);
 }
 
 int cudasp_row_values_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint32_t* d_tweak_y, uint32_t n,
