@@ -212,3 +212,16 @@ def test_multi_variants_fall_back(torch):
     plant(torch, batches, labels)
     opts = dict(output_count=2, label_negation=True)
     same(run_multi(torch, batches, labels, max_rows=2000, **opts), run_per_batch(torch, batches, labels, **opts))
+
+
+def test_fused_single_batch_equals_two_kernels(torch, monkeypatch):
+    """cudasp_scan_device runs both stages in one k_scan_multi launch by
+    default; CUDASP_FUSED_SINGLE=0 selects the two stage kernels.  Same flags
+    and match sets on ragged batches with labels."""
+    labels = [LABEL, SPEND]
+    batches = [make_batch(torch, 77 + 30000 * i, n) for i, n in enumerate([3001, 1, 300, 20000])]
+    plant(torch, batches, labels)
+    fused = run_per_batch(torch, batches, labels)
+    monkeypatch.setenv("CUDASP_FUSED_SINGLE", "0")
+    same(run_per_batch(torch, batches, labels), fused)
+    assert sum(c for _, _, c in fused) > 0
