@@ -836,10 +836,14 @@ struct cudasp_scanner {
   size_t outputs_cap = 0;
   // multi-batch persistent path (cudasp_scan_device_batches)
   MultiBatch* d_multi = nullptr;   // batch descriptors on the device
-  MultiBatch* h_multi = nullptr;   // pinned staging of the descriptors
-  uint32_t multi_cap = 0;          // descriptors the two buffers hold
-  hipEvent_t multi_copied = nullptr;  // the last descriptor upload has been read
-  bool multi_pending = false;
+  // pinned staging of the descriptors: a ring of MULTI_STAGING areas of
+  // multi_cap descriptors each, so queued launches do not make the host wait
+  // for an earlier upload before it can stage the next one
+  MultiBatch* h_multi = nullptr;
+  uint32_t multi_cap = 0;                       // descriptors per area (and in d_multi)
+  hipEvent_t multi_copied[8] = {};              // area i's upload has been read
+  bool multi_pending[8] = {};
+  uint32_t multi_next = 0;
   uint32_t* d_counter = nullptr;   // the persistent kernel's work counter
   uint32_t* d_mscratch = nullptr;  // mscratch_words u32
   uint64_t mscratch_words = 0;
@@ -942,7 +946,8 @@ void free_scanner(cudasp_scanner* s) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_multi) (void)hipHostFree(s->h_multi);
-  if (s->multi_copied) (void)hipEventDestroy(s->multi_copied);
+  for (hipEvent_t e : s->multi_copied)
+    if (e) (void)hipEventDestroy(e);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -1056,11 +1061,13 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
                         uint32_t rmax, uint32_t g1_x100, uint32_t g2_x100, uint64_t blocks_req) {
   if (total_wr >= (1ull << 31)) return set_error(CUDASP_ERR_CAPACITY, "too many rows in one multi-batch call");
   const uint32_t nb = (uint32_t)md.size();
-  if (s->multi_pending) {  // the previous upload must have been read before the staging is reused
-    HIP_TRY(hipEventSynchronize(s->multi_copied));
-    s->multi_pending = false;
-  }
+  constexpr uint32_t RING = sizeof(s->multi_pending) / sizeof(s->multi_pending[0]);
   if (nb > s->multi_cap) {
+    for (uint32_t i = 0; i < RING; i++)  // every staged upload has been read before the areas move
+      if (s->multi_pending[i]) {
+        HIP_TRY(hipEventSynchronize(s->multi_copied[i]));
+        s->multi_pending[i] = false;
+      }
     if (s->d_multi) HIP_TRY(hipFree(s->d_multi));
     if (s->h_multi) HIP_TRY(hipHostFree(s->h_multi));
     s->d_multi = nullptr;
@@ -1068,10 +1075,16 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
     s->multi_cap = 0;
     const uint32_t cap = nb < 256 ? 256 : nb;
     HIP_TRY(hipMalloc(&s->d_multi, (size_t)cap * sizeof(MultiBatch)));
-    HIP_TRY(hipHostMalloc((void**)&s->h_multi, (size_t)cap * sizeof(MultiBatch), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&s->h_multi, (size_t)cap * RING * sizeof(MultiBatch), hipHostMallocDefault));
     s->multi_cap = cap;
   }
-  if (!s->multi_copied) HIP_TRY(hipEventCreateWithFlags(&s->multi_copied, hipEventDisableTiming));
+  const uint32_t area = s->multi_next;
+  s->multi_next = (area + 1) % RING;
+  if (s->multi_pending[area]) {  // this area's previous upload must have been read before it is reused
+    HIP_TRY(hipEventSynchronize(s->multi_copied[area]));
+    s->multi_pending[area] = false;
+  }
+  if (!s->multi_copied[area]) HIP_TRY(hipEventCreateWithFlags(&s->multi_copied[area], hipEventDisableTiming));
   if (!s->d_counter) HIP_TRY(hipMalloc(&s->d_counter, sizeof(uint32_t)));
   if (!s->cus) {
     int cus = 0;
@@ -1101,10 +1114,14 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
     HIP_TRY(hipMalloc(&s->d_mscratch, (size_t)full * 4));
     s->mscratch_words = full;
   }
-  memcpy(s->h_multi, md.data(), (size_t)nb * sizeof(MultiBatch));
-  HIP_TRY(hipMemcpyAsync(s->d_multi, s->h_multi, (size_t)nb * sizeof(MultiBatch), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipEventRecord(s->multi_copied, st));
-  s->multi_pending = true;
+  // d_multi itself is reused in stream order: launches of one scanner run on
+  // one stream (include/cudasp_abi.h), so this upload lands after the
+  // previous kernel has read it
+  MultiBatch* stage = s->h_multi + (size_t)area * s->multi_cap;
+  memcpy(stage, md.data(), (size_t)nb * sizeof(MultiBatch));
+  HIP_TRY(hipMemcpyAsync(s->d_multi, stage, (size_t)nb * sizeof(MultiBatch), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipEventRecord(s->multi_copied[area], st));
+  s->multi_pending[area] = true;
   HIP_TRY(hipMemsetAsync(s->d_counter, 0, sizeof(uint32_t), st));
   const uint64_t waves = blocks * (BLOCK / 64);
   const uint32_t g1 = (uint32_t)(waves * g1_x100 / 100), g2 = (uint32_t)(waves * g2_x100 / 100);
