@@ -1022,6 +1022,15 @@ int launch_match(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t
   return CUDASP_OK;
 }
 
+// Whether k_scan_multi can run this scanner's launches: output index 0 only
+// (the reference's), an HBM fixed-base width, and scratch for at least one
+// 256-thread block within 4 GiB (thousands of labels would not fit; those
+// scanners use the two stage kernels).
+static bool multi_ok(const cudasp_scanner* s) {
+  return s->consts.output_count == 1 && (s->fb_bits == 22 || s->fb_bits == 26) &&
+         (uint64_t)multi_scratch_words(s->consts.label_count) * 4 * BLOCK <= (1ull << 32) - 1;
+}
+
 // Guided-scheduling thresholds of k_scan_multi in hundredths of the grid's
 // waves: 6 rows per thread while more than G2 x waves wave-rows remain, 2
 // while more than G1 x waves, then 1 (CUDASP_MULTI_G1 / CUDASP_MULTI_G2
@@ -1137,8 +1146,7 @@ int launch_pipeline(cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, c
                     uint32_t* match_count, int64_t* values, uint32_t* t_out, hipStream_t st) {
   if (n == 0) return CUDASP_OK;
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
-  if (s->fused_single && !values && !t_out && flags && s->consts.output_count == 1 &&
-      (s->fb_bits == 22 || s->fb_bits == 26) && !s->rows_a_force && !s->rows_b_force) {
+  if (s->fused_single && !values && !t_out && flags && multi_ok(s) && !s->rows_a_force && !s->rows_b_force) {
     // both stages in one k_scan_multi launch over this batch: ROWS_A rows per
     // thread throughout, one wave per chunk
     std::vector<MultiBatch> md(1, multi_desc(tx, ty, outputs, offs, lens, n, flags, match_rows, match_count, 0));
@@ -1421,8 +1429,8 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
     if (b.n && (!b.tweak_x || !b.tweak_y || !b.output_offsets || !b.output_lengths || !b.match_flags))
       return set_error(CUDASP_ERR_INVALID_ARG, "batch %u: null device buffer", i);
   }
-  const bool persistent = s->consts.output_count == 1 && (s->fb_bits == 22 || s->fb_bits == 26);
-  if (!persistent) {  // the per-batch path (protocol variants, the LDS width)
+  const bool persistent = multi_ok(s);
+  if (!persistent) {  // the per-batch path (protocol variants, the LDS width, very many labels)
     for (uint32_t i = 0; i < count; i++) {
       const cudasp_device_batch& b = batches[i];
       int rc = cudasp_scan_device(s, b.tweak_x, b.tweak_y, b.outputs, b.output_offsets, b.output_lengths, b.n,
