@@ -225,3 +225,17 @@ def test_fused_single_batch_equals_two_kernels(torch, monkeypatch):
     monkeypatch.setenv("CUDASP_FUSED_SINGLE", "0")
     same(run_per_batch(torch, batches, labels), fused)
     assert sum(c for _, _, c in fused) > 0
+
+
+def test_multi_100_labels(torch, monkeypatch):
+    """100 label keys (6 x 100 prefix products per thread in the label
+    scratch): the multi-batch path equals the two stage kernels, and planted
+    values of label indices 0..99 are found."""
+    import bench
+    labels = bench.label_keys(100)
+    batches = [make_batch(torch, 900 + 5000 * i, n) for i, n in enumerate([1500, 700])]
+    plant(torch, batches, labels, every=3)
+    got = run_multi(torch, batches, labels)
+    monkeypatch.setenv("CUDASP_FUSED_SINGLE", "0")
+    same(got, run_per_batch(torch, batches, labels))
+    assert sum(c for _, _, c in got) == len(range(0, 1500, 3)) + len(range(1, 700, 3))
