@@ -14,12 +14,14 @@ round-robins its executor threads over GPUs, src/cudasp_extension.cu:523-529),
 so the total work is fixed as N grows (`--shard weak` gives every rank its own
 table instead).  Each rank's batches are resident in HBM, tweak limbs
 column-major per batch.  A step is one pass of the hot path over the rank's
-batches: every batch goes through the two kernels of cudasp_scan_device
+batches: by default (`--launch multi`) one cudasp_scan_device_batches call
+over all of them -- one persistent kernel (k_scan_multi) runs both stages
 (stage A: d*T + tagged hash; stage B: t*G + B, labels, compare, flag + ballot
-compaction), batches round-robin over `--streams` HIP streams (the
-reference's per-thread streams, src/cudasp_gpu.cu:505).  No collective in the
-data path: torch.distributed carries the bracketing barrier and the max of the
-elapsed time.  After the timed steps, rank 0 at N = 1 also reports the
+compaction) for every row, with per-batch flags and match lists; with
+`--launch batches` every batch goes through cudasp_scan_device, round-robin
+over `--streams` HIP streams (the reference's per-thread streams,
+src/cudasp_gpu.cu:505).  No collective in the data path: torch.distributed
+carries the bracketing barrier and the max of the elapsed time.  After the timed steps, rank 0 at N = 1 also reports the
 PCIe-inclusive end-to-end rate of the table-function host (`e2e`,
 tools/host_e2e) -- never the `value`.
 
