@@ -26,6 +26,7 @@
 
 #include "../../include/cudasp_abi.h"
 #include "scan_prepare.hpp"
+#include "scan_multi.hpp"
 
 using namespace cudasp;
 
@@ -355,38 +356,6 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 // one Z inversion in stage A (t stays in the thread), then one Z inversion and
 // one label inversion in stage B.  Exit: every wave leaves when the counter
 // passes the last wave-row.
-struct MultiBatch {
-  const uint32_t* tx;
-  const uint32_t* ty;
-  const int64_t* outputs;
-  const uint32_t* offs;
-  const uint32_t* lens;
-  uint8_t* flags;
-  uint32_t* match_rows;
-  uint32_t* match_count;
-  uint32_t n;
-  uint32_t first_wr;
-};
-
-// The batch holding wave-row w (w wave-uniform): the last batch with
-// first_wr <= w.
-__device__ __forceinline__ uint32_t multi_batch_of(const MultiBatch* __restrict__ bd, uint32_t nb, uint32_t w) {
-  uint32_t lo = 0, hi = nb;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (bd[mid].first_wr <= w) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-// Row of this lane in wave-row w of batch `b`; *active = false for the padding
-// of the batch's last wave-row (which then reads batch row 0).
-__device__ __forceinline__ uint32_t multi_row(const MultiBatch& b, uint32_t w, uint32_t lane, bool* active) {
-  const uint32_t r = (w - b.first_wr) * 64u + lane;
-  *active = r < b.n;
-  return *active ? r : 0u;
-}
-
 #ifndef CUDASP_MULTI_RMAX
 #define CUDASP_MULTI_RMAX 6
 #endif
@@ -414,7 +383,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
     if (lane == 0) {
       const uint32_t prev = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t rem = prev < total_wr ? total_wr - prev : 0u;
-      R = rem > g2 ? rmax : (rem > g1 ? 2u : 1u);
+      R = multi_piece_rows(rem, g1, g2, rmax);
       base = atomicAdd(counter, R);
     }
     base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);

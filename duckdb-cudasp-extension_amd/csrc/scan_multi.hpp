@@ -1,0 +1,56 @@
+// Work distribution of the multi-batch persistent scan (k_scan_multi,
+// scan_kernels.hip), written once as __host__ __device__ code so that
+// tests/native/cudasp_emu.cpp can replay the schedule on the CPU and check
+// that every row of every batch is scanned exactly once.
+//
+// The batches' rows form a virtual row space of 64-row wave-rows: batch b
+// occupies wave-rows [first_wr, first_wr + ceil(n / 64)), so a wave-row never
+// spans two batches and the last one of a batch is padded.
+#pragma once
+#include <stdint.h>
+
+#include "secp256k1_fe.hpp"  // CUDASP_HD
+
+namespace cudasp {
+
+// Device descriptor of one batch (cudasp_device_batch plus its first wave-row).
+struct MultiBatch {
+  const uint32_t* tx;
+  const uint32_t* ty;
+  const int64_t* outputs;
+  const uint32_t* offs;
+  const uint32_t* lens;
+  uint8_t* flags;
+  uint32_t* match_rows;
+  uint32_t* match_count;
+  uint32_t n;
+  uint32_t first_wr;
+};
+
+// The batch holding wave-row w (w wave-uniform): the last batch with
+// first_wr <= w.
+CUDASP_HD uint32_t multi_batch_of(const MultiBatch* __restrict__ bd, uint32_t nb, uint32_t w) {
+  uint32_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (bd[mid].first_wr <= w) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// Row of this lane in wave-row w of batch `b`; *active = false for the padding
+// of the batch's last wave-row (which then reads batch row 0).
+CUDASP_HD uint32_t multi_row(const MultiBatch& b, uint32_t w, uint32_t lane, bool* active) {
+  const uint32_t r = (w - b.first_wr) * 64u + lane;
+  *active = r < b.n;
+  return *active ? r : 0u;
+}
+
+// Wave-rows of the next piece (= rows per thread) with `rem` wave-rows left:
+// rmax while more than g2 remain, then 2, then 1 below g1 (guided
+// self-scheduling; g1 = g2 = 0 gives rmax throughout).
+CUDASP_HD uint32_t multi_piece_rows(uint32_t rem, uint32_t g1, uint32_t g2, uint32_t rmax) {
+  return rem > g2 ? rmax : (rem > g1 ? (rmax < 2u ? rmax : 2u) : 1u);
+}
+
+}  // namespace cudasp

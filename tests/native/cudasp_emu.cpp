@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../duckdb-cudasp-extension_amd/csrc/scan_prepare.hpp"
+#include "../../duckdb-cudasp-extension_amd/csrc/scan_multi.hpp"
 
 namespace cudasp {
 void fe_check_fail(const char* what, int limb, uint32_t v) {
@@ -370,6 +371,78 @@ int emu_row_values_grouped(const uint8_t scan[32], const uint8_t spend[64], cons
     if (L) hits |= match_labels_rows(k, labels.data(), outputs, offs, lens, g, 1, n, n, count, sb, PB, values);
     if (flags)
       for (int j = 0; j < count; j++) flags[g + j] = (hits >> j) & 1u;
+  }
+  return 0;
+}
+
+// k_scan_multi's work distribution replayed on the CPU: `waves` wavefronts
+// claim pieces from one counter with the kernel's read-then-add protocol, in a
+// seeded random interleaving (so a wave may size its piece from a stale
+// counter value, as on the GPU).  Descriptors are laid out as
+// cudasp_scan_device_batches lays them out (empty batches skipped, each batch
+// from a fresh wave-row).  cover[sum(sizes)] counts how often each batch row
+// was scanned by an active lane; stats[0..4] = pieces of rmax / 2 / 1 rows,
+// pieces in total, pieces whose rows ran past the last wave-row.
+int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, uint32_t g1, uint32_t g2,
+                       uint32_t rmax, uint64_t seed, uint32_t* cover, uint64_t* stats) {
+  if (waves == 0 || rmax < 1) return CUDASP_ERR_INVALID_ARG;
+  std::vector<MultiBatch> md;
+  std::vector<uint64_t> row0;  // index of each descriptor's row 0 in cover
+  uint64_t total_wr = 0, at = 0;
+  for (uint32_t i = 0; i < count; i++) {
+    if (sizes[i]) {
+      MultiBatch m{};
+      m.n = sizes[i];
+      m.first_wr = (uint32_t)total_wr;
+      md.push_back(m);
+      row0.push_back(at);
+      total_wr += (sizes[i] + 63u) / 64u;
+    }
+    at += sizes[i];
+  }
+  for (uint64_t i = 0; i < at; i++) cover[i] = 0;
+  for (int i = 0; i < 5; i++) stats[i] = 0;
+  if (md.empty()) return 0;
+  const uint32_t nb = (uint32_t)md.size(), twr = (uint32_t)total_wr;
+  uint32_t counter = 0;
+  std::vector<uint8_t> done(waves, 0);
+  std::vector<int32_t> sized(waves, -1);  // piece size read from the counter, -1 = not read yet
+  uint64_t x = seed * 6364136223846793005ull + 1442695040888963407ull;
+  uint32_t live = waves;
+  while (live) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 29;
+    uint32_t v = (uint32_t)(x % waves);
+    while (done[v]) v = (v + 1) % waves;
+    if (sized[v] < 0) {  // lane 0 reads the counter and sizes its piece
+      const uint32_t rem = counter < twr ? twr - counter : 0u;
+      sized[v] = (int32_t)multi_piece_rows(rem, g1, g2, rmax);
+      continue;
+    }
+    const uint32_t R = (uint32_t)sized[v];
+    const uint32_t base = counter;  // atomicAdd
+    counter += R;
+    sized[v] = -1;
+    if (base >= twr) {
+      done[v] = 1;
+      live--;
+      continue;
+    }
+    stats[R == rmax ? 0 : (R == 2 ? 1 : 2)]++;
+    stats[3]++;
+    if (R > twr - base) stats[4]++;
+    const int cnt = (int)(R < twr - base ? R : twr - base);
+    for (int j = 0; j < cnt; j++) {
+      const uint32_t w = base + (uint32_t)j;
+      const uint32_t b = multi_batch_of(md.data(), nb, w);
+      for (uint32_t lane = 0; lane < 64; lane++) {
+        bool active;
+        const uint32_t r = multi_row(md[b], w, lane, &active);
+        if (active) cover[row0[b] + r]++;
+        else if (r != 0) return -1;  // padding lanes read row 0
+      }
+    }
   }
   return 0;
 }
