@@ -8,7 +8,13 @@ t, against the device's slots (CUs x 4 SIMDs x waves per SIMD).  A dispatch's
 demand is counted until it ends, so the tail of a launch (its last waves) still
 counts as full demand: the figure is a lower bound of the idle slots.
 
-  python tools/timeline.py TRACE.csv [--slots 3072] [--gap-ms 0.5]
+  python tools/timeline.py TRACE.csv [--slots 3072] [--gap-ms 0.5] [--copies COPY_TRACE.csv]
+
+Per burst it also gives the fill and the drain: from the burst's first dispatch
+to the first moment the demand reaches the slots, and from the last such moment
+to the burst's end.  With --copies (a rocprofv3 --memory-copy-trace CSV) it
+adds the copies that overlap the burst: their count and summed time per
+direction.
 """
 import argparse
 import collections
@@ -37,17 +43,22 @@ def profile(burst, slots):
     ev.sort()
     under = 0.0
     by_count = collections.Counter()
+    full_first = full_last = None
     demand, running, prev = 0, 0, ev[0][0]
     for t, d, w in ev:
         dt = (t - prev) / 1e6
         if dt > 0:
             if demand < slots:
                 under += dt
+            elif full_first is None:
+                full_first = prev
+            if demand >= slots:
+                full_last = t
             by_count[min(running, 4)] += dt
         demand += d * w
         running += d
         prev = t
-    return under, by_count
+    return under, by_count, full_first, full_last
 
 
 def main():
@@ -55,7 +66,13 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--slots", type=int, default=256 * 4 * 3)
     ap.add_argument("--gap-ms", type=float, default=0.5)
+    ap.add_argument("--copies")
     a = ap.parse_args()
+    copies = []
+    if a.copies:
+        for r in csv.DictReader(open(a.copies)):
+            d = r.get("Direction") or r.get("Kind") or "?"
+            copies.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), d))
     spans = []
     for r in csv.DictReader(open(a.trace)):
         name = r["Kernel_Name"].split("(")[0]
@@ -67,12 +84,22 @@ def main():
         per = collections.defaultdict(float)
         for s in b:
             per[s[2]] += (s[1] - s[0]) / 1e6
-        under, by_count = profile(b, a.slots)
+        under, by_count, ff, fl = profile(b, a.slots)
         print("burst %d: %d dispatches, span %.2f ms, demand < %d slots for %.2f ms; running 1/2/3/>=4: %s" % (
             i, len(b), (t1 - t0) / 1e6, a.slots, under,
             " / ".join("%.2f" % by_count[k] for k in (1, 2, 3, 4))))
         for k, v in sorted(per.items(), key=lambda kv: -kv[1])[:4]:
             print("    %-40s %8.2f ms summed" % (k[:40], v))
+        if ff is not None:
+            print("    fill %.2f ms, drain %.2f ms" % ((ff - t0) / 1e6, (t1 - fl) / 1e6))
+        cs = [c for c in copies if c[1] >= t0 and c[0] <= t1]
+        if cs:
+            cper = collections.defaultdict(lambda: [0, 0.0])
+            for c in cs:
+                cper[c[2]][0] += 1
+                cper[c[2]][1] += (c[1] - c[0]) / 1e6
+            for k, (n, ms) in sorted(cper.items()):
+                print("    %-24s %5d copies %8.2f ms summed" % (k[:24], n, ms))
 
 
 if __name__ == "__main__":
