@@ -361,6 +361,7 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 #endif
 constexpr int MULTI_RMAX = CUDASP_MULTI_RMAX;  // rows per thread while much work remains (tuned)
 static_assert(MULTI_RMAX >= 2 && MULTI_RMAX <= 16, "multi-batch rows per thread");
+static_assert(ROWS_A <= MULTI_RMAX, "the fused single-batch launch runs ROWS_A rows per thread in k_scan_multi");
 constexpr uint32_t multi_scratch_words(uint32_t label_count) {
   return VB_SCRATCH_WORDS + PEND_WORDS * MULTI_RMAX + FW * label_count * MULTI_RMAX;
 }
@@ -1038,6 +1039,8 @@ static MultiBatch multi_desc(const uint32_t* tx, const uint32_t* ty, const int64
 static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, uint64_t total_wr, hipStream_t st,
                         uint32_t rmax, uint32_t g1_x100, uint32_t g2_x100, uint64_t blocks_req) {
   if (total_wr >= (1ull << 31)) return set_error(CUDASP_ERR_CAPACITY, "too many rows in one multi-batch call");
+  if (rmax < 1 || rmax > (uint32_t)MULTI_RMAX)  // the kernel's pending slots hold MULTI_RMAX rows per thread
+    return set_error(CUDASP_ERR_INVALID_ARG, "multi-batch rows per thread %u outside 1..%d", rmax, MULTI_RMAX);
   const uint32_t nb = (uint32_t)md.size();
   constexpr uint32_t RING = sizeof(s->multi_pending) / sizeof(s->multi_pending[0]);
   if (nb > s->multi_cap) {
