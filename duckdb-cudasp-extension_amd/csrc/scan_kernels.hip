@@ -354,19 +354,91 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 // the last pieces are short and the GPU stays full to the end (a fused
 // single-batch launch uses g1 = g2 = 0: rmax rows per thread throughout).  A thread's R rows share
 // one Z inversion in stage A (t stays in the thread), then one Z inversion and
-// one label inversion in stage B.  Exit: every wave leaves when the counter
-// passes the last wave-row.
+// one label inversion in stage B.  PIPE (the default): a wave finishes a piece's
+// stage B one iteration later, so the piece's stage-B Z inversion joins the
+// next piece's stage-A one -- one inversion per piece instead of two.  Exit:
+// every wave leaves when the counter passes the last wave-row and its last
+// piece is finished.
 #ifndef CUDASP_MULTI_RMAX
 #define CUDASP_MULTI_RMAX 6
 #endif
 constexpr int MULTI_RMAX = CUDASP_MULTI_RMAX;  // rows per thread while much work remains (tuned)
 static_assert(MULTI_RMAX >= 2 && MULTI_RMAX <= 16, "multi-batch rows per thread");
 static_assert(ROWS_A <= MULTI_RMAX, "the fused single-batch launch runs ROWS_A rows per thread in k_scan_multi");
-constexpr uint32_t multi_scratch_words(uint32_t label_count) {
-  return VB_SCRATCH_WORDS + PEND_WORDS * MULTI_RMAX + FW * label_count * MULTI_RMAX;
+// Pending slots per thread: one piece, or with the pipelined schedule
+// (PIPE) the previous piece's stage-B points beside the new piece's stage-A
+// points.
+constexpr int multi_pend_slots(bool pipe) { return MULTI_RMAX * (pipe ? 2 : 1); }
+constexpr uint32_t multi_scratch_words(uint32_t label_count, bool pipe) {
+  return VB_SCRATCH_WORDS + PEND_WORDS * multi_pend_slots(pipe) + FW * label_count * MULTI_RMAX;
 }
 
-template <int FBB>
+// Wave-row w of the batches as (descriptor, batch row) of this lane.
+__device__ __forceinline__ const MultiBatch& multi_locate(const MultiBatch* __restrict__ bd, uint32_t nb, uint32_t w,
+                                                          uint32_t lane, uint32_t* r, bool* active) {
+  const MultiBatch& b = bd[multi_batch_of(bd, nb, w)];
+  *r = multi_row(b, w, lane, active);
+  return b;
+}
+
+// Flags of rows base .. base + count - 1 (hits: bit j = row j matched) and
+// their compaction, one wave-row (= one batch) at a time.
+__device__ __forceinline__ void multi_emit(const MultiBatch* __restrict__ bd, uint32_t nb, uint32_t base, int count,
+                                           uint32_t lane, uint32_t hits) {
+#pragma unroll 1
+  for (int j = 0; j < count; j++) {
+    uint32_t r;
+    bool active;
+    const MultiBatch& b = multi_locate(bd, nb, base + (uint32_t)j, lane, &r, &active);
+    const bool hit = active && ((hits >> j) & 1u);
+    if (active) b.flags[r] = hit ? 1 : 0;
+    if (b.match_rows != nullptr) {
+      const uint64_t m = __ballot(hit);
+      if (m) {
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(b.match_count, (uint32_t)__popcll(m));
+        at = __shfl(at, 0);
+        if (hit) b.match_rows[at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = r;
+      }
+    }
+  }
+}
+
+// Stage B's second half for the `count` rows from wave-row `base` whose F
+// points wait in pending slots 0 .. count - 1 with their 1/Z: base compare,
+// labels (one batched inversion), flags and compaction.
+__device__ __forceinline__ void multi_finish(const MultiBatch* __restrict__ bd, uint32_t nb, uint32_t base, int count,
+                                             uint32_t lane, const ScanConsts& k, const uint32_t* __restrict__ labels,
+                                             const Scratch& sc, int pb, int lb) {
+  uint32_t hits = 0;
+#pragma unroll 1
+  for (int j = 0; j < count; j++) {
+    uint32_t r;
+    bool active;
+    const MultiBatch& b = multi_locate(bd, nb, base + (uint32_t)j, lane, &r, &active);
+    gej P;
+    fe zi;
+    pend_load(P, sc, pb, j);
+    scr_load(zi, sc, PEND_ZI(pb, j));
+    if (row_match_base(P, zi, k, b.outputs, b.offs[r], b.lens[r], sc, pb, j, nullptr)) hits |= 1u << j;
+  }
+  if (k.label_count)
+    hits |= match_labels_core(k, labels, count, sc, pb, lb,
+                              [&](int j, const int64_t*& o, uint32_t& off, uint32_t& len, int64_t*& vrow,
+                                  uint32_t& vstride) {
+                                uint32_t r;
+                                bool active;
+                                const MultiBatch& b = multi_locate(bd, nb, base + (uint32_t)j, lane, &r, &active);
+                                o = b.outputs;
+                                off = b.offs[r];
+                                len = b.lens[r];
+                                vrow = nullptr;
+                                vstride = 0;
+                              });
+  multi_emit(bd, nb, base, count, lane, hits);
+}
+
+template <int FBB, bool PIPE>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const MultiBatch* __restrict__ bd, uint32_t nb,
                                                                    uint32_t total_wr, const int8_t* __restrict__ naf,
                                                                    ScanConsts k, const uint32_t* __restrict__ fb,
@@ -377,27 +449,37 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = make_scratch(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
-  constexpr int PB = VB_SCRATCH_WORDS;                      // pending rows
-  constexpr int LB = VB_SCRATCH_WORDS + PEND_WORDS * MULTI_RMAX;  // label prefix products
+  constexpr int PB = VB_SCRATCH_WORDS;                             // pending rows
+  constexpr int LB = VB_SCRATCH_WORDS + PEND_WORDS * multi_pend_slots(PIPE);  // label prefix products
+  // The previous piece (PIPE): its F points wait in slots 0 .. count_p - 1.
+  uint32_t base_p = 0;
+  int count_p = 0;
+  bool more = true;
   for (;;) {
-    uint32_t base = 0, R = 1;
-    if (lane == 0) {
-      const uint32_t prev = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t rem = prev < total_wr ? total_wr - prev : 0u;
-      R = multi_piece_rows(rem, g1, g2, rmax);
-      base = atomicAdd(counter, R);
+    uint32_t base = 0;
+    int count = 0;
+    if (more) {
+      uint32_t R = 1;
+      if (lane == 0) {
+        const uint32_t prev = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t rem = prev < total_wr ? total_wr - prev : 0u;
+        R = multi_piece_rows(rem, g1, g2, rmax);
+        base = atomicAdd(counter, R);
+      }
+      base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+      R = (uint32_t)__builtin_amdgcn_readfirstlane((int)R);
+      if (base >= total_wr)
+        more = false;
+      else
+        count = (int)(R < total_wr - base ? R : total_wr - base);
     }
-    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-    R = (uint32_t)__builtin_amdgcn_readfirstlane((int)R);
-    if (base >= total_wr) break;
-    const int count = (int)(R < total_wr - base ? R : total_wr - base);
-    // stage A: S = d T of the thread's rows, one shared inversion
+    if (count == 0 && count_p == 0) break;
+    // stage A: S = d T of the piece's rows (after the previous piece's F points)
 #pragma unroll 1
     for (int j = 0; j < count; j++) {
-      const uint32_t w = base + (uint32_t)j;
-      const MultiBatch& b = bd[multi_batch_of(bd, nb, w)];
+      uint32_t r;
       bool active;
-      const uint32_t r = multi_row(b, w, lane, &active);
+      const MultiBatch& b = multi_locate(bd, nb, base + (uint32_t)j, lane, &r, &active);
       uint32_t x[8], y[8];
 #pragma unroll
       for (int q = 0; q < 8; q++) {
@@ -406,69 +488,33 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
       }
       gej P;
       row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
-      pend_store(sc, PB, j, P);
+      pend_store(sc, PB, count_p + j, P);
     }
-    pend_invert<MULTI_RMAX>(sc, PB, count);
-    // t of each row, then stage B's F = t G + B in the same pending slot
+    // one inversion: the new S points, and with PIPE the previous piece's F points
+    pend_invert<2 * MULTI_RMAX>(sc, PB, count_p + count);
+    if constexpr (PIPE) {
+      if (count_p) multi_finish(bd, nb, base_p, count_p, lane, k, labels, sc, PB, LB);
+    }
+    // t of each row, then stage B's F = t G + B into slot j
 #pragma unroll 1
     for (int j = 0; j < count; j++) {
       gej P;
       fe zi;
-      pend_load(P, sc, PB, j);
-      scr_load(zi, sc, PEND_ZI(PB, j));
+      pend_load(P, sc, PB, count_p + j);
+      scr_load(zi, sc, PEND_ZI(PB, count_p + j));
       uint32_t sx[8], t[8];
       const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
       bip352_shared_secret_hash(t, k.mid, sx, y_odd);
       gej F;
       row_match_point<FBB>(F, t, fb, k);
-      pend_store(sc, PB, j, F);
+      pend_store(sc, PB, j, F);  // slot count_p + j' (j' < j) is consumed already
     }
-    pend_invert<MULTI_RMAX>(sc, PB, count);
-    uint32_t hits = 0;
-#pragma unroll 1
-    for (int j = 0; j < count; j++) {
-      const uint32_t w = base + (uint32_t)j;
-      const MultiBatch& b = bd[multi_batch_of(bd, nb, w)];
-      bool active;
-      const uint32_t r = multi_row(b, w, lane, &active);
-      gej P;
-      fe zi;
-      pend_load(P, sc, PB, j);
-      scr_load(zi, sc, PEND_ZI(PB, j));
-      if (row_match_base(P, zi, k, b.outputs, b.offs[r], b.lens[r], sc, PB, j, nullptr)) hits |= 1u << j;
-    }
-    if (k.label_count)
-      hits |= match_labels_core(k, labels, count, sc, PB, LB,
-                                [&](int j, const int64_t*& o, uint32_t& off, uint32_t& len, int64_t*& vrow,
-                                    uint32_t& vstride) {
-                                  const uint32_t w = base + (uint32_t)j;
-                                  const MultiBatch& b = bd[multi_batch_of(bd, nb, w)];
-                                  bool active;
-                                  const uint32_t r = multi_row(b, w, lane, &active);
-                                  o = b.outputs;
-                                  off = b.offs[r];
-                                  len = b.lens[r];
-                                  vrow = nullptr;
-                                  vstride = 0;
-                                });
-    // flags and compaction, one wave-row (= one batch) at a time
-#pragma unroll 1
-    for (int j = 0; j < count; j++) {
-      const uint32_t w = base + (uint32_t)j;
-      const MultiBatch& b = bd[multi_batch_of(bd, nb, w)];
-      bool active;
-      const uint32_t r = multi_row(b, w, lane, &active);
-      const bool hit = active && ((hits >> j) & 1u);
-      if (active) b.flags[r] = hit ? 1 : 0;
-      if (b.match_rows != nullptr) {
-        const uint64_t m = __ballot(hit);
-        if (m) {
-          uint32_t at = 0;
-          if (lane == 0) at = atomicAdd(b.match_count, (uint32_t)__popcll(m));
-          at = __shfl(at, 0);
-          if (hit) b.match_rows[at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = r;
-        }
-      }
+    if constexpr (PIPE) {
+      base_p = base;
+      count_p = count;
+    } else {
+      pend_invert<MULTI_RMAX>(sc, PB, count);
+      multi_finish(bd, nb, base, count, lane, k, labels, sc, PB, LB);
     }
   }
 }
@@ -823,6 +869,9 @@ struct cudasp_scanner {
   // CUDASP_FUSED_SINGLE=0 selects the two kernels (A/B; the stage entry points,
   // the values path, forced launch shapes and the variants always use them)
   bool fused_single = true;
+  // k_scan_multi with the pipelined schedule (one Z inversion per piece);
+  // CUDASP_MULTI_PIPE=0 selects the two-inversion schedule (A/B)
+  bool multi_pipe = true;
 };
 
 namespace {
@@ -998,7 +1047,7 @@ int launch_match(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t
 // scanners use the two stage kernels).
 static bool multi_ok(const cudasp_scanner* s) {
   return s->consts.output_count == 1 && (s->fb_bits == 22 || s->fb_bits == 26) &&
-         (uint64_t)multi_scratch_words(s->consts.label_count) * 4 * BLOCK <= (1ull << 32) - 1;
+         (uint64_t)multi_scratch_words(s->consts.label_count, s->multi_pipe) * 4 * BLOCK <= (1ull << 32) - 1;
 }
 
 // Guided-scheduling thresholds of k_scan_multi in hundredths of the grid's
@@ -1075,7 +1124,7 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
   }
   // grid: at most CUDASP_WAVES_A waves per SIMD (one 256-thread block = one
   // wave per SIMD of a CU), no more waves than wave-rows, within 4 GiB of scratch
-  const uint64_t words = multi_scratch_words(s->consts.label_count);
+  const uint64_t words = multi_scratch_words(s->consts.label_count, s->multi_pipe);
   const uint64_t full_blocks = (uint64_t)s->cus * CUDASP_WAVES_A;
   const uint64_t cap_blocks = ((1ull << 32) - 1) / 4 / (words * BLOCK);
   uint64_t blocks = blocks_req ? blocks_req : full_blocks;
@@ -1106,9 +1155,10 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
   HIP_TRY(hipMemsetAsync(s->d_counter, 0, sizeof(uint32_t), st));
   const uint64_t waves = blocks * (BLOCK / 64);
   const uint32_t g1 = (uint32_t)(waves * g1_x100 / 100), g2 = (uint32_t)(waves * g2_x100 / 100);
-  hipLaunchKernelGGL(s->fb_bits == 26 ? k_scan_multi<26> : k_scan_multi<22>, dim3((uint32_t)blocks), dim3(BLOCK), 0,
-                     st, s->d_multi, nb, (uint32_t)total_wr, s->d_naf, s->consts, s->d_fb, s->d_labels,
-                     s->d_mscratch, s->d_counter, g1, g2, rmax);
+  auto kf = s->multi_pipe ? (s->fb_bits == 26 ? k_scan_multi<26, true> : k_scan_multi<22, true>)
+                          : (s->fb_bits == 26 ? k_scan_multi<26, false> : k_scan_multi<22, false>);
+  hipLaunchKernelGGL(kf, dim3((uint32_t)blocks), dim3(BLOCK), 0, st, s->d_multi, nb, (uint32_t)total_wr, s->d_naf,
+                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, s->d_counter, g1, g2, rmax);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
 }
@@ -1207,6 +1257,7 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
     s->fill_threads = (uint32_t)cus * 4 * CUDASP_WAVES_A * 64 / 4;
     s->fill_threads_b = (uint32_t)cus * 4 * CUDASP_WAVES_B * 64 / 4;
     if (const char* f = getenv("CUDASP_FUSED_SINGLE")) s->fused_single = atoi(f) != 0;
+    if (const char* f = getenv("CUDASP_MULTI_PIPE")) s->multi_pipe = atoi(f) != 0;
     if (const char* f = getenv("CUDASP_ROWS_A_FORCE")) {
       const int r = atoi(f);
       if (r == 1 || r == 2 || r == ROWS_A) s->rows_a_force = r;

@@ -239,3 +239,23 @@ def test_multi_100_labels(torch, monkeypatch):
     monkeypatch.setenv("CUDASP_FUSED_SINGLE", "0")
     same(got, run_per_batch(torch, batches, labels))
     assert sum(c for _, _, c in got) == len(range(0, 1500, 3)) + len(range(1, 700, 3))
+
+
+@pytest.mark.parametrize("g1,g2", [("0", "0"), ("150", "400"), ("100000", "100000")])
+def test_multi_pipelined_equals_unpipelined(torch, monkeypatch, g1, g2):
+    """The default schedule finishes a piece's stage B one iteration later,
+    with its Z inversion merged into the next piece's stage-A inversion
+    (CUDASP_MULTI_PIPE=0: two inversions per piece).  Same flags and match
+    sets as that schedule and as the two stage kernels, in every chunk-size
+    regime, with labels."""
+    monkeypatch.setenv("CUDASP_MULTI_G1", g1)
+    monkeypatch.setenv("CUDASP_MULTI_G2", g2)
+    labels = [LABEL, SPEND]
+    batches = [make_batch(torch, 4242 + 25000 * i, n) for i, n in enumerate([5000, 1, 65, 12000, 640])]
+    plant(torch, batches, labels)
+    piped = run_multi(torch, batches, labels)
+    assert sum(c for _, _, c in piped) > 0
+    monkeypatch.setenv("CUDASP_MULTI_PIPE", "0")
+    same(run_multi(torch, batches, labels), piped)
+    monkeypatch.setenv("CUDASP_FUSED_SINGLE", "0")
+    same(run_per_batch(torch, batches, labels), piped)

@@ -27,6 +27,7 @@ def test_kernel_names():
     assert k("void k_match<false, 2>(x)") == "void k_match<false, 2>"
     assert k("k_layout_probe(unsigned int const*)") == "k_layout_probe"
     assert k("void k_scan_multi<26>(MultiBatch const*, unsigned int)") == "k_scan_multi"
+    assert k("void k_scan_multi<26, true>(cudasp::MultiBatch const*, unsigned int)") == "k_scan_multi"
 
 
 def test_committed_profiles_have_bench_keys():

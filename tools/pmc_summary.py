@@ -31,7 +31,7 @@ def kernel_key(name):
     plain names bench.py looks up, the small-launch instances (rows_a_for,
     rows_b_for) stay separate."""
     k = name.split("(")[0]
-    if re.fullmatch(r"void k_scan_multi<\d+>", k):  # the multi-batch kernel, any fixed-base width
+    if re.fullmatch(r"void k_scan_multi<\d+(, (true|false))?>", k):  # the multi-batch kernel, any width / schedule
         return "k_scan_multi"
     m = re.fullmatch(r"void k_shared_secret<(\d+)>", k)
     if m:
