@@ -355,22 +355,27 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 // single-batch launch uses g1 = g2 = 0: rmax rows per thread throughout).  A thread's R rows share
 // one Z inversion in stage A (t stays in the thread), then one Z inversion and
 // one label inversion in stage B.  PIPE (the default): a wave finishes a piece's
-// stage B one iteration later, so the piece's stage-B Z inversion joins the
-// next piece's stage-A one -- one inversion per piece instead of two.  Exit:
-// every wave leaves when the counter passes the last wave-row and its last
-// piece is finished.
+// stage B one iteration later and its labels one more iteration later, so the
+// piece's stage-B Z inversion and its label inversion join the following
+// pieces' stage-A inversions -- one inversion per piece instead of two (three
+// with labels).  Exit: every wave leaves when the counter passes the last
+// wave-row and its last pieces are finished.
 #ifndef CUDASP_MULTI_RMAX
 #define CUDASP_MULTI_RMAX 6
 #endif
 constexpr int MULTI_RMAX = CUDASP_MULTI_RMAX;  // rows per thread while much work remains (tuned)
 static_assert(MULTI_RMAX >= 2 && MULTI_RMAX <= 16, "multi-batch rows per thread");
 static_assert(ROWS_A <= MULTI_RMAX, "the fused single-batch launch runs ROWS_A rows per thread in k_scan_multi");
-// Pending slots per thread: one piece, or with the pipelined schedule
-// (PIPE) the previous piece's stage-B points beside the new piece's stage-A
-// points.
-constexpr int multi_pend_slots(bool pipe) { return MULTI_RMAX * (pipe ? 2 : 1); }
+// Scratch of a k_scan_multi thread (u32 words from the slot's base): the
+// stage-A table, then the pending slots -- one piece's, or with the pipelined
+// schedule (PIPE) the previous piece's F points beside the new piece's S
+// points plus one slot for the label product of the piece before that --,
+// the label prefix products of one piece, and (PIPE with labels) that piece's
+// affine F points and label product while their inversion is pending.
+constexpr int multi_pend_slots(bool pipe) { return pipe ? 2 * MULTI_RMAX + 1 : MULTI_RMAX; }
 constexpr uint32_t multi_scratch_words(uint32_t label_count, bool pipe) {
-  return VB_SCRATCH_WORDS + PEND_WORDS * multi_pend_slots(pipe) + FW * label_count * MULTI_RMAX;
+  return VB_SCRATCH_WORDS + PEND_WORDS * multi_pend_slots(pipe) + FW * label_count * MULTI_RMAX +
+         (pipe && label_count ? 2 * FW * MULTI_RMAX + FW : 0);
 }
 
 // Wave-row w of the batches as (descriptor, batch row) of this lane.
@@ -451,9 +456,14 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
   const uint32_t lane = threadIdx.x & 63u;
   constexpr int PB = VB_SCRATCH_WORDS;                             // pending rows
   constexpr int LB = VB_SCRATCH_WORDS + PEND_WORDS * multi_pend_slots(PIPE);  // label prefix products
-  // The previous piece (PIPE): its F points wait in slots 0 .. count_p - 1.
-  uint32_t base_p = 0;
-  int count_p = 0;
+  const int QF = LB + FW * (int)k.label_count * MULTI_RMAX;  // PIPE: piece Q's affine F (x, y per row)
+  const int QACC = QF + 2 * FW * MULTI_RMAX;                 // PIPE: piece Q's label product
+  // PIPE: piece P's F points wait in slots 0 .. count_p - 1 for their 1/Z;
+  // with labels, piece Q (base compared, label prefix products formed) waits
+  // for the inverse of its label product.  Each joins the next iteration's
+  // inversion, so a piece costs one inversion instead of three.
+  uint32_t base_p = 0, base_q = 0, hits_q = 0;
+  int count_p = 0, count_q = 0;
   bool more = true;
   for (;;) {
     uint32_t base = 0;
@@ -473,7 +483,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
       else
         count = (int)(R < total_wr - base ? R : total_wr - base);
     }
-    if (count == 0 && count_p == 0) break;
+    if (count == 0 && count_p == 0 && count_q == 0) break;
     // stage A: S = d T of the piece's rows (after the previous piece's F points)
 #pragma unroll 1
     for (int j = 0; j < count; j++) {
@@ -490,10 +500,70 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
       row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
       pend_store(sc, PB, count_p + j, P);
     }
-    // one inversion: the new S points, and with PIPE the previous piece's F points
-    pend_invert<2 * MULTI_RMAX>(sc, PB, count_p + count);
-    if constexpr (PIPE) {
-      if (count_p) multi_finish(bd, nb, base_p, count_p, lane, k, labels, sc, PB, LB);
+    if constexpr (!PIPE) {
+      pend_invert<MULTI_RMAX>(sc, PB, count);
+    } else {
+      // one inversion: the new S points, piece P's F points, piece Q's label product
+      int ninv = count_p + count;
+      if (count_q) {
+        fe acc;
+        scr_load(acc, sc, QACC);
+        scr_store(sc, PEND_Z(PB, ninv), acc);
+        ninv++;
+      }
+      pend_invert<2 * MULTI_RMAX + 1>(sc, PB, ninv);
+      const auto qf_at = [&](int j, ge& F) {
+        scr_load(F.x, sc, QF + 2 * FW * j);
+        scr_load(F.y, sc, QF + 2 * FW * j + FW);
+      };
+      const auto q_out = [&](int j, const int64_t*& o, uint32_t& off, uint32_t& len, int64_t*& vrow,
+                             uint32_t& vstride) {
+        uint32_t r;
+        bool active;
+        const MultiBatch& b = multi_locate(bd, nb, base_q + (uint32_t)j, lane, &r, &active);
+        o = b.outputs;
+        off = b.offs[r];
+        len = b.lens[r];
+        vrow = nullptr;
+        vstride = 0;
+      };
+      if (count_q) {  // piece Q: its labels, then its flags
+        fe inv;
+        scr_load(inv, sc, PEND_ZI(PB, ninv - 1));
+        hits_q |= labels_backward(inv, k, labels, count_q, sc, LB, qf_at, q_out);
+        multi_emit(bd, nb, base_q, count_q, lane, hits_q);
+        count_q = 0;
+      }
+      if (count_p) {  // piece P: affine F, base compare; its labels wait one iteration
+        uint32_t hits = 0;
+#pragma unroll 1
+        for (int j = 0; j < count_p; j++) {
+          uint32_t r;
+          bool active;
+          const MultiBatch& b = multi_locate(bd, nb, base_p + (uint32_t)j, lane, &r, &active);
+          gej P;
+          fe zi;
+          pend_load(P, sc, PB, j);
+          scr_load(zi, sc, PEND_ZI(PB, j));
+          ge F;
+          gej_to_ge_zinv(F, P, zi);
+          if (k.label_count) {
+            scr_store(sc, QF + 2 * FW * j, F.x);
+            scr_store(sc, QF + 2 * FW * j + FW, F.y);
+          }
+          if (outputs_match(k, b.outputs, b.offs[r], b.lens[r], F.x, fe_upper64(F.x))) hits |= 1u << j;
+        }
+        if (k.label_count) {
+          fe acc;
+          labels_forward(acc, k, labels, count_p, sc, LB, qf_at);
+          scr_store(sc, QACC, acc);
+          base_q = base_p;
+          count_q = count_p;
+          hits_q = hits;
+        } else {
+          multi_emit(bd, nb, base_p, count_p, lane, hits);
+        }
+      }
     }
     // t of each row, then stage B's F = t G + B into slot j
 #pragma unroll 1

@@ -698,23 +698,17 @@ CUDASP_HD bool row_match_base(const gej& R, const fe& zi, const ScanConsts& k, c
   return outputs_match(k, outputs, off, len, F.x, v);
 }
 
-// Label sums F_j + L_l of a thread's pending rows j < count, all with ONE
-// batched inversion over the count x L denominators (Montgomery's trick;
-// prefix products at scratch words lb + (j L + l) FW) instead of one per row.
-// Same values and hits as row_match_finish.  Returns the rows with a label hit
-// as a bit mask.  row_out(j, outputs, off, len, vrow, vstride) gives row j's
-// outputs list and, if vrow != nullptr, where its label values go
-// (vrow[(1 + l) vstride]).
-template <class RowOut>
-CUDASP_HD uint32_t match_labels_core(const ScanConsts& k, const uint32_t* labels, int count, const Scratch& sc, int pb,
-                                     int lb, const RowOut& row_out) {
+// Label sums F_j + L_l of a thread's rows j < count, first half: the count x L
+// denominators' prefix products at scratch words lb + (j L + l) FW, and their
+// product in acc (Montgomery's trick).  f_at(j, F) loads row j's affine F.
+template <class FAt>
+CUDASP_HD void labels_forward(fe& acc, const ScanConsts& k, const uint32_t* labels, int count, const Scratch& sc,
+                              int lb, const FAt& f_at) {
   const int L = (int)k.label_count;
-  fe acc;
   fe_set_int(acc, 1);
   for (int j = 0; j < count; j++) {
     ge F;
-    scr_load(F.x, sc, PEND_X(pb, j));
-    scr_load(F.y, sc, PEND_Y(pb, j));
+    f_at(j, F);
     for (int l = 0; l < L; l++) {
       ge Ll;
       ge_from_words(Ll, labels + (size_t)l * 16);
@@ -724,8 +718,16 @@ CUDASP_HD uint32_t match_labels_core(const ScanConsts& k, const uint32_t* labels
       fe_mul(acc, acc, d);
     }
   }
-  fe inv;
-  fe_inv(inv, acc);
+}
+
+// Second half, from inv = 1 / acc: x of every sum, the values and the
+// compares.  Returns the rows with a label hit as a bit mask.  row_out(j,
+// outputs, off, len, vrow, vstride) gives row j's outputs list and, if
+// vrow != nullptr, where its label values go (vrow[(1 + l) vstride]).
+template <class FAt, class RowOut>
+CUDASP_HD uint32_t labels_backward(fe inv, const ScanConsts& k, const uint32_t* labels, int count, const Scratch& sc,
+                                   int lb, const FAt& f_at, const RowOut& row_out) {
+  const int L = (int)k.label_count;
   uint32_t hits = 0;
   for (int j = count - 1; j >= 0; j--) {
     const int64_t* outputs;
@@ -733,8 +735,7 @@ CUDASP_HD uint32_t match_labels_core(const ScanConsts& k, const uint32_t* labels
     int64_t* vrow;
     row_out(j, outputs, off, len, vrow, vstride);
     ge F;
-    scr_load(F.x, sc, PEND_X(pb, j));
-    scr_load(F.y, sc, PEND_Y(pb, j));
+    f_at(j, F);
     bool hit = false;
     for (int l = L - 1; l >= 0; l--) {
       ge Ll;
@@ -757,6 +758,23 @@ CUDASP_HD uint32_t match_labels_core(const ScanConsts& k, const uint32_t* labels
     if (hit) hits |= 1u << j;
   }
   return hits;
+}
+
+// Label sums F_j + L_l of a thread's pending rows j < count (F affine in the
+// pending slots' X / Y words), all with ONE batched inversion over the
+// count x L denominators instead of one per row.  Same values and hits as
+// row_match_finish.
+template <class RowOut>
+CUDASP_HD uint32_t match_labels_core(const ScanConsts& k, const uint32_t* labels, int count, const Scratch& sc, int pb,
+                                     int lb, const RowOut& row_out) {
+  const auto f_at = [&](int j, ge& F) {
+    scr_load(F.x, sc, PEND_X(pb, j));
+    scr_load(F.y, sc, PEND_Y(pb, j));
+  };
+  fe acc, inv;
+  labels_forward(acc, k, labels, count, sc, lb, f_at);
+  fe_inv(inv, acc);
+  return labels_backward(inv, k, labels, count, sc, lb, f_at, row_out);
 }
 
 // match_labels_core for the rows g + j G of one batch (k_match, the
