@@ -259,3 +259,57 @@ def test_multi_pipelined_equals_unpipelined(torch, monkeypatch, g1, g2):
     same(run_multi(torch, batches, labels), piped)
     monkeypatch.setenv("CUDASP_FUSED_SINGLE", "0")
     same(run_per_batch(torch, batches, labels), piped)
+
+
+def test_many_small_batches(torch, monkeypatch):
+    """600 ragged batches (0..200 rows) cut from one table: more descriptors
+    than the scanner's first staging area holds (it grows), then a second
+    call on the same scanner with the batches in reverse order (the staging
+    ring).  Flags and match-row sets equal the two stage kernels' over the
+    whole table."""
+    from cudasp_amd import Scanner
+    rng = np.random.default_rng(600)
+    sizes = [int(x) for x in rng.integers(0, 201, 600)]
+    sizes[:3] = [0, 1, 64]
+    total = sum(sizes)
+    labels = [LABEL]
+    big = make_batch(torch, 123457, total)
+    plant(torch, [big], labels, every=11)
+    monkeypatch.setenv("CUDASP_FUSED_SINGLE", "0")
+    want = run_per_batch(torch, [big], labels)[0][0]
+    monkeypatch.delenv("CUDASP_FUSED_SINGLE")
+    cuts = np.concatenate([[0], np.cumsum(sizes)])
+    subs = []
+    for i, n in enumerate(sizes):
+        a = int(cuts[i])
+        subs.append(dict(tweak_x=big["tweak_x"][:, a:a + n].contiguous(), tweak_y=big["tweak_y"][:, a:a + n].contiguous(),
+                         outputs=big["outputs"], offsets=big["offsets"][a:a + max(n, 1)],
+                         lengths=big["lengths"][a:a + max(n, 1)], n=n, first=a))
+
+    def descs(order):
+        out = []
+        for i in order:
+            b = subs[i]
+            n = b["n"]
+            b["res"] = (torch.full((max(n, 1),), 7, dtype=torch.uint8, device="cuda"),
+                        torch.zeros(max(n, 1), dtype=torch.int32, device="cuda"),
+                        torch.zeros(1, dtype=torch.int32, device="cuda"))
+            fl, rows, cnt = b["res"]
+            out.append(dict(tweak_x=b["tweak_x"], tweak_y=b["tweak_y"], outputs=b["outputs"], offsets=b["offsets"],
+                            lengths=b["lengths"], flags=fl[:n], match_rows=rows, match_count=cnt))
+        return out
+
+    with Scanner(SCAN, SPEND, labels, max_rows=1000) as s:
+        for order in (range(600), range(599, -1, -1)):
+            s.scan_device_batches(descs(order))
+            s.sync()
+            found = 0
+            for b in subs:
+                n, a = b["n"], b["first"]
+                fl, rows, cnt = b["res"]
+                got = fl[:n].cpu().numpy()
+                assert (got == want[a:a + n]).all(), "batch at row %d" % a
+                c = int(cnt.item())
+                assert sorted(rows[:c].cpu().tolist()) == np.nonzero(want[a:a + n])[0].tolist()
+                found += c
+            assert found == int(want.sum()) > 0
