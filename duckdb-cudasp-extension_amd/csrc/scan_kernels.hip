@@ -361,7 +361,7 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 // with labels).  Exit: every wave leaves when the counter passes the last
 // wave-row and its last pieces are finished.
 #ifndef CUDASP_MULTI_RMAX
-#define CUDASP_MULTI_RMAX 6
+#define CUDASP_MULTI_RMAX 5
 #endif
 constexpr int MULTI_RMAX = CUDASP_MULTI_RMAX;  // rows per thread while much work remains (tuned)
 static_assert(MULTI_RMAX >= 2 && MULTI_RMAX <= 16, "multi-batch rows per thread");
@@ -1121,7 +1121,7 @@ static bool multi_ok(const cudasp_scanner* s) {
 }
 
 // Guided-scheduling thresholds of k_scan_multi in hundredths of the grid's
-// waves: 6 rows per thread while more than G2 x waves wave-rows remain, 2
+// waves: MULTI_RMAX rows per thread while more than G2 x waves wave-rows remain, 2
 // while more than G1 x waves, then 1 (CUDASP_MULTI_G1 / CUDASP_MULTI_G2
 // override the defaults for tuning).
 static uint32_t multi_threshold_x100(const char* env, uint32_t dflt_x100) {

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-RMAX = 6
+RMAX = 5  # CUDASP_MULTI_RMAX
 
 
 @pytest.fixture(scope="module")
@@ -59,7 +59,7 @@ def test_every_row_once(emu, sizes, waves, g1, g2, seed):
 
 
 def test_guided_tail(emu):
-    """With the bench's thresholds the bulk runs 6 rows per thread and the tail
+    """With the bench's thresholds the bulk runs RMAX rows per thread and the tail
     goes in 2- and 1-row pieces.  The replay lets a wave size its piece from a
     counter value up to a whole round of the other waves old (on the GPU the
     read and the add are back to back), so only the shape is checked."""
