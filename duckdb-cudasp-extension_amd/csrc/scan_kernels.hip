@@ -361,7 +361,7 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 // with labels).  Exit: every wave leaves when the counter passes the last
 // wave-row and its last pieces are finished.
 #ifndef CUDASP_MULTI_RMAX
-#define CUDASP_MULTI_RMAX 5
+#define CUDASP_MULTI_RMAX 6
 #endif
 constexpr int MULTI_RMAX = CUDASP_MULTI_RMAX;  // rows per thread while much work remains (tuned)
 static_assert(MULTI_RMAX >= 2 && MULTI_RMAX <= 16, "multi-batch rows per thread");
@@ -1546,7 +1546,13 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
     total_wr += (b.n + 63u) / 64u;
   }
   if (md.empty()) return CUDASP_OK;
-  return launch_multi(s, md, total_wr, st, MULTI_RMAX, multi_threshold_x100("CUDASP_MULTI_G1", 150),
+  // CUDASP_MULTI_ROWS = 2..MULTI_RMAX: rows per thread of the bulk (tuning)
+  uint32_t rmax = MULTI_RMAX;
+  if (const char* e = getenv("CUDASP_MULTI_ROWS")) {
+    const long v = atol(e);
+    if (v >= 2 && v <= MULTI_RMAX) rmax = (uint32_t)v;
+  }
+  return launch_multi(s, md, total_wr, st, rmax, multi_threshold_x100("CUDASP_MULTI_G1", 150),
                       multi_threshold_x100("CUDASP_MULTI_G2", 400), 0);
 }
 

@@ -183,7 +183,7 @@ def test_multi_16_labels_variable_outputs(torch):
 @pytest.mark.parametrize("g1,g2", [("0", "0"), ("100000", "100000"), ("0", "100000"), ("150", "400")])
 def test_multi_guided_regimes(torch, monkeypatch, g1, g2):
     """Every chunk size regime of the guided schedule (CUDASP_MULTI_G1/G2,
-    hundredths of the grid's waves): all 5 (MULTI_RMAX), all 1, all 2 rows per thread, and
+    hundredths of the grid's waves): all 6 (MULTI_RMAX), all 1, all 2 rows per thread, and
     the default mix, give the per-batch results."""
     monkeypatch.setenv("CUDASP_MULTI_G1", g1)
     monkeypatch.setenv("CUDASP_MULTI_G2", g2)

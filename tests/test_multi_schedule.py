@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-RMAX = 5  # CUDASP_MULTI_RMAX
+RMAX = 6  # CUDASP_MULTI_RMAX
 
 
 @pytest.fixture(scope="module")
