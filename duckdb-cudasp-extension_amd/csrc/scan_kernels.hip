@@ -352,9 +352,9 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 // atomic per piece): R = rmax (<= MULTI_RMAX) rows per thread while more than
 // g2 wave-rows remain, then 2, then 1 below g1 -- guided self-scheduling, so
 // the last pieces are short and the GPU stays full to the end (a fused
-// single-batch launch uses g1 = g2 = 0: rmax rows per thread throughout).  A thread's R rows share
-// one Z inversion in stage A (t stays in the thread), then one Z inversion and
-// one label inversion in stage B.  PIPE (the default): a wave finishes a piece's
+// single-batch launch uses g1 = g2 = 0: rmax rows per thread throughout).  A
+// thread's R rows share one Z inversion in stage A (t stays in the thread),
+// then one Z inversion and one label inversion in stage B.  PIPE (the default): a wave finishes a piece's
 // stage B one iteration later and its labels one more iteration later, so the
 // piece's stage-B Z inversion and its label inversion join the following
 // pieces' stage-A inversions -- one inversion per piece instead of two (three
