@@ -443,6 +443,17 @@ __device__ __forceinline__ void multi_finish(const MultiBatch* __restrict__ bd, 
   multi_emit(bd, nb, base, count, lane, hits);
 }
 
+// Measurement builds only (-DCUDASP_MULTI_TRACE=1, tools/multi_trace.py): per
+// wave of the last k_scan_multi launch, its start and end (s_memrealtime
+// ticks), pieces and wave-rows, read back by cudasp_debug_multi_trace.
+#ifndef CUDASP_MULTI_TRACE
+#define CUDASP_MULTI_TRACE 0
+#endif
+#if CUDASP_MULTI_TRACE
+constexpr uint32_t MULTI_TRACE_WAVES = 8192;
+__device__ uint64_t g_multi_trace[MULTI_TRACE_WAVES * 4];
+#endif
+
 template <int FBB, bool PIPE>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const MultiBatch* __restrict__ bd, uint32_t nb,
                                                                    uint32_t total_wr, const int8_t* __restrict__ naf,
@@ -465,6 +476,10 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
   uint32_t base_p = 0, base_q = 0, hits_q = 0;
   int count_p = 0, count_q = 0;
   bool more = true;
+#if CUDASP_MULTI_TRACE
+  const uint64_t trace_t0 = wall_clock64();
+  uint32_t trace_pieces = 0, trace_rows = 0;
+#endif
   for (;;) {
     uint32_t base = 0;
     int count = 0;
@@ -484,6 +499,10 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
         count = (int)(R < total_wr - base ? R : total_wr - base);
     }
     if (count == 0 && count_p == 0 && count_q == 0) break;
+#if CUDASP_MULTI_TRACE
+    trace_pieces += count ? 1u : 0u;
+    trace_rows += (uint32_t)count;
+#endif
     // stage A: S = d T of the piece's rows (after the previous piece's F points)
 #pragma unroll 1
     for (int j = 0; j < count; j++) {
@@ -587,6 +606,15 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
       multi_finish(bd, nb, base, count, lane, k, labels, sc, PB, LB);
     }
   }
+#if CUDASP_MULTI_TRACE
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
+  if (lane == 0 && wave < MULTI_TRACE_WAVES) {
+    g_multi_trace[wave * 4 + 0] = trace_t0;
+    g_multi_trace[wave * 4 + 1] = wall_clock64();
+    g_multi_trace[wave * 4 + 2] = trace_pieces;
+    g_multi_trace[wave * 4 + 3] = trace_rows;
+  }
+#endif
 }
 
 // One entry per thread of a table with `windows` windows of `entries` odd
@@ -1555,6 +1583,22 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
   return launch_multi(s, md, total_wr, st, rmax, multi_threshold_x100("CUDASP_MULTI_G1", 150),
                       multi_threshold_x100("CUDASP_MULTI_G2", 400), 0);
 }
+
+#if CUDASP_MULTI_TRACE
+// Measurement builds only (not in include/cudasp_abi.h): copies up to
+// max_waves records (start, end, pieces, wave-rows) of the last k_scan_multi
+// launch; returns the number of records and the realtime clock in *hz.
+extern "C" int cudasp_debug_multi_trace(uint64_t* out, uint32_t max_waves, int* hz) {
+  const uint32_t n = max_waves < MULTI_TRACE_WAVES ? max_waves : MULTI_TRACE_WAVES;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_multi_trace), (size_t)n * 4 * sizeof(uint64_t)));
+  int dev = 0, rate_khz = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev));
+  *hz = rate_khz * 1000;
+  return (int)n;
+}
+#endif
 
 int cudasp_row_values_device(cudasp_scanner* s, const uint32_t* d_tweak_x, const uint32_t* d_tweak_y, uint32_t n,
                              uint32_t* d_t, int64_t* d_values, void* stream) {
