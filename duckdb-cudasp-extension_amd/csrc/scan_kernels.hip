@@ -349,10 +349,11 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 // space in 64-row "wave-rows" (batch b starts at wave-row first_wr; its last
 // wave-row is padded, padding lanes compute batch row 0 and store nothing).
 // Each wavefront takes R consecutive wave-rows from a device counter (one
-// atomic per piece): R = rmax (<= MULTI_RMAX) rows per thread while more than
-// g2 wave-rows remain, then 2, then 1 below g1 -- guided self-scheduling, so
-// the last pieces are short and the GPU stays full to the end (a fused
-// single-batch launch uses g1 = g2 = 0: rmax rows per thread throughout).  A
+// atomic per piece) of R = (remaining wave-rows) / (grid waves) rows per
+// thread, at least 1 and at most rmax (<= MULTI_RMAX) -- guided
+// self-scheduling (multi_piece_rows), so no piece outlasts the work left to
+// the other waves and the GPU stays full to the end (a fused single-batch
+// launch uses g1 = 0: rmax rows per thread throughout).  A
 // thread's R rows share one Z inversion in stage A (t stays in the thread),
 // then one Z inversion and one label inversion in stage B.  PIPE (the default): a wave finishes a piece's
 // stage B one iteration later and its labels one more iteration later, so the
@@ -1148,10 +1149,10 @@ static bool multi_ok(const cudasp_scanner* s) {
          (uint64_t)multi_scratch_words(s->consts.label_count, s->multi_pipe) * 4 * BLOCK <= (1ull << 32) - 1;
 }
 
-// Guided-scheduling thresholds of k_scan_multi in hundredths of the grid's
-// waves: MULTI_RMAX rows per thread while more than G2 x waves wave-rows remain, 2
-// while more than G1 x waves, then 1 (CUDASP_MULTI_G1 / CUDASP_MULTI_G2
-// override the defaults for tuning).
+// Guided-scheduling parameters of k_scan_multi in hundredths of the grid's
+// waves (multi_piece_rows): a piece is rem / (G1 x waves) rows; rmax rows
+// while more than G2 x waves remain (0: no such phase).  CUDASP_MULTI_G1 /
+// CUDASP_MULTI_G2 override the defaults (100 / 0) for tuning.
 static uint32_t multi_threshold_x100(const char* env, uint32_t dflt_x100) {
   if (const char* e = getenv(env)) {
     const long v = atol(e);
@@ -1180,7 +1181,7 @@ static MultiBatch multi_desc(const uint32_t* tx, const uint32_t* ty, const int64
 
 // One k_scan_multi launch over the described batches (total_wr wave-rows):
 // uploads the descriptors, resets the work counter, launches on `st`.  rmax:
-// rows per thread of the bulk; g1/g2: guided thresholds (hundredths of the
+// rows per thread of the bulk; g1/g2: guided-scheduling parameters (hundredths of the
 // grid's waves); blocks: 0 = the persistent grid (every wave slot), else a
 // grid of that many blocks.
 static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, uint64_t total_wr, hipStream_t st,
@@ -1580,8 +1581,8 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
     const long v = atol(e);
     if (v >= 2 && v <= MULTI_RMAX) rmax = (uint32_t)v;
   }
-  return launch_multi(s, md, total_wr, st, rmax, multi_threshold_x100("CUDASP_MULTI_G1", 150),
-                      multi_threshold_x100("CUDASP_MULTI_G2", 400), 0);
+  return launch_multi(s, md, total_wr, st, rmax, multi_threshold_x100("CUDASP_MULTI_G1", 100),
+                      multi_threshold_x100("CUDASP_MULTI_G2", 0), 0);
 }
 
 #if CUDASP_MULTI_TRACE

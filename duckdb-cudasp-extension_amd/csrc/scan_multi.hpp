@@ -47,10 +47,15 @@ CUDASP_HD uint32_t multi_row(const MultiBatch& b, uint32_t w, uint32_t lane, boo
 }
 
 // Wave-rows of the next piece (= rows per thread) with `rem` wave-rows left:
-// rmax while more than g2 remain, then 2, then 1 below g1 (guided
-// self-scheduling; g1 = g2 = 0 gives rmax throughout).
+// guided self-scheduling, rem / g1 rows (at least 1, at most rmax; g1 = the
+// grid's waves for the classic rule), so a piece is never longer than the
+// time the other waves need for what remains and the waves run out of work
+// together; rmax while more than g2 wave-rows remain (g2 = 0: the rule
+// throughout), and rmax throughout when g1 = 0.
 CUDASP_HD uint32_t multi_piece_rows(uint32_t rem, uint32_t g1, uint32_t g2, uint32_t rmax) {
-  return rem > g2 ? rmax : (rem > g1 ? (rmax < 2u ? rmax : 2u) : 1u);
+  if (g1 == 0 || (g2 != 0 && rem > g2)) return rmax;
+  const uint32_t r = rem / g1;
+  return r < 1u ? 1u : (r > rmax ? rmax : r);
 }
 
 }  // namespace cudasp

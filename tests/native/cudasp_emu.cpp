@@ -381,11 +381,12 @@ int emu_row_values_grouped(const uint8_t scan[32], const uint8_t spend[64], cons
 // counter value, as on the GPU).  Descriptors are laid out as
 // cudasp_scan_device_batches lays them out (empty batches skipped, each batch
 // from a fresh wave-row).  cover[sum(sizes)] counts how often each batch row
-// was scanned by an active lane; stats[0..4] = pieces of rmax / 2 / 1 rows,
-// pieces in total, pieces whose rows ran past the last wave-row.
+// was scanned by an active lane; stats[r - 1] (r = 1..16) = pieces of r rows,
+// stats[16] = pieces in total, stats[17] = pieces whose rows ran past the last
+// wave-row.
 int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, uint32_t g1, uint32_t g2,
                        uint32_t rmax, uint64_t seed, uint32_t* cover, uint64_t* stats) {
-  if (waves == 0 || rmax < 1) return CUDASP_ERR_INVALID_ARG;
+  if (waves == 0 || rmax < 1 || rmax > 16) return CUDASP_ERR_INVALID_ARG;
   std::vector<MultiBatch> md;
   std::vector<uint64_t> row0;  // index of each descriptor's row 0 in cover
   uint64_t total_wr = 0, at = 0;
@@ -401,7 +402,7 @@ int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, ui
     at += sizes[i];
   }
   for (uint64_t i = 0; i < at; i++) cover[i] = 0;
-  for (int i = 0; i < 5; i++) stats[i] = 0;
+  for (int i = 0; i < 18; i++) stats[i] = 0;
   if (md.empty()) return 0;
   const uint32_t nb = (uint32_t)md.size(), twr = (uint32_t)total_wr;
   uint32_t counter = 0;
@@ -429,9 +430,9 @@ int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, ui
       live--;
       continue;
     }
-    stats[R == rmax ? 0 : (R == 2 ? 1 : 2)]++;
-    stats[3]++;
-    if (R > twr - base) stats[4]++;
+    stats[R - 1]++;
+    stats[16]++;
+    if (R > twr - base) stats[17]++;
     const int cnt = (int)(R < twr - base ? R : twr - base);
     for (int j = 0; j < cnt; j++) {
       const uint32_t w = base + (uint32_t)j;

@@ -180,13 +180,17 @@ def test_multi_16_labels_variable_outputs(torch):
     same(run_multi(torch, batches, labels), want)
 
 
-@pytest.mark.parametrize("g1,g2", [("0", "0"), ("100000", "100000"), ("0", "100000"), ("150", "400")])
-def test_multi_guided_regimes(torch, monkeypatch, g1, g2):
+@pytest.mark.parametrize("g1,g2,rows", [("0", "0", None), ("100000", "100000", None), ("0", "0", "2"),
+                                         ("100", "0", None), ("150", "400", None)])
+def test_multi_guided_regimes(torch, monkeypatch, g1, g2, rows):
     """Every chunk size regime of the guided schedule (CUDASP_MULTI_G1/G2,
-    hundredths of the grid's waves): all 6 (MULTI_RMAX), all 1, all 2 rows per thread, and
-    the default mix, give the per-batch results."""
+    hundredths of the grid's waves; CUDASP_MULTI_ROWS): all 6 (MULTI_RMAX),
+    all 1, all 2 rows per thread, the default rule (every size from 6 down to
+    1) and a leading 6-row phase, give the per-batch results."""
     monkeypatch.setenv("CUDASP_MULTI_G1", g1)
     monkeypatch.setenv("CUDASP_MULTI_G2", g2)
+    if rows:
+        monkeypatch.setenv("CUDASP_MULTI_ROWS", rows)
     labels = [LABEL]
     batches = [make_batch(torch, 555 + 20000 * i, n) for i, n in enumerate([9000, 17, 4000])]
     plant(torch, batches, labels)
@@ -241,7 +245,7 @@ def test_multi_100_labels(torch, monkeypatch):
     assert sum(c for _, _, c in got) == len(range(0, 1500, 3)) + len(range(1, 700, 3))
 
 
-@pytest.mark.parametrize("g1,g2", [("0", "0"), ("150", "400"), ("100000", "100000")])
+@pytest.mark.parametrize("g1,g2", [("0", "0"), ("100", "0"), ("100000", "100000")])
 def test_multi_pipelined_equals_unpipelined(torch, monkeypatch, g1, g2):
     """The default schedule finishes a piece's stage B one iteration later,
     with its Z inversion merged into the next piece's stage-A inversion

@@ -1,8 +1,8 @@
 """CPU: the work distribution of the multi-batch persistent kernel (k_scan_multi,
 duckdb-cudasp-extension_amd/csrc/scan_multi.hpp) replayed on the host with the
 kernel's own helpers.  Whatever the interleaving of the waves' counter reads and
-adds, every row of every batch is scanned by exactly one active lane, padding
-lanes stay inactive, and the guided schedule ends on one-row pieces."""
+adds, every row of every batch is scanned by exactly one active lane and padding
+lanes stay inactive; the guided rule sizes pieces by the work left."""
 import ctypes
 import os
 import subprocess
@@ -24,23 +24,30 @@ def emu():
 
 
 def schedule(emu, sizes, waves, g1, g2, rmax=RMAX, seed=1):
+    """cover per row; stats: pieces by size (index r - 1), total, past the end."""
     sizes = np.asarray(sizes, dtype=np.uint32)
     cover = np.zeros(max(1, int(sizes.sum())), dtype=np.uint32)
-    stats = np.zeros(5, dtype=np.uint64)
+    stats = np.zeros(18, dtype=np.uint64)
     rc = emu.emu_multi_schedule(sizes.ctypes.data, len(sizes), waves, g1, g2, rmax, seed,
                                 cover.ctypes.data, stats.ctypes.data)
     assert rc == 0
     return cover[: int(sizes.sum())], stats
 
 
+def wave_rows(sizes):
+    return sum((n + 63) // 64 for n in sizes)
+
+
 # the GPU test's ragged batch set (tests/test_multi_batch_gpu.py), bench-like
-# batches, and a single fused batch (g1 = g2 = 0)
+# batches, and a single fused batch (g1 = 0); g1 = waves is the default rule,
+# g2 > 0 adds a leading rmax phase
 CASES = [
+    ([3001, 64, 1, 0, 129, 70000, 65, 2047], 48, 48, 0),
     ([3001, 64, 1, 0, 129, 70000, 65, 2047], 48, 72, 192),
-    ([300000] * 5, 3072, 4608, 12288),
-    ([0, 0, 7], 12, 18, 48),
-    ([1] * 300, 12, 18, 48),
-    ([65536 + 63, 64 * 1000 + 1], 768, 1152, 3072),
+    ([300000] * 5, 3072, 3072, 0),
+    ([0, 0, 7], 12, 12, 0),
+    ([1] * 300, 12, 12, 0),
+    ([65536 + 63, 64 * 1000 + 1], 768, 768, 0),
     ([300000], 294, 0, 0),
 ]
 
@@ -51,35 +58,53 @@ def test_every_row_once(emu, sizes, waves, g1, g2, seed):
     cover, stats = schedule(emu, sizes, waves, g1, g2, seed=seed)
     assert cover.size == sum(sizes)
     assert np.all(cover == 1)
-    wr = sum((n + 63) // 64 for n in sizes)
-    assert stats[3] == stats[0] + stats[1] + stats[2]
+    assert stats[16] == stats[:16].sum()
     # pieces past the end only at the tail: at most one per wave
-    assert stats[4] <= waves
-    assert stats[0] * RMAX + stats[1] * 2 + stats[2] >= wr
+    assert stats[17] <= waves
+    assert sum((r + 1) * int(stats[r]) for r in range(16)) >= wave_rows(sizes)
+    assert stats[RMAX:16].sum() == 0  # never more than rmax rows
 
 
-def test_guided_tail(emu):
-    """With the bench's thresholds the bulk runs RMAX rows per thread and the tail
-    goes in 2- and 1-row pieces.  The replay lets a wave size its piece from a
-    counter value up to a whole round of the other waves old (on the GPU the
-    read and the add are back to back), so only the shape is checked."""
-    waves, g1, g2 = 3072, 4608, 12288
+def test_guided_rule_sizes(emu):
+    """The default rule (g1 = waves): most of a long step in rmax pieces, then
+    every size down to 1 as the work runs out.  The replay lets a wave size its
+    piece from a counter value up to a whole round of the other waves old (on
+    the GPU the read and the add are back to back), so only the shape is
+    checked."""
+    waves = 3072
     sizes = [300000] * 20
-    cover, stats = schedule(emu, sizes, waves, g1, g2)
+    cover, stats = schedule(emu, sizes, waves, waves, 0)
     assert np.all(cover == 1)
-    wr = sum((n + 63) // 64 for n in sizes)
-    assert stats[0] * RMAX >= wr - g2 - RMAX * waves  # bulk in rmax pieces (stale reads aside)
-    assert stats[1] > 0 and stats[2] > 0
+    wr = wave_rows(sizes)
+    assert RMAX * int(stats[RMAX - 1]) >= wr - RMAX * RMAX * 2 * waves  # the bulk in rmax pieces
+    assert all(stats[r] > 0 for r in range(RMAX))  # sizes 1 .. rmax all occur
+
+
+def test_piece_rows_rule(emu):
+    """multi_piece_rows itself, through one wave (no interleaving): a piece
+    with rem wave-rows left has min(rmax, max(1, rem // g1)) rows."""
+    waves, g1 = 1, 10
+    sizes = [64 * 100]
+    _, stats = schedule(emu, sizes, waves, g1, 0)
+    rem, want = 100, np.zeros(18, dtype=np.uint64)
+    while rem > 0:
+        r = min(RMAX, max(1, rem // g1))
+        want[r - 1] += 1
+        want[16] += 1
+        if r > rem:
+            want[17] += 1
+        rem -= r
+    assert (stats == want).all()
 
 
 def test_fixed_pieces(emu):
-    """g1 = g2 = 0 (the fused single-batch launch): every piece has rmax rows."""
+    """g1 = 0 (the fused single-batch launch): every piece has rmax rows."""
     cover, stats = schedule(emu, [100000], 300, 0, 0)
     assert np.all(cover == 1)
-    assert stats[1] == 0 and stats[2] == 0
-    assert stats[0] == -(-((100000 + 63) // 64) // RMAX)
+    assert stats[16] == stats[RMAX - 1]
+    assert stats[RMAX - 1] == -(-((100000 + 63) // 64) // RMAX)
 
 
 def test_empty(emu):
-    cover, stats = schedule(emu, [0, 0], 12, 18, 48)
-    assert cover.size == 0 and stats[3] == 0
+    cover, stats = schedule(emu, [0, 0], 12, 12, 0)
+    assert cover.size == 0 and stats[16] == 0
