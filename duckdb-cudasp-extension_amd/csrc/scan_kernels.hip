@@ -462,7 +462,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
                                                                    const uint32_t* __restrict__ labels,
                                                                    uint32_t* __restrict__ scr,
                                                                    uint32_t* __restrict__ counter, uint32_t g1,
-                                                                   uint32_t g2, uint32_t rmax) {
+                                                                   uint32_t g2, uint32_t rmax, uint32_t adaptive) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = make_scratch(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
@@ -477,6 +477,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
   uint32_t base_p = 0, base_q = 0, hits_q = 0;
   int count_p = 0, count_q = 0;
   bool more = true;
+  uint32_t mine = 0;  // wave-rows this wave has claimed (lane 0)
 #if CUDASP_MULTI_TRACE
   const uint64_t trace_t0 = wall_clock64();
   uint32_t trace_pieces = 0, trace_rows = 0;
@@ -489,8 +490,9 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
       if (lane == 0) {
         const uint32_t prev = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t rem = prev < total_wr ? total_wr - prev : 0u;
-        R = multi_piece_rows(rem, g1, g2, rmax);
+        R = adaptive ? multi_piece_rows_adaptive(rem, prev, mine, g1, g2, rmax) : multi_piece_rows(rem, g1, g2, rmax);
         base = atomicAdd(counter, R);
+        mine += R;
       }
       base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
       R = (uint32_t)__builtin_amdgcn_readfirstlane((int)R);
@@ -971,6 +973,9 @@ struct cudasp_scanner {
   // k_scan_multi with the pipelined schedule (one Z inversion per piece);
   // CUDASP_MULTI_PIPE=0 selects the two-inversion schedule (A/B)
   bool multi_pipe = true;
+  // k_scan_multi pieces sized by each wave's share of the work done
+  // (multi_piece_rows_adaptive); CUDASP_MULTI_ADAPT=0 selects the plain rule
+  bool multi_adaptive = true;
 };
 
 namespace {
@@ -1257,7 +1262,8 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
   auto kf = s->multi_pipe ? (s->fb_bits == 26 ? k_scan_multi<26, true> : k_scan_multi<22, true>)
                           : (s->fb_bits == 26 ? k_scan_multi<26, false> : k_scan_multi<22, false>);
   hipLaunchKernelGGL(kf, dim3((uint32_t)blocks), dim3(BLOCK), 0, st, s->d_multi, nb, (uint32_t)total_wr, s->d_naf,
-                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, s->d_counter, g1, g2, rmax);
+                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, s->d_counter, g1, g2, rmax,
+                     s->multi_adaptive ? 1u : 0u);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
 }
@@ -1357,6 +1363,7 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
     s->fill_threads_b = (uint32_t)cus * 4 * CUDASP_WAVES_B * 64 / 4;
     if (const char* f = getenv("CUDASP_FUSED_SINGLE")) s->fused_single = atoi(f) != 0;
     if (const char* f = getenv("CUDASP_MULTI_PIPE")) s->multi_pipe = atoi(f) != 0;
+    if (const char* f = getenv("CUDASP_MULTI_ADAPT")) s->multi_adaptive = atoi(f) != 0;
     if (const char* f = getenv("CUDASP_ROWS_A_FORCE")) {
       const int r = atoi(f);
       if (r == 1 || r == 2 || r == ROWS_A) s->rows_a_force = r;

@@ -58,4 +58,20 @@ CUDASP_HD uint32_t multi_piece_rows(uint32_t rem, uint32_t g1, uint32_t g2, uint
   return r < 1u ? 1u : (r > rmax ? rmax : r);
 }
 
+// The adaptive form: a wave that has already claimed `mine` wave-rows of the
+// `prev` claimed by all sizes its next piece by its own share of the work done,
+// rem x mine / prev rows (at least 1, at most rmax), so that the piece ends
+// when the other waves finish what remains, however unevenly the SIMDs share
+// their issue slots among resident waves (the oldest wave of a SIMD issues
+// first: on gfx950 the three waves of a SIMD progress at ~1 : 0.3 : 0.05).
+// A wave's first piece is one wave-row (its speed is not known yet); g1 = 0
+// (a fused single-batch launch) keeps rmax throughout.
+CUDASP_HD uint32_t multi_piece_rows_adaptive(uint32_t rem, uint32_t prev, uint32_t mine, uint32_t g1, uint32_t g2,
+                                             uint32_t rmax) {
+  if (g1 == 0) return rmax;
+  if (mine == 0 || prev == 0) return 1u;
+  const uint64_t r = (uint64_t)rem * mine / prev;
+  return r < 1u ? 1u : (r > rmax ? rmax : (uint32_t)r);
+}
+
 }  // namespace cudasp

@@ -375,7 +375,8 @@ int emu_row_values_grouped(const uint8_t scan[32], const uint8_t spend[64], cons
   return 0;
 }
 
-// k_scan_multi's work distribution replayed on the CPU: `waves` wavefronts
+// k_scan_multi's work distribution replayed on the CPU (adaptive: the
+// multi_piece_rows_adaptive sizing of the default launch): `waves` wavefronts
 // claim pieces from one counter with the kernel's read-then-add protocol, in a
 // seeded random interleaving (so a wave may size its piece from a stale
 // counter value, as on the GPU).  Descriptors are laid out as
@@ -385,7 +386,7 @@ int emu_row_values_grouped(const uint8_t scan[32], const uint8_t spend[64], cons
 // stats[16] = pieces in total, stats[17] = pieces whose rows ran past the last
 // wave-row.
 int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, uint32_t g1, uint32_t g2,
-                       uint32_t rmax, uint64_t seed, uint32_t* cover, uint64_t* stats) {
+                       uint32_t rmax, uint32_t adaptive, uint64_t seed, uint32_t* cover, uint64_t* stats) {
   if (waves == 0 || rmax < 1 || rmax > 16) return CUDASP_ERR_INVALID_ARG;
   std::vector<MultiBatch> md;
   std::vector<uint64_t> row0;  // index of each descriptor's row 0 in cover
@@ -408,6 +409,7 @@ int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, ui
   uint32_t counter = 0;
   std::vector<uint8_t> done(waves, 0);
   std::vector<int32_t> sized(waves, -1);  // piece size read from the counter, -1 = not read yet
+  std::vector<uint32_t> mine(waves, 0);   // wave-rows each wave has claimed
   uint64_t x = seed * 6364136223846793005ull + 1442695040888963407ull;
   uint32_t live = waves;
   while (live) {
@@ -418,12 +420,14 @@ int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, ui
     while (done[v]) v = (v + 1) % waves;
     if (sized[v] < 0) {  // lane 0 reads the counter and sizes its piece
       const uint32_t rem = counter < twr ? twr - counter : 0u;
-      sized[v] = (int32_t)multi_piece_rows(rem, g1, g2, rmax);
+      sized[v] = (int32_t)(adaptive ? multi_piece_rows_adaptive(rem, counter, mine[v], g1, g2, rmax)
+                                    : multi_piece_rows(rem, g1, g2, rmax));
       continue;
     }
     const uint32_t R = (uint32_t)sized[v];
     const uint32_t base = counter;  // atomicAdd
     counter += R;
+    mine[v] += R;
     sized[v] = -1;
     if (base >= twr) {
       done[v] = 1;

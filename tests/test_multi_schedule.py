@@ -19,16 +19,16 @@ def emu():
     subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])
     lib = ctypes.CDLL(os.path.join(HERE, "native", "libcudasp_emu29.so"))
     V, U = ctypes.c_void_p, ctypes.c_uint32
-    lib.emu_multi_schedule.argtypes = [V, U, U, U, U, U, ctypes.c_uint64, V, V]
+    lib.emu_multi_schedule.argtypes = [V, U, U, U, U, U, U, ctypes.c_uint64, V, V]
     return lib
 
 
-def schedule(emu, sizes, waves, g1, g2, rmax=RMAX, seed=1):
+def schedule(emu, sizes, waves, g1, g2, rmax=RMAX, seed=1, adaptive=0):
     """cover per row; stats: pieces by size (index r - 1), total, past the end."""
     sizes = np.asarray(sizes, dtype=np.uint32)
     cover = np.zeros(max(1, int(sizes.sum())), dtype=np.uint32)
     stats = np.zeros(18, dtype=np.uint64)
-    rc = emu.emu_multi_schedule(sizes.ctypes.data, len(sizes), waves, g1, g2, rmax, seed,
+    rc = emu.emu_multi_schedule(sizes.ctypes.data, len(sizes), waves, g1, g2, rmax, adaptive, seed,
                                 cover.ctypes.data, stats.ctypes.data)
     assert rc == 0
     return cover[: int(sizes.sum())], stats
@@ -54,8 +54,9 @@ CASES = [
 
 @pytest.mark.parametrize("sizes,waves,g1,g2", CASES)
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_every_row_once(emu, sizes, waves, g1, g2, seed):
-    cover, stats = schedule(emu, sizes, waves, g1, g2, seed=seed)
+@pytest.mark.parametrize("adaptive", [0, 1])
+def test_every_row_once(emu, sizes, waves, g1, g2, seed, adaptive):
+    cover, stats = schedule(emu, sizes, waves, g1, g2, seed=seed, adaptive=adaptive)
     assert cover.size == sum(sizes)
     assert np.all(cover == 1)
     assert stats[16] == stats[:16].sum()
@@ -108,3 +109,26 @@ def test_fixed_pieces(emu):
 def test_empty(emu):
     cover, stats = schedule(emu, [0, 0], 12, 12, 0)
     assert cover.size == 0 and stats[16] == 0
+
+
+def test_adaptive_rule(emu):
+    """The default sizing (multi_piece_rows_adaptive) through one wave: the
+    first piece is one wave-row; then the wave's share of the claimed work is
+    all of it, so pieces are min(rmax, rem) rows: 100 = 1 + 16 x 6 + 3."""
+    _, stats = schedule(emu, [64 * 100], 1, 1, 0, adaptive=1)
+    want = np.zeros(18, dtype=np.uint64)
+    want[0] = 1
+    want[RMAX - 1] = 16
+    want[2] = 1
+    want[16] = want[:16].sum()
+    assert (stats == want).all()
+
+
+def test_adaptive_long_step(emu):
+    """Bench-like step with the adaptive sizing: the bulk still runs in rmax
+    pieces (each wave's first piece is one wave-row)."""
+    waves = 3072
+    sizes = [300000] * 20
+    cover, stats = schedule(emu, sizes, waves, waves, 0, adaptive=1)
+    assert np.all(cover == 1)
+    assert RMAX * int(stats[RMAX - 1]) >= 0.8 * wave_rows(sizes)
