@@ -349,11 +349,13 @@ __global__ __launch_bounds__(BLOCK) void k_or_flags(const uint8_t* __restrict__ 
 // space in 64-row "wave-rows" (batch b starts at wave-row first_wr; its last
 // wave-row is padded, padding lanes compute batch row 0 and store nothing).
 // Each wavefront takes R consecutive wave-rows from a device counter (one
-// atomic per piece) of R = (remaining wave-rows) / (grid waves) rows per
-// thread, at least 1 and at most rmax (<= MULTI_RMAX) -- guided
-// self-scheduling (multi_piece_rows), so no piece outlasts the work left to
-// the other waves and the GPU stays full to the end (a fused single-batch
-// launch uses g1 = 0: rmax rows per thread throughout).  A
+// atomic per piece) of R rows per thread, 1 .. rmax (<= MULTI_RMAX): by
+// default the wave's share of the work left, rem x (rows it has claimed) /
+// (rows all have claimed) (multi_piece_rows_adaptive: the waves of a SIMD
+// progress at very different rates, so each is sized by its own), else
+// guided self-scheduling, rem / (grid waves) (multi_piece_rows) -- no piece
+// outlasts the work left to the other waves and the GPU stays full to the end
+// (a fused single-batch launch uses g1 = 0: rmax rows per thread throughout).  A
 // thread's R rows share one Z inversion in stage A (t stays in the thread),
 // then one Z inversion and one label inversion in stage B.  PIPE (the default): a wave finishes a piece's
 // stage B one iteration later and its labels one more iteration later, so the
