@@ -8,7 +8,9 @@ Contract (see DESIGN.md "Measurement"):
 
 Workload (BASELINE.json metric "tx/sec through cudasp_scan on 32M-row tweak
 table at 1/2/4/8 MI355X", configs[3]): ONE 32.7M-row synthetic table, cut into
-the reference's batch_size = 300000-row batches; batch b is scanned by rank
+batches of at most the reference's default 300000 rows (at N = 1 exactly
+300000; at N > 1 the largest size whose batch count is a multiple of N, so
+every rank gets the same number of batches: balanced_batch_size); batch b is scanned by rank
 b mod N (the product's assignment, cudasp_assign_gpu; the reference
 round-robins its executor threads over GPUs, src/cudasp_extension.cu:523-529),
 so the total work is fixed as N grows (`--shard weak` gives every rank its own
@@ -239,6 +241,22 @@ def shard_first_row(rank, rows_per_rank):
     """Global index of a rank's first row (weak scaling: rank r owns rows
     [r * rows_per_rank, (r + 1) * rows_per_rank) of one conceptual table)."""
     return rank * rows_per_rank
+
+
+def balanced_batch_size(rows, world, cap=300_000):
+    """The bench's default batch_size for the round-robin table: the largest
+    size <= cap (the reference's default batch_size) whose batch count is a
+    multiple of `world`, so that round-robin gives every rank the same number
+    of batches.  At N = 1 this is cap itself (109 batches of 300000 rows);
+    at N = 8 it is 112 batches of 291965 rows (14 per rank) instead of
+    300000-row batches 14/13 per rank, whose largest share sets the job time.
+    batch_size is the SQL function's own parameter (`batch_size := INTEGER`,
+    src/cudasp_extension.cu:626-635); BASELINE configs[3] does not fix it."""
+    if rows <= 0:
+        return cap
+    nb = -(-rows // cap)
+    nb = -(-nb // world) * world
+    return -(-rows // nb)
 
 
 def rank_batches(shard, rows, batch, rank, world, assign):
@@ -569,7 +587,9 @@ def main():
     ap.add_argument("--shard", choices=["roundrobin", "weak"], default="roundrobin",
                     help="roundrobin: ONE table, batch b on rank b mod N (BASELINE configs[3], strong scaling); "
                          "weak: every rank scans its own table")
-    ap.add_argument("--batch-size", type=int, default=300_000)
+    ap.add_argument("--batch-size", type=int, default=0,
+                    help="0 = balanced: the largest size <= 300000 (the reference default) giving every rank the "
+                         "same batch count under round-robin (300000 at N = 1); weak scaling uses 300000")
     ap.add_argument("--labels", type=int, default=0)
     ap.add_argument("--output-count", type=int, default=1,
                     help="protocol variant: output indices k = 0..K-1 per row (1 = the reference)")
@@ -611,6 +631,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.batch_size <= 0:
+        args.batch_size = balanced_batch_size(args.rows, world) if args.shard == "roundrobin" else 300_000
     # The window width is the process default for every scanner and the
     # synthetic-table generator (read once by the library).
     os.environ["CUDASP_FB_BITS"] = str(args.fb_bits if args.fb_bits in (22, 26) else 22)

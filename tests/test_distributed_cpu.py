@@ -135,3 +135,31 @@ def test_rank_batches_cover_config4_table():
         assert sum(m for p in per for _, m in p) == rows
         loads = [len(p) for p in per]
         assert max(loads) - min(loads) <= 1
+
+
+def test_balanced_batch_size_equal_rank_shares():
+    """The bench's default batch_size: 300000 at N = 1 (the reference's
+    default); at N = 2/4/8 every rank gets the same number of batches, the
+    batches cover the table exactly, and rank row counts differ by less than
+    one batch (only the short last batch differs)."""
+    _paths()
+    import bench
+    from cudasp_amd import assign_gpu
+    rows = 32_700_000
+    assert bench.balanced_batch_size(rows, 1) == 300_000
+    assert bench.balanced_batch_size(rows, 8) == 291_965
+    for world in (1, 2, 3, 4, 8):
+        batch = bench.balanced_batch_size(rows, world)
+        assert batch <= 300_000
+        per = [bench.rank_batches("roundrobin", rows, batch, r, world, assign_gpu) for r in range(world)]
+        assert len({len(p) for p in per}) == 1
+        firsts = sorted(g0 for p in per for g0, _ in p)
+        assert firsts == list(range(0, rows, batch))
+        shares = [sum(m for _, m in p) for p in per]
+        assert sum(shares) == rows
+        assert max(shares) - min(shares) < batch
+    for rows in (1, 1000, 299_999, 300_001, 1_000_000):
+        for world in (1, 2, 8):
+            batch = bench.balanced_batch_size(rows, world)
+            assert 0 < batch <= 300_000
+            assert -(-rows // batch) <= -(-(-(-rows // 300_000)) // world) * world
