@@ -1,5 +1,5 @@
 # Multi-rank rehearsals of the multi-batch bench on one MI355X over gloo:
-# 4 ranks, round-robin config 4 (each rank its 27-28 batches in one
+# 4 ranks, round-robin config 4 (each rank its 28 batches, balanced batch size, in one
 # k_scan_multi launch per step, 4 processes sharing the GPU).
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O; cd $R
