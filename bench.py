@@ -252,8 +252,8 @@ def balanced_batch_size(rows, world, cap=300_000):
     300000-row batches 14/13 per rank, whose largest share sets the job time.
     batch_size is the SQL function's own parameter (`batch_size := INTEGER`,
     src/cudasp_extension.cu:626-635); BASELINE configs[3] does not fix it."""
-    if rows <= 0:
-        return cap
+    if rows <= 0 or world <= 1:
+        return cap  # N = 1: the reference's batches as configs[1]/[2] state them
     nb = -(-rows // cap)
     nb = -(-nb // world) * world
     return -(-rows // nb)

@@ -148,6 +148,9 @@ def test_balanced_batch_size_equal_rank_shares():
     rows = 32_700_000
     assert bench.balanced_batch_size(rows, 1) == 300_000
     assert bench.balanced_batch_size(rows, 8) == 291_965
+    # configs[1]/[2] state batch_size=300000: one GPU keeps it whatever the rows
+    for r in (1_000_000, 9_400_000, 100_000_000):
+        assert bench.balanced_batch_size(r, 1) == 300_000
     for world in (1, 2, 3, 4, 8):
         batch = bench.balanced_batch_size(rows, world)
         assert batch <= 300_000
