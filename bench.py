@@ -8,13 +8,14 @@ Contract (see DESIGN.md "Measurement"):
 
 Workload (BASELINE.json metric "tx/sec through cudasp_scan on 32M-row tweak
 table at 1/2/4/8 MI355X", configs[3]): ONE 32.7M-row synthetic table, cut into
-batches of at most the reference's default 300000 rows (at N = 1 exactly
-300000; at N > 1 the largest size whose batch count is a multiple of N, so
-every rank gets the same number of batches: balanced_batch_size); batch b is scanned by rank
-b mod N (the product's assignment, cudasp_assign_gpu; the reference
-round-robins its executor threads over GPUs, src/cudasp_extension.cu:523-529),
-so the total work is fixed as N grows (`--shard weak` gives every rank its own
-table instead).  Each rank's batches are resident in HBM, tweak limbs
+batches of the reference's default batch_size 300000 at every N (BASELINE.md
+section 3 row 4); batch b is scanned by rank b mod N (the product's
+assignment, cudasp_assign_gpu; the reference round-robins its executor
+threads over GPUs, src/cudasp_extension.cu:523-529), so the total work is
+fixed as N grows (`--shard weak` gives every rank its own table instead).  At
+N > 1 a secondary line re-cuts the same table into equal batch counts per
+rank (balanced_batch_size) and reports it as `value_balanced`, never as the
+headline.  Each rank's batches are resident in HBM, tweak limbs
 column-major per batch.  A step is one pass of the hot path over the rank's
 batches: by default (`--launch multi`) one cudasp_scan_device_batches call
 over all of them -- one persistent kernel (k_scan_multi) runs both stages
@@ -23,9 +24,12 @@ compaction) for every row, with per-batch flags and match lists; with
 `--launch batches` every batch goes through cudasp_scan_device, round-robin
 over `--streams` HIP streams (the reference's per-thread streams,
 src/cudasp_gpu.cu:505).  No collective in the data path: torch.distributed
-carries the bracketing barrier and the max of the elapsed time.  After the timed steps, rank 0 at N = 1 also reports the
-PCIe-inclusive end-to-end rate of the table-function host (`e2e`,
-tools/host_e2e) -- never the `value`.
+carries the bracketing barrier and the max of the elapsed time.  After the
+timed steps, rank 0 also reports the PCIe-inclusive end-to-end rate of the
+table-function host over all N GPUs (`e2e`: tools/host_e2e as a child
+process, the same table shape in host memory, fed by executor threads through
+the calls DuckDB makes; at N > 1 the other ranks wait at a CPU barrier) --
+never the `value`.
 
 Synthetic data: T_i = (s0 + g) G with s0 = SHA256("cudasp-synth-v1")
 mod n and g the global row index; 2 splitmix64 outputs per row (seed
@@ -407,37 +411,95 @@ def layout_probe(lib, tab, reps=5):
                      "mapping and no arithmetic: the layout's own HBM roofline, one launch over the rank table")
 
 
+def cgroup_cpu_quota():
+    """CPUs of this process's cgroup CPU quota (cgroup v2 cpu.max or v1
+    cfs_quota_us / cfs_period_us), or None when there is no quota."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            lines = f.read().splitlines()
+    except OSError:
+        lines = []
+    paths = []
+    for ln in lines:
+        parts = ln.split(":", 2)
+        if len(parts) == 3 and (parts[0] == "0" or "cpu" in parts[1].split(",")):
+            paths.append((parts[0] == "0", parts[2]))
+    for v2, rel in paths + [(True, "/"), (False, "/")]:
+        try:
+            if v2:
+                with open(os.path.join("/sys/fs/cgroup", rel.lstrip("/"), "cpu.max")) as f:
+                    q, p = f.read().split()[:2]
+                if q != "max":
+                    return float(q) / float(p), "cgroup v2 cpu.max"
+            else:
+                base = os.path.join("/sys/fs/cgroup/cpu", rel.lstrip("/"))
+                with open(os.path.join(base, "cpu.cfs_quota_us")) as f:
+                    q = int(f.read())
+                with open(os.path.join(base, "cpu.cfs_period_us")) as f:
+                    p = int(f.read())
+                if q > 0:
+                    return q / p, "cgroup v1 cfs quota"
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
 def host_cores():
-    """Host CPUs this process may use: the affinity mask, capped by
-    OMP_NUM_THREADS when the environment sets it (on the GPU pool the box's
-    CPU share is set there, while the mask shows the whole machine)."""
+    """Host CPUs this process may use: the affinity mask, capped by the
+    cgroup CPU quota when one is set; without a quota, by OMP_NUM_THREADS
+    when the environment sets it (the GPU pool states the box's CPU share
+    there while the mask shows the whole machine, and asks that worker pools
+    stay within it).  Returns (cores, visible, source)."""
     visible = len(os.sched_getaffinity(0))
-    cap = os.environ.get("OMP_NUM_THREADS")
-    use = min(visible, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else visible
-    return use, visible
+    quota, src = cgroup_cpu_quota()
+    if quota is not None and quota < visible:
+        return max(1, int(quota)), visible, src
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and 0 < int(omp) < visible:
+        return int(omp), visible, "OMP_NUM_THREADS (no cgroup CPU quota; affinity shows %d CPUs)" % visible
+    return visible, visible, "sched_getaffinity"
 
 
-def e2e_leg(args, mean_k):
+def e2e_leg(args, labels, world, fb_bits):
     """PCIe-inclusive end-to-end rate through the table-function host
-    (include/cudasp_host.h, the calls DuckDB's executor makes): tools/host_e2e
-    as a child process, the same global table shape in host memory, fed as
-    DuckDB-style 2048-row chunks by --e2e-threads executor threads; its first
-    query warms the process (scanner creation, table build), the second is
-    timed.  The child gets GPU_MAX_HW_QUEUES=16, what the DuckDB extension sets
-    at load when the environment leaves it unset
-    (duckdb_ext/cudasp_extension.cpp)."""
+    (include/cudasp_host.h, the calls DuckDB's executor makes) over all
+    `world` GPUs: tools/host_e2e as a fresh child process (this process only
+    waits for it), the same table shape in host memory -- rows, batch_size,
+    label keys (bench.label_keys, passed as a file), outputs per row (fixed k,
+    or 1..kmax from the same generators as the device legs) and planted base
+    and label matches -- fed as DuckDB-style 2048-row chunks by executor
+    threads.  Its first query warms the process (scanners, batch slots,
+    fixed-base tables), then `reps` queries are timed and the median is
+    reported; every query must emit exactly the planted rows.  The child runs
+    with the environment's GPU_MAX_HW_QUEUES (HIP's default 4 unless
+    --e2e-hw-queues sets one)."""
     import subprocess
+    import tempfile
     exe = os.path.join(ROOT, "tools", "host_e2e")
     if not os.path.exists(exe):
         return dict(error="tools/host_e2e not built (make -C duckdb-cudasp-extension_amd)")
-    k = max(1, int(round(mean_k)))
-    env = dict(os.environ, CUDASP_FB_BITS=str(args.fb_bits), GPU_MAX_HW_QUEUES=str(args.e2e_hw_queues))
-    cmd = [exe, str(args.rows), str(args.e2e_threads), str(args.batch_size), str(args.labels), str(k), "rows"]
+    threads = args.e2e_threads or 8 * world
+    reps = args.e2e_reps or (5 if args.rows <= 2_000_000 else 3 if args.rows <= 10_000_000 else 1)
+    env = dict(os.environ, CUDASP_FB_BITS=str(fb_bits))
+    if args.e2e_hw_queues:
+        env["GPU_MAX_HW_QUEUES"] = str(args.e2e_hw_queues)
+    lf = None
+    cmd = [exe, "--rows", str(args.rows), "--threads", str(threads), "--batch", str(args.batch_size),
+           "--labels", str(len(labels)), "--input", args.e2e_input, "--reps", str(reps)]
+    if labels:
+        lf = tempfile.NamedTemporaryFile(prefix="cudasp_labels_", suffix=".bin", delete=False)
+        lf.write(b"".join(labels))
+        lf.close()
+        cmd += ["--labels-file", lf.name]
+    cmd += ["--outputs-max", str(args.outputs_max)] if args.outputs_max else ["--outputs", str(args.outputs_per_row)]
     t0 = time.perf_counter()
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.e2e_timeout, env=env)
     except subprocess.TimeoutExpired:
         return dict(error="timed out after %d s" % args.e2e_timeout, cmd=" ".join(cmd[1:]))
+    finally:
+        if lf is not None:
+            os.unlink(lf.name)
     line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else ""
     try:
         res = json.loads(line)
@@ -445,10 +507,10 @@ def e2e_leg(args, mean_k):
         return dict(error="exit %d: %s" % (r.returncode, (r.stderr or r.stdout)[-400:]), cmd=" ".join(cmd[1:]))
     res["exit_code"] = r.returncode
     res["wall_s"] = round(time.perf_counter() - t0, 2)
-    res["args"] = " ".join(cmd[1:])
-    res["fixed_base_bits"] = args.fb_bits
-    if args.outputs_max:
-        res["note"] = "fixed %d outputs per row (host_e2e has no variable-length lists)" % k
+    res["args"] = " ".join(c if c != (lf.name if lf else None) else "<label keys>" for c in cmd[1:])
+    res["fixed_base_bits"] = fb_bits
+    if r.stderr.strip():
+        res["stderr_tail"] = r.stderr.strip()[-300:]
     return res
 
 
@@ -529,6 +591,23 @@ def cpu_baseline_optimized(smp, labels, threads):
                 sample_matches=int(flags.sum()))
 
 
+def cpu_port_sweep(smp, labels, cores, rows):
+    """port-optimized at a few thread counts (cores/4, cores/2, cores; never
+    more threads than the allotted cores) over the first `rows` rows of the
+    sample: how the CPU bar scales with the host share."""
+    sub = dict(smp)
+    n = min(rows, smp["rows"])
+    used = int(smp["offs"][n - 1]) + int(smp["lens"][n - 1]) if n else 0
+    sub.update(tweaks=smp["tweaks"][:n], outs=smp["outs"][:used], offs=smp["offs"][:n], lens=smp["lens"][:n],
+               gpu_flags=smp["gpu_flags"][:n], rows=n, batches=1)
+    out = []
+    for t in sorted({max(1, cores // 4), max(1, cores // 2), cores}):
+        r = cpu_baseline_optimized(sub, labels, t)
+        out.append(dict(threads=t, value=r.get("value"), seconds=r.get("seconds"),
+                        flags_match_gpu=r.get("flags_match_gpu"), error=r.get("error")))
+    return dict(rows=n, unit="tx/s", kind="port-optimized", points=out)
+
+
 def sq_profile_path(args):
     """The PMC instruction-count summary matching this run's shape (launch
     mode, labels, outputs per row, fixed-base width, variants):
@@ -577,6 +656,30 @@ def alu_roofline(path, value_per_gpu, multi=False):
                      "integer ops issue at about half of it on gfx950" % sq.get("shape", "see source"))
 
 
+def timed_steps(step, steps, warmup, device, barrier, counter=None):
+    """W untimed then K timed steps, each bracketed by barrier + synchronize;
+    returns (per-step seconds, found per step)."""
+    found = []
+    for _ in range(warmup):
+        step()
+        torch.cuda.synchronize(device)
+        if counter is not None:
+            found.append(counter())
+    times = []
+    events = []
+    for _ in range(steps):
+        barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        step(events)
+        torch.cuda.synchronize(device)
+        barrier()
+        times.append(time.perf_counter() - t0)
+        if counter is not None:
+            found.append(counter())
+    return times, events, found
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -587,9 +690,11 @@ def main():
     ap.add_argument("--shard", choices=["roundrobin", "weak"], default="roundrobin",
                     help="roundrobin: ONE table, batch b on rank b mod N (BASELINE configs[3], strong scaling); "
                          "weak: every rank scans its own table")
-    ap.add_argument("--batch-size", type=int, default=0,
-                    help="0 = balanced: the largest size <= 300000 (the reference default) giving every rank the "
-                         "same batch count under round-robin (300000 at N = 1); weak scaling uses 300000")
+    ap.add_argument("--batch-size", type=int, default=300_000,
+                    help="rows per batch (the reference's default 300000, BASELINE.md section 3, at every N); "
+                         "0 = balanced: the largest size <= 300000 giving every rank the same batch count")
+    ap.add_argument("--no-balanced", action="store_true",
+                    help="at N > 1, skip the secondary value_balanced line (equal batch counts per rank)")
     ap.add_argument("--labels", type=int, default=0)
     ap.add_argument("--output-count", type=int, default=1,
                     help="protocol variant: output indices k = 0..K-1 per row (1 = the reference)")
@@ -597,9 +702,9 @@ def main():
     ap.add_argument("--outputs-per-row", type=int, default=2)
     ap.add_argument("--outputs-max", type=int, default=0,
                     help="variable outputs per row, uniform in [1, N] (15 -> mean 8, config 5); 0 = fixed")
-    ap.add_argument("--fb-bits", type=int, default=26, choices=[7, 22, 26],
-                    help="fixed-base window width (26: 21.5 GB HBM table, 22: 1.5 GiB, 7: 151.5 KB staged in LDS; "
-                         "same results)")
+    ap.add_argument("--fb-bits", type=int, default=0, choices=[0, 7, 22, 26],
+                    help="fixed-base window width; 0 = the product default (cudasp_default_fixed_base_bits: 26 "
+                         "on MI355X, 21.5 GB HBM table; 22: 1.5 GiB; 7: 151.5 KB staged in LDS; same results)")
     ap.add_argument("--launch", choices=["multi", "batches"], default="multi",
                     help="multi: the rank's batches in one cudasp_scan_device_batches call (one persistent kernel "
                          "for both stages); batches: cudasp_scan_device per batch, round-robin over --streams")
@@ -611,12 +716,17 @@ def main():
                     help="full batches timed alone on one stream after the timed steps (roofline kernel_ms)")
     ap.add_argument("--cpu-rows", type=int, default=1200000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this process may use")
+    ap.add_argument("--cpu-sweep-rows", type=int, default=200000,
+                    help="rows of the port-optimized thread sweep (0 = no sweep)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layout-probe", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--e2e-threads", type=int, default=8)
-    ap.add_argument("--e2e-hw-queues", type=int, default=16)
-    ap.add_argument("--e2e-timeout", type=int, default=420)
+    ap.add_argument("--e2e-threads", type=int, default=0, help="executor threads of the e2e leg; 0 = 8 per GPU")
+    ap.add_argument("--e2e-reps", type=int, default=0, help="timed e2e queries (median); 0 = by table size")
+    ap.add_argument("--e2e-input", choices=["rows", "columns"], default="rows")
+    ap.add_argument("--e2e-hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for the e2e child; 0 = the environment's (HIP default 4)")
+    ap.add_argument("--e2e-timeout", type=int, default=600)
     ap.add_argument("--pmc-summary", default="",
                     help="HBM traffic summary (default: profiles/r02_pmc_hbm_multi.json with --launch multi, "
                          "profiles/r02_pmc_hbm_k_shared_secret.json with --launch batches)")
@@ -633,18 +743,27 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.batch_size <= 0:
         args.batch_size = balanced_batch_size(args.rows, world) if args.shard == "roundrobin" else 300_000
-    # The window width is the process default for every scanner and the
-    # synthetic-table generator (read once by the library).
-    os.environ["CUDASP_FB_BITS"] = str(args.fb_bits if args.fb_bits in (22, 26) else 22)
+    if args.fb_bits in (22, 26):
+        # the process default for every scanner and the synthetic-table
+        # generator (read once by the library); 0 keeps the product default
+        os.environ["CUDASP_FB_BITS"] = str(args.fb_bits)
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
+    cpu_group = None
     if world > 1:
+        import datetime
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(args.dist_backend)
+        # host-side waits (the e2e leg) on a CPU group: no collective kernel
+        # spins on the other ranks' GPUs meanwhile
+        cpu_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(minutes=30))
     lib = _native.load()
     from cudasp_amd import assign_gpu
+    product_fb_bits = int(lib.cudasp_default_fixed_base_bits())
+    if args.fb_bits == 0:
+        args.fb_bits = product_fb_bits
 
     labels = label_keys(args.labels)
     gen_stream = torch.cuda.Stream(device)
@@ -674,23 +793,8 @@ def main():
         else:
             run_step(tab, scanners, streams, events=events, tail_rows=(args.tail_rows_a, args.tail_rows_b))
 
-    step_found = []
-    for _ in range(args.warmup):
-        step()
-        torch.cuda.synchronize(device)
-        step_found.append(int(tab.match_count.sum().item()))
-
-    times = []
-    events = []
-    for _ in range(args.steps):
-        barrier()
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        step(events)
-        torch.cuda.synchronize(device)
-        barrier()
-        times.append(time.perf_counter() - t0)
-        step_found.append(int(tab.match_count.sum().item()))
+    times, events, step_found = timed_steps(step, args.steps, args.warmup, device, barrier,
+                                            lambda: int(tab.match_count.sum().item()))
     total_s = float(np.sum(times))
     found = int(tab.match_count.sum().item())
     flagged = int(tab.flags.sum().item())
@@ -760,7 +864,8 @@ def main():
                                  if args.shard == "roundrobin" else "every rank scans its own table (weak)"),
                     rows=args.rows, shard=args.shard, batch_size=args.batch_size, labels=args.labels,
                     output_count=args.output_count, label_negation=args.label_negation,
-                    outputs_per_row=round(mean_k, 3), fixed_base_bits=args.fb_bits, launch=args.launch,
+                    outputs_per_row=round(mean_k, 3), fixed_base_bits=args.fb_bits,
+                    fixed_base_bits_product_default=product_fb_bits, launch=args.launch,
                     streams=1 if multi else args.streams, batches_rank0=tab.nb, parallelism="dp%d" % world),
         roofline=dict(bound="hbm", achieved=achieved_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                       frac=achieved_gbs / HBM_PEAK_GBS, traffic=traffic,
@@ -787,22 +892,59 @@ def main():
                 result["layout_probe"]["traffic_ratio"] = probe_traffic / (result["layout_probe"]["algorithmic_bytes"]
                                                                            / result["layout_probe"]["rows"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        use, visible = host_cores()
+        use, visible, source = host_cores()
         threads = args.cpu_threads or use
         smp = cpu_sample(tab, args.cpu_rows)
+        result["host_cores_allotted"] = dict(cores=use, source=source, visible=visible,
+                                             omp_num_threads=os.environ.get("OMP_NUM_THREADS"))
         result["cpu_baseline"] = cpu_baseline(smp, labels, threads, args.output_count, args.label_negation)
         result["cpu_baseline"]["host_cpus_visible"] = visible
         if args.output_count == 1 and not args.label_negation:
             result["cpu_baseline_optimized"] = cpu_baseline_optimized(smp, labels, threads)
+            if args.cpu_sweep_rows:
+                result["cpu_baseline_optimized_sweep"] = cpu_port_sweep(smp, labels, use, args.cpu_sweep_rows)
         del smp
     for s in scanners:
         s.close()
-    if rank == 0 and world == 1 and not args.no_e2e and args.output_count == 1 and not args.label_negation:
-        # after the device-resident legs, with this process's GPU work drained
+
+    # Secondary line at N > 1: the same table in equal batch counts per rank.
+    if world > 1 and args.shard == "roundrobin" and not args.no_balanced:
+        bb = balanced_batch_size(args.rows, world)
+        del descs, tab
+        torch.cuda.empty_cache()
+        btab = Table(lib, device, rank_batches("roundrobin", args.rows, bb, rank, world, assign_gpu), bb,
+                     args.outputs_per_row, labels, dev_stream=gen_stream, kmax=args.outputs_max)
+        bsc = Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=bb, device=device)
+        bsc.set_fixed_base_bits(args.fb_bits)
+        bdescs = multi_descs(btab)
+        btimes, _, _ = timed_steps(lambda ev=None: run_step_multi(btab, bsc, streams[0], bdescs, ev), args.steps,
+                                   args.warmup, device, barrier)
+        bfound = int(btab.match_count.sum().item())
+        bt, bfound, _, bexp = aggregate(world, args.dist_backend, float(np.sum(btimes)), bfound, 0, btab.expected)
+        result["value_balanced"] = args.rows * args.steps / bt
+        result["balanced"] = dict(batch_size=bb, batches=-(-args.rows // bb), ms_per_step=bt / args.steps * 1e3,
+                                  found=bfound, expected_planted=bexp,
+                                  note="secondary: the table re-cut so every rank gets the same batch count; the "
+                                       "headline `value` keeps batch_size %d at every N" % args.batch_size)
+        bsc.close()
+        del bdescs, btab
+        torch.cuda.empty_cache()
+    else:
+        del descs, tab
+        torch.cuda.empty_cache()
+
+    if not args.no_e2e and args.output_count == 1 and not args.label_negation:
+        # After the device-resident legs: rank 0 starts the end-to-end child
+        # over all N GPUs while the other ranks wait at a CPU barrier.
         torch.cuda.synchronize(device)
-        e2e = e2e_leg(args, mean_k)
-        result["e2e"] = e2e
-        result["e2e_tx_s"] = e2e.get("tx_per_s")
+        if world > 1:
+            dist.barrier(group=cpu_group)
+        if rank == 0:
+            e2e = e2e_leg(args, labels, world, args.fb_bits)
+            result["e2e"] = e2e
+            result["e2e_tx_s"] = e2e.get("tx_per_s")
+        if world > 1:
+            dist.barrier(group=cpu_group)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -1,35 +1,55 @@
 // cudasp_scan table-function host, DuckDB-independent (include/cudasp_host.h).
 //
 // Same state machine as the reference host (src/cudasp_extension.cu:87-659):
-// bind validation with the same messages, per-thread accumulation with the
-// same NULL rules, the `>= batch_size` trigger, round-robin GPU per thread,
-// mutex-guarded global match list, last-thread-emits in 2048-row chunks.
-// What differs, by design:
-//   * rows are accumulated into flat columns (one byte arena for txids, one
-//     n x 64 tweak array, a CSR for outputs) instead of two heap strings per
-//     row (:202-204), and handed to the kernels in one copy, with no
-//     column-major repack on the host (:249-341) and no u64[n][64] staging
-//     (src/cudasp_gpu.cu:705-761);
-//   * each thread keeps one scanner (keys bound once, device buffers reused)
-//     instead of allocating and freeing per batch (src/cudasp_gpu.cu:487-666);
-//   * rows are accumulated straight into pinned host buffers and batches run
-//     asynchronously, double-buffered: while the GPU scans batch b (H2D,
-//     transpose, both kernels, D2H of the flags, all on the thread's stream),
-//     the DuckDB thread accumulates batch b+1; the reference blocks the thread
-//     for the whole GPU round trip (README.md:140 "serial table scan overhead");
-//   * a failed batch is reported (cudasp_tf_function/final return an error)
-//     instead of being dropped silently (:325, :378);
-//   * a tweak_key BLOB that is not 64 bytes is an error instead of an
-//     out-of-bounds read (:333, ConvertTweakKeyToU32 always reads 64 bytes).
+// bind validation with the same messages, per-thread chunks with the same
+// NULL rules, round-robin GPU per thread, mutex-guarded global match list,
+// last-thread-emits in 2048-row chunks.  What differs, by design:
+//
+//   * Rows do not wait in per-thread batches.  Each GPU has one *device feed*
+//     per query: a ring of pinned batch slots that every executor thread fills
+//     at once (a thread reserves room for its chunk under the feed's lock and
+//     copies outside it), and a few streams, each with its own scanner, that
+//     run the closed slots.  A slot closes at >= batch_size rows -- the
+//     reference's trigger (:416-418), applied to the device's rows instead of
+//     one thread's -- and the last thread still copying into it launches it:
+//     H2D of the row blobs and the outputs CSR, the on-device transpose, both
+//     stages fused in one k_scan_multi launch, D2H of the flags.  So
+//       - the first launch starts after batch_size rows of the whole table,
+//         not of one thread (the reference waits for one thread's batch);
+//       - a table smaller than threads x batch_size still runs as full
+//         batches while the threads are reading, instead of every thread's
+//         partial batch in in_out_function_final (1M rows over 8 threads:
+//         the reference runs 8 batches of 125k rows at the end);
+//       - the end of the query drains one partial slot per device, not one
+//         per thread;
+//       - executor threads and GPUs are independent: a thread's chunks go to
+//         the devices round-robin (chunk c of thread t to logical GPU
+//         (t + c) mod num_gpus), so any thread count feeds any GPU count; a
+//         thread's "assigned GPU" (:523-529) is where its chunks start;
+//       - the streams in flight per device are the feed's (at most 4: the
+//         HIP runtime's default GPU_MAX_HW_QUEUES), not one per thread.
+//     Batch composition therefore differs from the reference; the emitted
+//     rows (a multiset -- the reference's order is unspecified) do not.
+//   * Flat columns instead of two heap strings per row (:202-204), no host
+//     transpose (:249-341) and no u64[n][64] staging (src/cudasp_gpu.cu:705-761).
+//   * Scanners, streams and slots are created once and kept in a process-wide
+//     pool across queries (src/cudasp_gpu.cu:487-666 allocates per batch).
+//   * A failed batch is reported (cudasp_tf_function/final return an error)
+//     instead of being dropped silently (:325, :378); a tweak_key BLOB that is
+//     not 64 bytes is an error instead of an out-of-bounds read (:59-75).
 #include "../../../include/cudasp_host.h"
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -41,8 +61,11 @@ namespace {
 constexpr uint64_t TWEAK_KEY_SIZE = 64;  // CudaspScanBindData::TWEAK_KEY_SIZE
 constexpr uint64_t SCALAR_SIZE = 32;     // CudaspScanBindData::SCALAR_SIZE
 constexpr uint32_t XONLY_SIZE = 32;      // full_x outputs: x-only keys
-// int64 words per output in the host/device outputs buffers.
-inline size_t out_words(const cudasp_tf_bind_data& b);
+constexpr int FEED_MAX_STREAMS = 4;
+constexpr int FEED_MAX_SLOTS = FEED_MAX_STREAMS + 2;
+// Rows resident on the GPU at once in k_scan_multi launches of 4 rows per
+// thread: 256 CUs x 4 SIMDs x 3 waves x 64 lanes x 4 rows.
+constexpr uint64_t GPU_FILL_ROWS = 786432;
 
 void write_err(char* err, size_t cap, const char* fmt, ...) {
   if (!err || cap == 0) return;
@@ -52,9 +75,14 @@ void write_err(char* err, size_t cap, const char* fmt, ...) {
   va_end(ap);
 }
 
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 }  // namespace
 
 extern "C" void cudasp_internal_set_error(const char* msg);
+extern "C" void* cudasp_internal_scanner_stream(cudasp_scanner* s);
 
 struct cudasp_tf_bind_data {
   uint64_t batch_size = CUDASP_TF_DEFAULT_BATCH;
@@ -66,68 +94,8 @@ struct cudasp_tf_bind_data {
 };
 
 namespace {
+
 inline size_t out_words(const cudasp_tf_bind_data& b) { return b.opt.full_x ? XONLY_SIZE / 8 : 1; }
-}  // namespace
-
-struct cudasp_tf_global {
-  std::atomic<uint64_t> currently_adding{0};
-  std::mutex finalize_lock;
-  std::mutex output_lock;
-  std::vector<std::string> output_txids;
-  std::vector<int32_t> output_heights;
-  std::vector<std::string> output_tweak_keys;
-  size_t output_position = 0;
-  std::atomic<bool> output_thread_claimed{false};
-  int num_gpus = 0;
-  std::atomic<int> next_gpu_assignment{0};
-  // logical GPU -> HIP device; the identity unless CUDASP_TF_DEVICE_MAP is set
-  std::vector<int> device_map;
-};
-
-// One accumulation/launch buffer set of a thread (double-buffered).
-struct HostSlot {
-  // row data for the kernels, pinned for asynchronous H2D
-  uint8_t* h_tweaks = nullptr;  // cap_rows x 64
-  uint32_t* h_offs = nullptr;
-  uint32_t* h_lens = nullptr;
-  uint8_t* h_flags = nullptr;
-  int64_t* h_outputs = nullptr;
-  size_t outputs_cap = 0;
-  size_t n_outputs = 0;
-  // row data for the emit (pageable)
-  std::vector<uint8_t> txid_bytes;
-  std::vector<uint64_t> txid_offset;
-  std::vector<uint32_t> txid_size;
-  std::vector<int32_t> heights;
-  uint32_t rows = 0;
-  // device side
-  uint8_t* d_rows = nullptr;
-  uint32_t* d_tx = nullptr;
-  uint32_t* d_ty = nullptr;
-  uint32_t* d_offs = nullptr;
-  uint32_t* d_lens = nullptr;
-  uint8_t* d_flags = nullptr;
-  int64_t* d_outputs = nullptr;
-  size_t d_outputs_cap = 0;
-  hipEvent_t done = nullptr;
-  bool in_flight = false;
-  uint32_t launched_rows = 0;
-};
-
-struct cudasp_tf_local {
-  bool finalized = false;
-  bool is_output_thread = false;
-  int assigned_gpu = -1;  // logical GPU (round-robin over num_gpus)
-  int device = -1;        // the HIP device it runs on
-  uint32_t cap_rows = 0;
-  HostSlot slots[2];
-  int cur = 0;
-  cudasp_scanner* scanner = nullptr;
-  hipStream_t stream = nullptr;
-  uint32_t rows() const { return slots[cur].rows; }
-};
-
-namespace {
 
 // Errors go to the library-wide thread-local message of cudasp_last_error().
 int host_fail(int code, const char* fmt, ...) {
@@ -140,7 +108,8 @@ int host_fail(int code, const char* fmt, ...) {
   return code;
 }
 
-inline bool valid(const uint8_t* v, uint32_t i) { return v == nullptr || v[i] != 0; }
+inline bool valid(const uint8_t* v, uint64_t i) { return v == nullptr || v[i] != 0; }
+inline bool bit(const uint8_t* bm, uint64_t i) { return bm == nullptr || ((bm[i >> 3] >> (i & 7)) & 1u); }
 
 #define HOST_HIP(expr)                                                                          \
   do {                                                                                          \
@@ -159,131 +128,125 @@ struct DeviceSet {
   }
 };
 
-// need: int64 words; ow: words per output already held (n_outputs * ow used).
-int ensure_outputs_cap(HostSlot& s, size_t need, size_t ow = 1) {
-  if (need <= s.outputs_cap) return CUDASP_OK;
-  size_t cap = s.outputs_cap ? s.outputs_cap : 4096;
-  while (cap < need) cap *= 2;
-  int64_t* p = nullptr;
-  HOST_HIP(hipHostMalloc((void**)&p, cap * sizeof(int64_t), hipHostMallocDefault));
-  if (s.n_outputs) memcpy(p, s.h_outputs, s.n_outputs * ow * sizeof(int64_t));
-  if (s.h_outputs) (void)hipHostFree(s.h_outputs);
-  s.h_outputs = p;
-  s.outputs_cap = cap;
-  return CUDASP_OK;
+// Streams (= scanners) of a device feed: enough 4-row-per-thread launches of
+// batch_size rows in flight to cover the GPU's wave slots, 2 to 4
+// (CUDASP_TF_STREAMS = 1..4 overrides).
+int feed_streams_for(uint64_t batch_size) {
+  if (const char* e = getenv("CUDASP_TF_STREAMS")) {
+    const int v = atoi(e);
+    if (v >= 1 && v <= FEED_MAX_STREAMS) return v;
+  }
+  // launches that fill the GPU, plus one to cover a slot being refilled
+  const uint64_t k = (GPU_FILL_ROWS + batch_size - 1) / (batch_size ? batch_size : 1) + 1;
+  return k < 2 ? 2 : (k > (uint64_t)FEED_MAX_STREAMS ? FEED_MAX_STREAMS : (int)k);
 }
 
-// GPU state of an executor thread (scanner, stream, pinned host and device
-// buffers of both slots).  It is created on the thread's first row and, when
-// the thread's local state is freed, parked in a process-wide pool instead of
-// being released: the next query's threads take it back and only rebind the
-// keys (cudasp_scanner_set_keys), so a query pays no pinned-memory or device
-// allocations once the pool is warm.
-struct GpuCtx {
+enum SlotState { SLOT_FREE, SLOT_FILLING, SLOT_CLOSED, SLOT_BUSY, SLOT_LAUNCHED };
+
+// One batch slot of a device feed.
+struct FeedSlot {
+  // pinned host buffers (H2D / D2H)
+  uint8_t* h_tweaks = nullptr;  // cap_rows x 64, the row blobs as DuckDB holds them
+  uint32_t* h_offs = nullptr;   // cap_rows, in outputs
+  uint32_t* h_lens = nullptr;
+  uint8_t* h_flags = nullptr;
+  int64_t* h_outputs = nullptr;  // outputs_cap int64 words
+  size_t outputs_cap = 0;
+  // emit data of the rows (pageable; only read for matches)
+  std::vector<uint8_t> txid_bytes;  // size() is the capacity
+  std::vector<uint64_t> txid_off;   // cap_rows
+  std::vector<uint32_t> txid_size;  // cap_rows
+  std::vector<int32_t> heights;     // cap_rows
+  // device buffers
+  uint8_t* d_rows = nullptr;
+  uint32_t* d_tx = nullptr;
+  uint32_t* d_ty = nullptr;
+  uint32_t* d_offs = nullptr;
+  uint32_t* d_lens = nullptr;
+  uint8_t* d_flags = nullptr;
+  int64_t* d_outputs = nullptr;
+  size_t d_outputs_cap = 0;  // words
+  hipEvent_t done = nullptr;
+  bool allocated = false;
+  // fill state, guarded by Feed::mu
+  SlotState state = SLOT_FREE;
+  uint32_t rows = 0;     // rows reserved
+  size_t words = 0;      // output words reserved
+  size_t txid_used = 0;  // txid bytes reserved
+  int writers = 0;       // reservations still copying
+  int stream = 0;        // stream (scanner) of its launch
+};
+
+// The GPU resources of a device feed, kept in a process-wide pool between
+// queries (a later query only rebinds the scanners' keys).
+struct FeedRes {
   int device = -1;
   uint32_t cap_rows = 0;
-  cudasp_scanner* scanner = nullptr;
-  hipStream_t stream = nullptr;
-  HostSlot slots[2];
+  int nstreams = 0;
+  cudasp_scanner* scanners[FEED_MAX_STREAMS] = {};
+  FeedSlot slots[FEED_MAX_SLOTS];
+  int nslots() const { return nstreams + 2; }
 };
+
+void free_slot(FeedSlot& s) {
+  void* host[] = {s.h_tweaks, s.h_offs, s.h_lens, s.h_flags, s.h_outputs};
+  for (void* p : host)
+    if (p) (void)hipHostFree(p);
+  void* dev[] = {s.d_rows, s.d_tx, s.d_ty, s.d_offs, s.d_lens, s.d_flags, s.d_outputs};
+  for (void* p : dev)
+    if (p) (void)hipFree(p);
+  if (s.done) (void)hipEventDestroy(s.done);
+  s = FeedSlot();
+}
+
+void release_res(FeedRes* r) {
+  if (!r) return;
+  {
+    DeviceSet dg(r->device);
+    for (int k = 0; k < r->nstreams; k++)
+      if (r->scanners[k]) (void)cudasp_scanner_sync(r->scanners[k]);
+    for (FeedSlot& s : r->slots) free_slot(s);
+  }
+  for (int k = 0; k < r->nstreams; k++)
+    if (r->scanners[k]) cudasp_scanner_destroy(r->scanners[k]);
+  delete r;
+}
 
 constexpr size_t POOL_MAX = 64;
 std::mutex g_pool_mu;
-std::vector<GpuCtx*> g_pool;
+std::vector<FeedRes*> g_pool;
 
-void reset_slot_state(HostSlot& s) {
-  s.txid_bytes.clear();
-  s.txid_offset.clear();
-  s.txid_size.clear();
-  s.heights.clear();
-  s.rows = 0;
-  s.n_outputs = 0;
-  s.in_flight = false;
-  s.launched_rows = 0;
-}
-
-void release_ctx(GpuCtx* c) {
-  DeviceSet dg(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (HostSlot& s : c->slots) {
-    void* host[] = {s.h_tweaks, s.h_offs, s.h_lens, s.h_flags, s.h_outputs};
-    for (void* p : host)
-      if (p) (void)hipHostFree(p);
-    void* dev[] = {s.d_rows, s.d_tx, s.d_ty, s.d_offs, s.d_lens, s.d_flags, s.d_outputs};
-    for (void* p : dev)
-      if (p) (void)hipFree(p);
-    if (s.done) (void)hipEventDestroy(s.done);
-  }
-  if (c->stream) (void)hipStreamDestroy(c->stream);
-  if (c->scanner) cudasp_scanner_destroy(c->scanner);
-  delete c;
-}
-
-// A pooled context for (device, at least cap_rows), or nullptr.
-GpuCtx* pool_take(int device, uint32_t cap_rows) {
+FeedRes* pool_take(int device, uint32_t cap_rows, int nstreams) {
   std::lock_guard<std::mutex> lock(g_pool_mu);
   for (size_t i = 0; i < g_pool.size(); i++) {
-    GpuCtx* c = g_pool[i];
-    if (c->device == device && c->cap_rows >= cap_rows) {
+    FeedRes* r = g_pool[i];
+    if (r->device == device && r->cap_rows == cap_rows && r->nstreams == nstreams) {
       g_pool[i] = g_pool.back();
       g_pool.pop_back();
-      return c;
+      return r;
     }
   }
   return nullptr;
 }
 
-void pool_put(GpuCtx* c) {
+void pool_put(FeedRes* r) {
   {
     std::lock_guard<std::mutex> lock(g_pool_mu);
     if (g_pool.size() < POOL_MAX) {
-      g_pool.push_back(c);
+      g_pool.push_back(r);
       return;
     }
   }
-  release_ctx(c);
+  release_res(r);
 }
 
-void ctx_to_local(GpuCtx* c, cudasp_tf_local& l) {
-  l.cap_rows = c->cap_rows;
-  l.scanner = c->scanner;
-  l.stream = c->stream;
-  for (int i = 0; i < 2; i++) {
-    l.slots[i] = std::move(c->slots[i]);
-    reset_slot_state(l.slots[i]);
-  }
-  l.cur = 0;
-  c->scanner = nullptr;
-  c->stream = nullptr;
-  delete c;
-}
-
-int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
-  if (l.scanner) return CUDASP_OK;
-  DeviceSet dg(l.device);
-  const uint32_t cap_rows = (uint32_t)(b.batch_size + CUDASP_TF_VECTOR_SIZE);
-  const auto* scan = (const uint8_t*)b.scan_private_key_data.data();
-  const auto* spend = (const uint8_t*)b.spend_public_key_data.data();
-  const auto* labels = (const uint8_t*)b.label_keys_flat.data();
-  const auto nlabels = (uint32_t)b.label_keys_data.size();
-  if (GpuCtx* c = pool_take(l.device, cap_rows)) {
-    int rc = cudasp_scanner_set_keys(c->scanner, scan, spend, labels, nlabels);
-    if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(c->scanner, &b.opt);
-    if (rc != CUDASP_OK) {
-      pool_put(c);
-      return host_fail(rc, "Failed to bind scanner on GPU %d: %s", l.assigned_gpu, cudasp_last_error());
-    }
-    ctx_to_local(c, l);
-    return CUDASP_OK;
-  }
-  l.cap_rows = cap_rows;
-  int rc = cudasp_scanner_create(l.device, scan, spend, labels, nlabels, l.cap_rows, &l.scanner);
-  if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(l.scanner, &b.opt);
-  if (rc != CUDASP_OK)
-    return host_fail(rc, "Failed to create scanner on GPU %d: %s", l.assigned_gpu, cudasp_last_error());
-  HOST_HIP(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
-  for (HostSlot& s : l.slots) {
-    size_t n = l.cap_rows;
+// Pinned/device buffers of a slot for cap_rows rows, at least `words` output
+// words and `txid` txid bytes.  Called with the slot owned by the caller
+// (state BUSY): no reservation, copy or launch touches it.
+int prepare_slot(FeedSlot& s, int device, uint32_t cap_rows, size_t words, size_t txid) {
+  DeviceSet dg(device);
+  if (!s.allocated) {
+    const size_t n = cap_rows;
     HOST_HIP(hipHostMalloc((void**)&s.h_tweaks, n * 64, hipHostMallocDefault));
     HOST_HIP(hipHostMalloc((void**)&s.h_offs, n * 4, hipHostMallocDefault));
     HOST_HIP(hipHostMalloc((void**)&s.h_lens, n * 4, hipHostMallocDefault));
@@ -295,95 +258,450 @@ int ensure_local_gpu(const cudasp_tf_bind_data& b, cudasp_tf_local& l) {
     HOST_HIP(hipMalloc((void**)&s.d_lens, n * 4));
     HOST_HIP(hipMalloc((void**)&s.d_flags, n));
     HOST_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
-    rc = ensure_outputs_cap(s, (size_t)n * 2);
-    if (rc != CUDASP_OK) return rc;
+    s.txid_off.resize(n);
+    s.txid_size.resize(n);
+    s.heights.resize(n);
+    s.allocated = true;
   }
+  if (words > s.outputs_cap) {
+    size_t cap = s.outputs_cap ? s.outputs_cap : 4096;
+    while (cap < words) cap *= 2;
+    if (s.h_outputs) (void)hipHostFree(s.h_outputs);
+    s.h_outputs = nullptr;
+    s.outputs_cap = 0;
+    HOST_HIP(hipHostMalloc((void**)&s.h_outputs, cap * sizeof(int64_t), hipHostMallocDefault));
+    s.outputs_cap = cap;
+  }
+  if (txid > s.txid_bytes.size()) s.txid_bytes.resize(txid);
   return CUDASP_OK;
 }
 
-// Park the thread's GPU state in the pool (after its work has drained).
-void free_local_gpu(cudasp_tf_local& l) {
-  if (!l.scanner && !l.stream) return;
-  GpuCtx* c = new GpuCtx();
-  c->device = l.device;
-  c->cap_rows = l.cap_rows;
-  c->scanner = l.scanner;
-  c->stream = l.stream;
-  for (int i = 0; i < 2; i++) {
-    c->slots[i] = std::move(l.slots[i]);
-    l.slots[i] = HostSlot();
+}  // namespace
+
+// One device feed of a query (see the header comment).
+struct Feed {
+  FeedRes* res = nullptr;
+  cudasp_tf_global* g = nullptr;
+  uint64_t batch_size = 0;
+  size_t ow = 1;  // int64 words per output
+  std::mutex mu;
+  std::condition_variable cv;
+  int open = 0;             // the slot being filled
+  uint32_t launch_seq = 0;  // round-robin over the streams
+  // capacity a slot opens with, per row (grown when slots close on output or
+  // txid space before batch_size rows: long output lists, long txids)
+  double words_per_row = 2.0;
+  double txid_per_row = 32.0;
+  int error = CUDASP_OK;
+  std::string error_msg;
+  std::mutex stream_mu[FEED_MAX_STREAMS];  // a scanner's host state is not re-entrant
+  // statistics (under mu)
+  uint64_t launches = 0, rows = 0;
+  double harvest_wait_s = 0;
+};
+
+struct cudasp_tf_global {
+  std::atomic<uint64_t> currently_adding{0};
+  std::mutex finalize_lock;
+  std::mutex output_lock;
+  std::vector<std::string> output_txids;
+  std::vector<int32_t> output_heights;
+  std::vector<std::string> output_tweak_keys;
+  size_t output_position = 0;
+  std::atomic<bool> output_thread_claimed{false};
+  int num_gpus = 0;
+  std::atomic<int> next_gpu_assignment{0};
+  // logical GPU -> HIP device; the identity unless CUDASP_TF_DEVICE_MAP is set
+  std::vector<int> device_map;
+  // device feeds, one per logical GPU, created on its first chunk
+  const cudasp_tf_bind_data* bind = nullptr;
+  int feed_streams = 0;
+  // feeds[lg] is written once, under feed_create_mu[lg]; threads look a feed
+  // up through feed_ptr[lg] (published after the feed is complete)
+  std::vector<std::unique_ptr<Feed>> feeds;
+  std::unique_ptr<std::atomic<Feed*>[]> feed_ptr;
+  std::unique_ptr<std::mutex[]> feed_create_mu;
+  int hw_queues = 0;  // GPU_MAX_HW_QUEUES at init (HIP's default 4 when unset)
+  int max_streams_per_device = 0;
+};
+
+struct cudasp_tf_local {
+  bool finalized = false;
+  bool is_output_thread = false;
+  int assigned_gpu = -1;  // logical GPU of the thread's first chunk (round-robin over num_gpus)
+  int device = -1;        // the HIP device it maps to
+  uint64_t chunks = 0;    // chunks fed so far (chunk c goes to logical GPU assigned_gpu + c)
+};
+
+namespace {
+
+int feed_fail(Feed& f, int rc) {
+  // first error of the feed wins; later callers report it too
+  if (f.error == CUDASP_OK) {
+    f.error = rc;
+    f.error_msg = cudasp_last_error();
   }
-  l.scanner = nullptr;
-  l.stream = nullptr;
-  {
-    DeviceSet dg(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-  }
-  if (!c->scanner || !c->stream) {
-    release_ctx(c);
-    return;
-  }
-  pool_put(c);
+  return rc;
 }
 
-// AccumulateInput (src/cudasp_extension.cu:154-224), into the current slot.
-int accumulate(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const cudasp_tf_chunk& c) {
-  int rc = ensure_local_gpu(b, l);
-  if (rc != CUDASP_OK) return rc;
-  HostSlot& s = l.slots[l.cur];
+int feed_error(const Feed& f) { return host_fail(f.error, "%s", f.error_msg.c_str()); }
+
+// Launch a closed slot (writers done).  Caller holds `lk` on f.mu; it is
+// released around the HIP calls (the slot is BUSY meanwhile).
+int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
+  FeedRes& r = *f.res;
+  s.state = SLOT_BUSY;
+  s.stream = (int)(f.launch_seq++ % (uint32_t)r.nstreams);
+  const uint32_t n = s.rows;
+  const size_t words = s.words;
+  lk.unlock();
+  int rc = CUDASP_OK;
+  {
+    std::lock_guard<std::mutex> sl(f.stream_mu[s.stream]);
+    cudasp_scanner* sc = r.scanners[s.stream];
+    hipStream_t st = (hipStream_t)cudasp_internal_scanner_stream(sc);
+    DeviceSet dg(r.device);
+    auto run = [&]() -> int {
+      if (words > s.d_outputs_cap) {  // the slot's previous launch has been harvested: no kernel reads it
+        if (s.d_outputs) HOST_HIP(hipFree(s.d_outputs));
+        s.d_outputs = nullptr;
+        s.d_outputs_cap = 0;
+        HOST_HIP(hipMalloc((void**)&s.d_outputs, s.outputs_cap * sizeof(int64_t)));
+        s.d_outputs_cap = s.outputs_cap;
+      }
+      HOST_HIP(hipMemcpyAsync(s.d_rows, s.h_tweaks, (size_t)n * 64, hipMemcpyHostToDevice, st));
+      HOST_HIP(hipMemcpyAsync(s.d_offs, s.h_offs, (size_t)n * 4, hipMemcpyHostToDevice, st));
+      HOST_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, st));
+      if (words)
+        HOST_HIP(hipMemcpyAsync(s.d_outputs, s.h_outputs, words * sizeof(int64_t), hipMemcpyHostToDevice, st));
+      int rc2 = cudasp_tweaks_to_columns(s.d_rows, n, s.d_tx, s.d_ty, st);
+      if (rc2 == CUDASP_OK)
+        rc2 = cudasp_scan_device(sc, s.d_tx, s.d_ty, s.d_outputs, s.d_offs, s.d_lens, n, s.d_flags, nullptr, nullptr,
+                                 st);
+      if (rc2 != CUDASP_OK)
+        return host_fail(rc2, "cudasp_scan batch of %u rows on device %d failed: %s", n, r.device,
+                         cudasp_last_error());
+      HOST_HIP(hipMemcpyAsync(s.h_flags, s.d_flags, n, hipMemcpyDeviceToHost, st));
+      HOST_HIP(hipEventRecord(s.done, st));
+      return CUDASP_OK;
+    };
+    rc = run();
+  }
+  lk.lock();
+  if (rc != CUDASP_OK) {
+    s.state = SLOT_FREE;  // its rows are lost; the query fails with rc
+    feed_fail(f, rc);
+  } else {
+    s.state = SLOT_LAUNCHED;
+    f.launches++;
+    f.rows += n;
+  }
+  f.cv.notify_all();
+  return rc;
+}
+
+// Wait for a launched slot and move its matches to the global list
+// (ProcessBatch :378-392).  Caller holds `lk`; released while waiting.
+int harvest_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
+  s.state = SLOT_BUSY;
+  lk.unlock();
+  const double t0 = now_s();
+  hipError_t e;
+  {
+    DeviceSet dg(f.res->device);
+    e = hipEventSynchronize(s.done);
+  }
+  const double waited = now_s() - t0;
+  if (e == hipSuccess) {
+    cudasp_tf_global& g = *f.g;
+    std::lock_guard<std::mutex> lock(g.output_lock);
+    for (uint32_t i = 0; i < s.rows; i++) {
+      if (!s.h_flags[i]) continue;
+      g.output_txids.emplace_back((const char*)s.txid_bytes.data() + s.txid_off[i], s.txid_size[i]);
+      g.output_heights.push_back(s.heights[i]);
+      g.output_tweak_keys.emplace_back((const char*)s.h_tweaks + (size_t)i * TWEAK_KEY_SIZE, TWEAK_KEY_SIZE);
+    }
+  }
+  lk.lock();
+  f.harvest_wait_s += waited;
+  s.state = SLOT_FREE;
+  f.cv.notify_all();
+  if (e != hipSuccess)
+    return feed_fail(f, host_fail(CUDASP_ERR_HIP, "batch on device %d failed: %s", f.res->device,
+                                  hipGetErrorString(e)));
+  return CUDASP_OK;
+}
+
+// Close the open slot (no more reservations) and move on to the next; the
+// last writer launches it (launch_locked directly if there is none).
+int close_open_locked(Feed& f, std::unique_lock<std::mutex>& lk) {
+  FeedSlot& s = f.res->slots[f.open];
+  s.state = SLOT_CLOSED;
+  f.open = (f.open + 1) % f.res->nslots();
+  if (s.writers == 0) return launch_locked(f, s, lk);
+  return CUDASP_OK;
+}
+
+struct Reservation {
+  FeedSlot* slot = nullptr;
+  uint32_t row0 = 0;
+  size_t word0 = 0;
+  size_t tx0 = 0;
+};
+
+// Room for a chunk of nrows rows, nwords output words and ntx txid bytes in
+// the feed's open slot.  Blocks while the ring is busy; harvests finished
+// slots on the way (that wait is the executor threads' back-pressure).
+int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation* out) {
+  FeedRes& r = *f.res;
+  std::unique_lock<std::mutex> lk(f.mu);
+  for (;;) {
+    if (f.error != CUDASP_OK) return feed_error(f);
+    FeedSlot& s = r.slots[f.open];
+    switch (s.state) {
+      case SLOT_FREE: {
+        const size_t want_words = std::max((size_t)(f.words_per_row * r.cap_rows), nwords);
+        const size_t want_tx = std::max((size_t)(f.txid_per_row * r.cap_rows), ntx);
+        if (!s.allocated || s.outputs_cap < want_words || s.txid_bytes.size() < want_tx) {
+          s.state = SLOT_BUSY;
+          lk.unlock();
+          const int rc = prepare_slot(s, r.device, r.cap_rows, want_words, want_tx);
+          lk.lock();
+          s.state = SLOT_FREE;
+          f.cv.notify_all();
+          if (rc != CUDASP_OK) return feed_fail(f, rc);
+        }
+        s.state = SLOT_FILLING;
+        s.rows = 0;
+        s.words = 0;
+        s.txid_used = 0;
+        s.writers = 0;
+        continue;
+      }
+      case SLOT_FILLING: {
+        if (s.rows + nrows <= r.cap_rows && s.words + nwords <= s.outputs_cap &&
+            s.txid_used + ntx <= s.txid_bytes.size()) {
+          out->slot = &s;
+          out->row0 = s.rows;
+          out->word0 = s.words;
+          out->tx0 = s.txid_used;
+          s.rows += nrows;
+          s.words += nwords;
+          s.txid_used += ntx;
+          s.writers++;
+          // >= batch_size (:416-418): closed now, launched by its last writer
+          if (s.rows >= f.batch_size) {
+            s.state = SLOT_CLOSED;
+            f.open = (f.open + 1) % r.nslots();
+          }
+          return CUDASP_OK;
+        }
+        if (s.rows == 0) {  // an empty slot (no writers) too small for this chunk: grow it
+          f.words_per_row = std::max(f.words_per_row, (double)nwords / r.cap_rows);
+          f.txid_per_row = std::max(f.txid_per_row, (double)ntx / r.cap_rows);
+          s.state = SLOT_BUSY;
+          lk.unlock();
+          const int rc = prepare_slot(s, r.device, r.cap_rows, nwords, ntx);
+          lk.lock();
+          s.state = SLOT_FILLING;
+          f.cv.notify_all();
+          if (rc != CUDASP_OK) {
+            s.state = SLOT_FREE;
+            return feed_fail(f, rc);
+          }
+          continue;
+        }
+        // out of output or txid space before batch_size rows: close it, and
+        // open later slots with room for this shape of row
+        const double rows_after = (double)(s.rows + nrows);
+        f.words_per_row = std::max(f.words_per_row, 1.25 * (s.words + nwords) / rows_after);
+        f.txid_per_row = std::max(f.txid_per_row, 1.25 * (s.txid_used + ntx) / rows_after);
+        const int rc = close_open_locked(f, lk);
+        if (rc != CUDASP_OK) return rc;
+        continue;
+      }
+      case SLOT_LAUNCHED: {
+        const int rc = harvest_locked(f, s, lk);
+        if (rc != CUDASP_OK) return rc;
+        continue;
+      }
+      default:  // CLOSED (writers still copying) or BUSY (allocating, launching, harvesting)
+        f.cv.wait(lk);
+    }
+  }
+}
+
+// A reservation's copy is done; the last writer of a closed slot launches it.
+int feed_commit(Feed& f, FeedSlot& s) {
+  std::unique_lock<std::mutex> lk(f.mu);
+  s.writers--;
+  if (s.state == SLOT_CLOSED && s.writers == 0) return launch_locked(f, s, lk);
+  return CUDASP_OK;
+}
+
+// End of the query's input: launch every feed's partial slot (all feeds
+// first, so the devices drain in parallel), then harvest everything.
+int feeds_flush(cudasp_tf_global& g) {
+  int rc = CUDASP_OK;
+  for (auto& fp : g.feeds) {
+    if (!fp) continue;
+    Feed& f = *fp;
+    std::unique_lock<std::mutex> lk(f.mu);
+    FeedSlot& s = f.res->slots[f.open];
+    if (s.state == SLOT_FILLING) {
+      if (s.rows > 0) {
+        const int r2 = close_open_locked(f, lk);
+        if (rc == CUDASP_OK) rc = r2;
+      } else {
+        s.state = SLOT_FREE;
+      }
+    }
+  }
+  for (auto& fp : g.feeds) {
+    if (!fp) continue;
+    Feed& f = *fp;
+    std::unique_lock<std::mutex> lk(f.mu);
+    for (int i = 0; i < f.res->nslots(); i++) {
+      FeedSlot& s = f.res->slots[(f.open + i) % f.res->nslots()];
+      while (s.state == SLOT_CLOSED || s.state == SLOT_BUSY) f.cv.wait(lk);
+      if (s.state == SLOT_LAUNCHED) {
+        const int r2 = harvest_locked(f, s, lk);
+        if (rc == CUDASP_OK) rc = r2;
+      }
+    }
+    if (rc == CUDASP_OK && f.error != CUDASP_OK) rc = feed_error(f);
+  }
+  return rc;
+}
+
+// The feed of logical GPU `lg`, created on first use: pooled resources for
+// (device, capacity, streams), or new scanners, rebound to this query's keys.
+int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** out) {
+  if ((*out = g.feed_ptr[lg].load(std::memory_order_acquire)) != nullptr) return CUDASP_OK;
+  std::lock_guard<std::mutex> lock(g.feed_create_mu[lg]);
+  if ((*out = g.feed_ptr[lg].load(std::memory_order_acquire)) != nullptr) return CUDASP_OK;
+  const int device = g.device_map[lg];
+  const uint32_t cap_rows = (uint32_t)(b.batch_size + CUDASP_TF_VECTOR_SIZE);
+  const auto* scan = (const uint8_t*)b.scan_private_key_data.data();
+  const auto* spend = (const uint8_t*)b.spend_public_key_data.data();
+  const auto* labels = (const uint8_t*)b.label_keys_flat.data();
+  const auto nlabels = (uint32_t)b.label_keys_data.size();
+  FeedRes* r = pool_take(device, cap_rows, g.feed_streams);
+  if (r) {
+    for (int k = 0; k < r->nstreams; k++) {
+      int rc = cudasp_scanner_set_keys(r->scanners[k], scan, spend, labels, nlabels);
+      if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(r->scanners[k], &b.opt);
+      if (rc != CUDASP_OK) {
+        pool_put(r);
+        return host_fail(rc, "Failed to bind scanner on GPU %d: %s", lg, cudasp_last_error());
+      }
+    }
+  } else {
+    r = new FeedRes();
+    r->device = device;
+    r->cap_rows = cap_rows;
+    r->nstreams = g.feed_streams;
+    for (int k = 0; k < r->nstreams; k++) {
+      int rc = cudasp_scanner_create(device, scan, spend, labels, nlabels, cap_rows, &r->scanners[k]);
+      if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(r->scanners[k], &b.opt);
+      if (rc != CUDASP_OK) {
+        std::string msg = cudasp_last_error();
+        release_res(r);
+        return host_fail(rc, "Failed to create scanner on GPU %d: %s", lg, msg.c_str());
+      }
+    }
+  }
+  auto f = std::make_unique<Feed>();
+  f->res = r;
+  f->g = &g;
+  f->batch_size = b.batch_size;
+  f->ow = out_words(b);
+  f->words_per_row = 2.0 * f->ow;
+  *out = f.get();
+  g.feeds[lg] = std::move(f);
+  g.feed_ptr[lg].store(*out, std::memory_order_release);
+  return CUDASP_OK;
+}
+
+// The logical GPU of a thread's next chunk: round-robin from its assigned GPU.
+int next_feed_index(const cudasp_tf_global& g, cudasp_tf_local& l) {
+  const uint64_t c = l.chunks++;
+  return g.num_gpus > 1 ? (int)((l.assigned_gpu + c) % (uint64_t)g.num_gpus) : 0;
+}
+
+// AccumulateInput (src/cudasp_extension.cu:154-224) for one DuckDB chunk:
+// count and validate the rows (NULL txid/height/tweak rows skipped, NULL list
+// = no outputs, NULL elements dropped, :195-221), reserve, copy, commit.
+int feed_chunk(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l, const cudasp_tf_chunk& c) {
   const size_t ow = out_words(b);
   if (b.opt.full_x && c.count > 0 && (!c.child_blob_data || !c.child_blob_size))
     return host_fail(CUDASP_ERR_INVALID_ARG, "full_x needs the outputs column as BLOB[] (child_blob_data)");
+  uint32_t nrows = 0;
+  size_t nouts = 0, ntx = 0;
   for (uint32_t i = 0; i < c.count; i++) {
-    // Only rows with valid txid, height and tweak_key (:195-197).
     if (!(valid(c.txid_valid, i) && valid(c.height_valid, i) && valid(c.tweak_valid, i))) continue;
     if (c.tweak_size[i] != TWEAK_KEY_SIZE)
       return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", c.tweak_size[i]);
-    uint32_t r = s.rows;
-    s.txid_offset.push_back(s.txid_bytes.size());
-    s.txid_size.push_back(c.txid_size[i]);
-    s.txid_bytes.insert(s.txid_bytes.end(), c.txid_data[i], c.txid_data[i] + c.txid_size[i]);
-    s.heights.push_back(c.height[i]);
+    nrows++;
+    ntx += c.txid_size[i];
+    if (!valid(c.list_valid, i)) continue;
+    for (uint64_t k = 0; k < c.list_length[i]; k++) {
+      const uint64_t ci = c.list_offset[i] + k;
+      if (!valid(c.child_valid, ci)) continue;
+      if (b.opt.full_x && c.child_blob_size[ci] != XONLY_SIZE)
+        return host_fail(CUDASP_ERR_INVALID_ARG, "full_x outputs must be 32-byte x-only keys, got %u bytes",
+                         c.child_blob_size[ci]);
+      nouts++;
+    }
+  }
+  if (nrows == 0) return CUDASP_OK;
+  Feed* f = nullptr;
+  int rc = feed_for(g, b, next_feed_index(g, l), &f);
+  if (rc != CUDASP_OK) return rc;
+  Reservation res;
+  rc = feed_reserve(*f, nrows, nouts * ow, ntx, &res);
+  if (rc != CUDASP_OK) return rc;
+  FeedSlot& s = *res.slot;
+  uint32_t r = res.row0;
+  size_t o = res.word0 / ow;  // output index
+  size_t tx = res.tx0;
+  for (uint32_t i = 0; i < c.count; i++) {
+    if (!(valid(c.txid_valid, i) && valid(c.height_valid, i) && valid(c.tweak_valid, i))) continue;
+    s.txid_off[r] = tx;
+    s.txid_size[r] = c.txid_size[i];
+    if (c.txid_size[i]) memcpy(s.txid_bytes.data() + tx, c.txid_data[i], c.txid_size[i]);
+    tx += c.txid_size[i];
+    s.heights[r] = c.height[i];
     memcpy(s.h_tweaks + (size_t)r * TWEAK_KEY_SIZE, c.tweak_data[i], TWEAK_KEY_SIZE);
-    // Outputs: NULL list -> length 0; NULL elements dropped (:206-221).
-    s.h_offs[r] = (uint32_t)s.n_outputs;
+    s.h_offs[r] = (uint32_t)o;
     uint32_t len = 0;
     if (valid(c.list_valid, i)) {
-      rc = ensure_outputs_cap(s, (s.n_outputs + c.list_length[i]) * ow, ow);
-      if (rc != CUDASP_OK) return rc;
       for (uint64_t k = 0; k < c.list_length[i]; k++) {
-        uint64_t ci = c.list_offset[i] + k;
-        if (!valid(c.child_valid, (uint32_t)ci)) continue;
-        if (b.opt.full_x) {
-          if (c.child_blob_size[ci] != XONLY_SIZE)
-            return host_fail(CUDASP_ERR_INVALID_ARG, "full_x outputs must be 32-byte x-only keys, got %u bytes",
-                             c.child_blob_size[ci]);
-          memcpy(s.h_outputs + s.n_outputs * ow, c.child_blob_data[ci], XONLY_SIZE);
-          s.n_outputs++;
-        } else {
-          s.h_outputs[s.n_outputs++] = c.child_values[ci];
-        }
+        const uint64_t ci = c.list_offset[i] + k;
+        if (!valid(c.child_valid, ci)) continue;
+        if (b.opt.full_x)
+          memcpy(s.h_outputs + o * ow, c.child_blob_data[ci], XONLY_SIZE);
+        else
+          s.h_outputs[o] = c.child_values[ci];
+        o++;
         len++;
       }
     }
     s.h_lens[r] = len;
-    s.rows = r + 1;
+    r++;
   }
-  return CUDASP_OK;
+  return feed_commit(*f, s);
 }
 
-// Columnar rows [r0, r1) of `c` (Arrow layout, cudasp_tf_columns) into the
-// current slot, same row rules as accumulate().  Without validity bitmaps and
-// with 64-byte tweaks the four columns are appended with bulk copies.
-inline bool bit(const uint8_t* bm, uint64_t i) { return bm == nullptr || ((bm[i >> 3] >> (i & 7)) & 1u); }
-
-int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const cudasp_tf_columns& c, uint64_t r0,
-                       uint64_t r1) {
-  int rc = ensure_local_gpu(b, l);
-  if (rc != CUDASP_OK) return rc;
-  HostSlot& s = l.slots[l.cur];
+// Columnar rows [r0, r1) of `c` (Arrow layout, cudasp_tf_columns), same row
+// rules as feed_chunk.  Without validity bitmaps and with 64-byte tweaks the
+// four columns are appended with bulk copies.
+int feed_columns(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l, const cudasp_tf_columns& c,
+                 uint64_t r0, uint64_t r1) {
   const uint64_t n = r1 - r0;
   const size_t ow = out_words(b);
+  const int32_t* txo = c.txid_offsets + c.txid_offset;
+  const int32_t* lo = c.list_offsets + c.list_offset;
   // full_x: the outputs child is binary (child_blob_offsets) or
   // fixed_size_binary(child_blob_fixed_width) of 32-byte x-only keys.
   auto child_blob = [&](uint64_t k, uint32_t* size) -> const uint8_t* {
@@ -395,21 +713,6 @@ int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const c
     *size = (uint32_t)c.child_blob_fixed_width;
     return c.child_blob_data + ck * (uint64_t)c.child_blob_fixed_width;
   };
-  auto push_output = [&](uint64_t k) -> int {
-    if (!b.opt.full_x) {
-      s.h_outputs[s.n_outputs++] = c.child_values[c.child_offset + k];
-      return CUDASP_OK;
-    }
-    uint32_t sz;
-    const uint8_t* p = child_blob(k, &sz);
-    if (sz != XONLY_SIZE)
-      return host_fail(CUDASP_ERR_INVALID_ARG, "full_x outputs must be 32-byte x-only keys, got %u bytes", sz);
-    memcpy(s.h_outputs + s.n_outputs * ow, p, XONLY_SIZE);
-    s.n_outputs++;
-    return CUDASP_OK;
-  };
-  const int32_t* txo = c.txid_offsets + c.txid_offset;
-  const int32_t* lo = c.list_offsets + c.list_offset;
   auto tweak_ptr = [&](uint64_t i, uint32_t* size) -> const uint8_t* {
     if (c.tweak_offsets) {
       const int32_t* to = c.tweak_offsets + c.tweak_offset;
@@ -418,6 +721,10 @@ int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const c
     }
     *size = (uint32_t)c.tweak_fixed_width;
     return c.tweak_data + (c.tweak_offset + i) * (uint64_t)c.tweak_fixed_width;
+  };
+  auto row_ok = [&](uint64_t i) {
+    return bit(c.txid_validity, c.txid_offset + i) && bit(c.height_validity, c.height_offset + i) &&
+           bit(c.tweak_validity, c.tweak_offset + i);
   };
   bool fast = !c.txid_validity && !c.height_validity && !c.tweak_validity && !c.list_validity && !c.child_validity;
   if (fast && c.tweak_offsets) {
@@ -429,126 +736,126 @@ int accumulate_columns(const cudasp_tf_bind_data& b, cudasp_tf_local& l, const c
   if (fast && b.opt.full_x) {  // bulk copy only for fixed 32-byte keys
     fast = !c.child_blob_offsets && c.child_blob_fixed_width == (int32_t)XONLY_SIZE;
   }
+  uint32_t nrows = 0;
+  size_t nouts = 0, ntx = 0;
   if (fast) {
-    const uint32_t r = s.rows;
-    uint32_t sz;
-    memcpy(s.h_tweaks + (size_t)r * TWEAK_KEY_SIZE, tweak_ptr(r0, &sz), n * TWEAK_KEY_SIZE);
-    s.heights.insert(s.heights.end(), c.height + c.height_offset + r0, c.height + c.height_offset + r1);
-    const size_t tbase = s.txid_bytes.size();
-    s.txid_bytes.insert(s.txid_bytes.end(), c.txid_data + txo[r0], c.txid_data + txo[r1]);
-    const uint64_t first = (uint64_t)lo[r0], total = (uint64_t)lo[r1] - first;
-    rc = ensure_outputs_cap(s, (s.n_outputs + total) * ow, ow);
-    if (rc != CUDASP_OK) return rc;
-    if (b.opt.full_x)
-      memcpy(s.h_outputs + s.n_outputs * ow, c.child_blob_data + (c.child_offset + first) * XONLY_SIZE,
-             total * XONLY_SIZE);
-    else
-      memcpy(s.h_outputs + s.n_outputs, c.child_values + c.child_offset + first, total * sizeof(int64_t));
+    nrows = (uint32_t)n;
+    nouts = (size_t)(lo[r1] - lo[r0]);
+    ntx = (size_t)(txo[r1] - txo[r0]);
+  } else {
     for (uint64_t i = r0; i < r1; i++) {
-      const uint32_t row = r + (uint32_t)(i - r0);
-      s.txid_offset.push_back(tbase + (size_t)(txo[i] - txo[r0]));
-      s.txid_size.push_back((uint32_t)(txo[i + 1] - txo[i]));
-      s.h_offs[row] = (uint32_t)(s.n_outputs + ((uint64_t)lo[i] - first));
+      if (!row_ok(i)) continue;
+      uint32_t tsize;
+      (void)tweak_ptr(i, &tsize);
+      if (tsize != TWEAK_KEY_SIZE)
+        return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", tsize);
+      nrows++;
+      ntx += (size_t)(txo[i + 1] - txo[i]);
+      if (!bit(c.list_validity, c.list_offset + i)) continue;
+      for (int64_t k = lo[i]; k < lo[i + 1]; k++) {
+        if (!bit(c.child_validity, c.child_offset + (uint64_t)k)) continue;
+        if (b.opt.full_x) {
+          uint32_t sz;
+          (void)child_blob((uint64_t)k, &sz);
+          if (sz != XONLY_SIZE)
+            return host_fail(CUDASP_ERR_INVALID_ARG, "full_x outputs must be 32-byte x-only keys, got %u bytes", sz);
+        }
+        nouts++;
+      }
+    }
+  }
+  if (nrows == 0) return CUDASP_OK;
+  Feed* f = nullptr;
+  int rc = feed_for(g, b, next_feed_index(g, l), &f);
+  if (rc != CUDASP_OK) return rc;
+  Reservation res;
+  rc = feed_reserve(*f, nrows, nouts * ow, ntx, &res);
+  if (rc != CUDASP_OK) return rc;
+  FeedSlot& s = *res.slot;
+  const uint32_t rbase = res.row0;
+  const size_t obase = res.word0 / ow;
+  if (fast) {
+    uint32_t sz;
+    memcpy(s.h_tweaks + (size_t)rbase * TWEAK_KEY_SIZE, tweak_ptr(r0, &sz), n * TWEAK_KEY_SIZE);
+    memcpy(s.heights.data() + rbase, c.height + c.height_offset + r0, n * sizeof(int32_t));
+    if (ntx) memcpy(s.txid_bytes.data() + res.tx0, c.txid_data + txo[r0], ntx);
+    const uint64_t first = (uint64_t)lo[r0];
+    if (nouts) {
+      if (b.opt.full_x)
+        memcpy(s.h_outputs + obase * ow, c.child_blob_data + (c.child_offset + first) * XONLY_SIZE, nouts * XONLY_SIZE);
+      else
+        memcpy(s.h_outputs + obase, c.child_values + c.child_offset + first, nouts * sizeof(int64_t));
+    }
+    for (uint64_t i = r0; i < r1; i++) {
+      const uint32_t row = rbase + (uint32_t)(i - r0);
+      s.txid_off[row] = res.tx0 + (size_t)(txo[i] - txo[r0]);
+      s.txid_size[row] = (uint32_t)(txo[i + 1] - txo[i]);
+      s.h_offs[row] = (uint32_t)(obase + ((uint64_t)lo[i] - first));
       s.h_lens[row] = (uint32_t)(lo[i + 1] - lo[i]);
     }
-    s.n_outputs += total;
-    s.rows = r + (uint32_t)n;
-    return CUDASP_OK;
+    return feed_commit(*f, s);
   }
+  uint32_t r = rbase;
+  size_t o = obase, tx = res.tx0;
   for (uint64_t i = r0; i < r1; i++) {
-    if (!(bit(c.txid_validity, c.txid_offset + i) && bit(c.height_validity, c.height_offset + i) &&
-          bit(c.tweak_validity, c.tweak_offset + i)))
-      continue;
+    if (!row_ok(i)) continue;
     uint32_t tsize;
     const uint8_t* tw = tweak_ptr(i, &tsize);
-    if (tsize != TWEAK_KEY_SIZE)
-      return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", tsize);
-    const uint32_t r = s.rows;
-    s.txid_offset.push_back(s.txid_bytes.size());
-    s.txid_size.push_back((uint32_t)(txo[i + 1] - txo[i]));
-    s.txid_bytes.insert(s.txid_bytes.end(), c.txid_data + txo[i], c.txid_data + txo[i + 1]);
-    s.heights.push_back(c.height[c.height_offset + i]);
+    const uint32_t tl = (uint32_t)(txo[i + 1] - txo[i]);
+    s.txid_off[r] = tx;
+    s.txid_size[r] = tl;
+    if (tl) memcpy(s.txid_bytes.data() + tx, c.txid_data + txo[i], tl);
+    tx += tl;
+    s.heights[r] = c.height[c.height_offset + i];
     memcpy(s.h_tweaks + (size_t)r * TWEAK_KEY_SIZE, tw, TWEAK_KEY_SIZE);
-    s.h_offs[r] = (uint32_t)s.n_outputs;
+    s.h_offs[r] = (uint32_t)o;
     uint32_t len = 0;
     if (bit(c.list_validity, c.list_offset + i)) {
-      rc = ensure_outputs_cap(s, (s.n_outputs + (uint64_t)(lo[i + 1] - lo[i])) * ow, ow);
-      if (rc != CUDASP_OK) return rc;
       for (int64_t k = lo[i]; k < lo[i + 1]; k++) {
-        if (bit(c.child_validity, c.child_offset + (uint64_t)k)) {
-          rc = push_output((uint64_t)k);
-          if (rc != CUDASP_OK) return rc;
-          len++;
+        if (!bit(c.child_validity, c.child_offset + (uint64_t)k)) continue;
+        if (b.opt.full_x) {
+          uint32_t sz;
+          memcpy(s.h_outputs + o * ow, child_blob((uint64_t)k, &sz), XONLY_SIZE);
+        } else {
+          s.h_outputs[o] = c.child_values[c.child_offset + (uint64_t)k];
         }
+        o++;
+        len++;
       }
     }
     s.h_lens[r] = len;
-    s.rows = r + 1;
+    r++;
   }
-  return CUDASP_OK;
+  return feed_commit(*f, s);
 }
 
-// Collect a finished batch's matches into the global list (ProcessBatch
-// :378-392) and reset the slot.
-int harvest(cudasp_tf_global& g, cudasp_tf_local& l, HostSlot& s) {
-  if (!s.in_flight) return CUDASP_OK;
-  {
-    DeviceSet dg(l.device);
-    HOST_HIP(hipEventSynchronize(s.done));
-  }
-  s.in_flight = false;
-  uint32_t n = s.launched_rows;
-  {
-    std::lock_guard<std::mutex> lock(g.output_lock);
-    for (uint32_t i = 0; i < n; i++) {
-      if (!s.h_flags[i]) continue;
-      g.output_txids.emplace_back((const char*)s.txid_bytes.data() + s.txid_offset[i], s.txid_size[i]);
-      g.output_heights.push_back(s.heights[i]);
-      g.output_tweak_keys.emplace_back((const char*)s.h_tweaks + (size_t)i * TWEAK_KEY_SIZE, TWEAK_KEY_SIZE);
+// Drain a query's feeds (work still in flight after an error or an aborted
+// query) and park their resources in the pool.
+void feeds_release(cudasp_tf_global& g) {
+  for (auto& fp : g.feeds) {
+    if (!fp) continue;
+    Feed& f = *fp;
+    FeedRes* r = f.res;
+    {
+      std::unique_lock<std::mutex> lk(f.mu);
+      for (FeedSlot& s : r->slots) {
+        while (s.state == SLOT_CLOSED || s.state == SLOT_BUSY) f.cv.wait(lk);
+        s.state = SLOT_FREE;
+        s.writers = 0;
+      }
     }
-  }
-  s.txid_bytes.clear();
-  s.txid_offset.clear();
-  s.txid_size.clear();
-  s.heights.clear();
-  s.rows = 0;
-  s.n_outputs = 0;
-  return CUDASP_OK;
-}
-
-// ProcessBatch (src/cudasp_extension.cu:226-410), asynchronous: enqueue the
-// current slot on the thread's stream and switch to the other slot, first
-// harvesting it if its previous batch is still outstanding.
-int launch_batch(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l) {
-  HostSlot& s = l.slots[l.cur];
-  uint32_t n = s.rows;
-  if (n > 0) {
-    DeviceSet dg(l.device);
-    hipStream_t st = l.stream;
-    const size_t words = s.n_outputs * out_words(b);
-    if (words > s.d_outputs_cap) {
-      if (s.d_outputs) HOST_HIP(hipFree(s.d_outputs));
-      s.d_outputs = nullptr;
-      size_t cap = s.outputs_cap;
-      HOST_HIP(hipMalloc((void**)&s.d_outputs, cap * sizeof(int64_t)));
-      s.d_outputs_cap = cap;
+    bool ok = f.error == CUDASP_OK;
+    {
+      DeviceSet dg(r->device);
+      for (int k = 0; k < r->nstreams; k++) ok = cudasp_scanner_sync(r->scanners[k]) == CUDASP_OK && ok;
     }
-    HOST_HIP(hipMemcpyAsync(s.d_rows, s.h_tweaks, (size_t)n * 64, hipMemcpyHostToDevice, st));
-    HOST_HIP(hipMemcpyAsync(s.d_offs, s.h_offs, (size_t)n * 4, hipMemcpyHostToDevice, st));
-    HOST_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, st));
-    if (words) HOST_HIP(hipMemcpyAsync(s.d_outputs, s.h_outputs, words * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    int rc = cudasp_tweaks_to_columns(s.d_rows, n, s.d_tx, s.d_ty, st);
-    if (rc == CUDASP_OK)
-      rc = cudasp_scan_device(l.scanner, s.d_tx, s.d_ty, s.d_outputs, s.d_offs, s.d_lens, n, s.d_flags, nullptr,
-                              nullptr, st);
-    if (rc != CUDASP_OK) return host_fail(rc, "cudasp_scan batch of %u rows failed: %s", n, cudasp_last_error());
-    HOST_HIP(hipMemcpyAsync(s.h_flags, s.d_flags, n, hipMemcpyDeviceToHost, st));
-    HOST_HIP(hipEventRecord(s.done, st));
-    s.in_flight = true;
-    s.launched_rows = n;
+    fp.reset();
+    if (ok)
+      pool_put(r);
+    else
+      release_res(r);
   }
-  l.cur ^= 1;
-  return harvest(g, l, l.slots[l.cur]);
+  g.feeds.clear();
 }
 
 }  // namespace
@@ -681,19 +988,64 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
       g->num_gpus = (int)map.size();
     }
   }
+  g->bind = b;
+  g->feed_streams = feed_streams_for(b->batch_size);
+  g->feeds.resize(g->num_gpus);
+  g->feed_ptr.reset(new std::atomic<Feed*>[g->num_gpus]);
+  for (int lg = 0; lg < g->num_gpus; lg++) g->feed_ptr[lg].store(nullptr);
+  g->feed_create_mu.reset(new std::mutex[g->num_gpus]);
+  // The HIP runtime maps a process's streams on a device onto
+  // GPU_MAX_HW_QUEUES hardware queues (4 unless set before HIP initialises);
+  // streams sharing a queue serialize their kernels.  Report the setting and
+  // warn when this query's streams on one device exceed it.
+  const char* hq = getenv("GPU_MAX_HW_QUEUES");
+  g->hw_queues = hq && atoi(hq) > 0 ? atoi(hq) : 4;
+  for (int lg = 0; lg < g->num_gpus; lg++) {
+    int on_dev = 0;
+    for (int d : g->device_map) on_dev += d == g->device_map[lg] ? g->feed_streams : 0;
+    if (on_dev > g->max_streams_per_device) g->max_streams_per_device = on_dev;
+  }
+  static std::atomic<bool> warned{false};
+  if (g->max_streams_per_device > g->hw_queues && !warned.exchange(true))
+    fprintf(stderr,
+            "cudasp_scan: %d streams per device exceed GPU_MAX_HW_QUEUES=%d; streams that share a hardware queue "
+            "run their kernels one after another\n",
+            g->max_streams_per_device, g->hw_queues);
   *out = g;
   return CUDASP_OK;
 }
 
-void cudasp_tf_global_free(cudasp_tf_global* g) { delete g; }
+void cudasp_tf_global_free(cudasp_tf_global* g) {
+  if (!g) return;
+  feeds_release(*g);
+  delete g;
+}
 
 int cudasp_tf_num_gpus(const cudasp_tf_global* g) { return g ? g->num_gpus : 0; }
+
+int cudasp_tf_get_stats(cudasp_tf_global* g, cudasp_tf_stats* out) {
+  if (!g || !out) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
+  memset(out, 0, sizeof(*out));
+  out->streams_per_feed = (uint32_t)g->feed_streams;
+  out->max_streams_per_device = (uint32_t)g->max_streams_per_device;
+  out->hw_queues = (uint32_t)g->hw_queues;
+  for (auto& fp : g->feeds) {
+    if (!fp) continue;
+    std::lock_guard<std::mutex> lock(fp->mu);
+    out->feeds++;
+    out->launches += fp->launches;
+    out->rows += fp->rows;
+    out->harvest_wait_s += fp->harvest_wait_s;
+  }
+  return CUDASP_OK;
+}
 
 int cudasp_tf_local_init(cudasp_tf_global* g, cudasp_tf_local** out) {
   if (!g || !out) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
   g->currently_adding++;
   auto* l = new cudasp_tf_local();
-  // Round-robin per thread (src/cudasp_extension.cu:523-529).
+  // Round-robin per thread (src/cudasp_extension.cu:523-529): the logical GPU
+  // of the thread's first chunk; later chunks continue round-robin.
   l->assigned_gpu = g->num_gpus > 1 ? (int)cudasp_assign_gpu((uint64_t)g->next_gpu_assignment.fetch_add(1),
                                                              (uint32_t)g->num_gpus)
                                     : 0;
@@ -702,11 +1054,7 @@ int cudasp_tf_local_init(cudasp_tf_global* g, cudasp_tf_local** out) {
   return CUDASP_OK;
 }
 
-void cudasp_tf_local_free(cudasp_tf_local* l) {
-  if (!l) return;
-  free_local_gpu(*l);
-  delete l;
-}
+void cudasp_tf_local_free(cudasp_tf_local* l) { delete l; }
 
 int cudasp_tf_local_gpu(const cudasp_tf_local* l) { return l ? l->assigned_gpu : -1; }
 
@@ -717,12 +1065,12 @@ uint32_t cudasp_assign_gpu(uint64_t ordinal, uint32_t num_gpus) {
 }
 
 void cudasp_tf_release_pool(void) {
-  std::vector<GpuCtx*> all;
+  std::vector<FeedRes*> all;
   {
     std::lock_guard<std::mutex> lock(g_pool_mu);
     all.swap(g_pool);
   }
-  for (GpuCtx* c : all) release_ctx(c);
+  for (FeedRes* r : all) release_res(r);
 }
 
 uint32_t cudasp_tf_pool_size(void) {
@@ -733,19 +1081,14 @@ uint32_t cudasp_tf_pool_size(void) {
 int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
                        const cudasp_tf_chunk* chunk) {
   if (!b || !g || !l || !chunk) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
-  // The batch slots hold batch_size + one vector of rows (the >= batch_size
-  // trigger runs after each chunk), so a chunk may not exceed one vector.
+  // The batch slots hold batch_size + one vector of rows (a slot closes once
+  // it holds >= batch_size), so a chunk may not exceed one vector.
   if (chunk->count > CUDASP_TF_VECTOR_SIZE)
     return host_fail(CUDASP_ERR_INVALID_ARG, "chunk of %u rows exceeds the vector size %d", chunk->count,
                      CUDASP_TF_VECTOR_SIZE);
   if (chunk->count > 0) {
-    int rc = accumulate(*b, *l, *chunk);
+    const int rc = feed_chunk(*b, *g, *l, *chunk);
     if (rc != CUDASP_OK) return rc;
-    // ShouldProcessBatch: accumulated >= batch_size (:416-418).
-    if (l->rows() >= b->batch_size) {
-      rc = launch_batch(*b, *g, *l);
-      if (rc != CUDASP_OK) return rc;
-    }
   }
   return CUDASP_TF_NEED_MORE_INPUT;
 }
@@ -765,15 +1108,11 @@ int cudasp_tf_function_columns(const cudasp_tf_bind_data* b, cudasp_tf_global* g
       return host_fail(CUDASP_ERR_INVALID_ARG, b->opt.full_x ? "full_x needs the outputs child as binary (child_blob_*)"
                                                               : "missing outputs child values");
   }
-  // DuckDB-sized pieces, with the same trigger as cudasp_tf_function.
+  // DuckDB-sized pieces, each fed like one chunk.
   for (uint64_t r0 = 0; r0 < c.count; r0 += CUDASP_TF_VECTOR_SIZE) {
     const uint64_t r1 = r0 + CUDASP_TF_VECTOR_SIZE < c.count ? r0 + CUDASP_TF_VECTOR_SIZE : c.count;
-    int rc = accumulate_columns(*b, *l, c, r0, r1);
+    const int rc = feed_columns(*b, *g, *l, c, r0, r1);
     if (rc != CUDASP_OK) return rc;
-    if (l->rows() >= b->batch_size) {
-      rc = launch_batch(*b, *g, *l);
-      if (rc != CUDASP_OK) return rc;
-    }
   }
   return CUDASP_TF_NEED_MORE_INPUT;
 }
@@ -782,24 +1121,23 @@ int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf
   if (!b || !g || !l || !out) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
   out->count = 0;
   if (!l->finalized) {
-    // Flush this thread's last rows and wait for both slots.
-    int rc = CUDASP_OK;
-    if (l->rows() > 0) rc = launch_batch(*b, *g, *l);
-    for (HostSlot& s : l->slots)
-      if (rc == CUDASP_OK) rc = harvest(*g, *l, s);
-    if (rc != CUDASP_OK) return rc;
-  }
-  if (!l->finalized) {
-    std::lock_guard<std::mutex> lock(g->finalize_lock);
-    g->currently_adding--;
-    l->finalized = true;
-  }
-  if (!l->is_output_thread) {
-    if (g->currently_adding.load() != 0) return CUDASP_TF_FINISHED;
+    // A thread's rows are already in the device feeds.  The last thread to
+    // finish launches every feed's partial slot, waits for all of them and
+    // becomes the output thread (:554-624: the last thread emits).
+    uint64_t remaining;
+    {
+      std::lock_guard<std::mutex> lock(g->finalize_lock);
+      remaining = --g->currently_adding;
+      l->finalized = true;
+    }
+    if (remaining != 0) return CUDASP_TF_FINISHED;
     bool expected = false;
     if (!g->output_thread_claimed.compare_exchange_strong(expected, true)) return CUDASP_TF_FINISHED;
     l->is_output_thread = true;
+    const int rc = feeds_flush(*g);
+    if (rc != CUDASP_OK) return rc;
   }
+  if (!l->is_output_thread) return CUDASP_TF_FINISHED;
   size_t total = g->output_txids.size();
   if (g->output_position < total) {
     size_t cnt = total - g->output_position;

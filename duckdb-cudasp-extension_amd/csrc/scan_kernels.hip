@@ -855,15 +855,29 @@ bool fb_bits_supported(int bits) { return bits == 22 || bits == 26 || bits == LD
 int g_default_fb_bits = 0;  // 0: not read yet
 std::once_flag g_default_fb_once;
 
-// The process default width: CUDASP_FB_BITS (22 or 26) from the environment,
-// else the build's FB_BITS.
+// Devices with at least this much memory take the 26-bit table by default
+// (21.5 GB: 7.5% of an MI355X's 288 GB); smaller ones the 22-bit table.
+constexpr uint64_t FB26_MIN_DEVICE_BYTES = 128ull << 30;
+
+// The process default width: CUDASP_FB_BITS (22 or 26) from the environment;
+// else 26 bits when the current device has >= 128 GiB (every MI355X), else
+// the build's FB_BITS.  Read once per process (the synthetic generator uses
+// it too).
 int default_fb_bits() {
   std::call_once(g_default_fb_once, [] {
     g_default_fb_bits = FB_BITS;
     if (const char* e = getenv("CUDASP_FB_BITS")) {
       const int b = atoi(e);
-      if (b == 22 || b == 26) g_default_fb_bits = b;  // the HBM widths (the synthetic generator uses it too)
+      if (b == 22 || b == 26) {
+        g_default_fb_bits = b;
+        return;
+      }
     }
+    int dev = 0;
+    size_t total = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceTotalMem(&total, dev) == hipSuccess &&
+        (uint64_t)total >= FB26_MIN_DEVICE_BYTES)
+      g_default_fb_bits = 26;
   });
   return g_default_fb_bits;
 }
@@ -935,10 +949,14 @@ struct cudasp_scanner {
   uint32_t t_cap_k = 1;            // output indices d_t / d_vflags are sized for
   std::vector<uint8_t> keys;       // scan key || spend key || label keys (set_options re-prepares)
   uint32_t raw_label_count = 0;
+  // Stage-kernel buffers (k_shared_secret / k_match: the stage entry points,
+  // the values path, the protocol variants, the LDS width).  Allocated on
+  // first use (ensure_stage_buffers): a scanner that only runs the fused
+  // k_scan_multi path -- every default-option batch -- never holds them.
   uint32_t* d_t = nullptr;         // 8 x (t_cap_k capacity)
   uint8_t* d_vflags = nullptr;     // t_cap_k x capacity (K > 1: per output index)
   uint32_t* d_vscratch = nullptr;  // VSCRATCH_WORDS x slots_a
-  uint32_t* d_lscratch = nullptr;  // lscratch_words(L) x slots_b
+  uint32_t* d_lscratch = nullptr;  // lscratch_words(label_cap) x slots_b
   uint32_t slots_a = 0, slots_b = 0;
   uint32_t fill_threads = 0;    // stage-A threads per launch that fill the device (rows_a_for)
   uint32_t fill_threads_b = 0;  // the same for stage B (rows_b_for)
@@ -1077,9 +1095,44 @@ void free_scanner(cudasp_scanner* s) {
   delete s;
 }
 
+// The stage kernels' buffers, allocated on a scanner's first stage-kernel
+// launch (sized for its capacity, output indices and label capacity).
+int ensure_stage_buffers(cudasp_scanner* s) {
+  if (s->d_t) return CUDASP_OK;
+  DeviceGuard g(s->device);
+  uint32_t* d_t = nullptr;
+  uint8_t* d_vflags = nullptr;
+  uint32_t* d_vscratch = nullptr;
+  uint32_t* d_lscratch = nullptr;
+  const size_t sizes[4] = {(size_t)8 * s->t_cap_k * s->capacity * 4, (size_t)s->t_cap_k * s->capacity,
+                           (size_t)VSCRATCH_WORDS * s->slots_a * 4,
+                           (size_t)lscratch_words(s->label_cap) * s->slots_b * 4};
+  void** ptrs[4] = {(void**)&d_t, (void**)&d_vflags, (void**)&d_vscratch, (void**)&d_lscratch};
+  for (int i = 0; i < 4; i++) {
+    if (i == 1 && s->t_cap_k <= 1) continue;  // per-index flags only with output_count > 1
+    hipError_t e = hipMalloc(ptrs[i], sizes[i] ? sizes[i] : 4);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      for (int j = 0; j < i; j++)
+        if (*ptrs[j]) (void)hipFree(*ptrs[j]);
+      return set_error(CUDASP_ERR_HIP, "hipMalloc(%zu) for the stage kernels failed: %s", sizes[i],
+                       hipGetErrorString(e));
+    }
+  }
+  s->d_t = d_t;
+  s->d_vflags = d_vflags;
+  s->d_vscratch = d_vscratch;
+  s->d_lscratch = d_lscratch;
+  return CUDASP_OK;
+}
+
 // Stage B with the LDS-staged 7-bit table (k_match_lds): 768-thread
 // workgroups, 2 rows per thread (6 for launches large enough to fill the
-// device at 6), within the label scratch's slots.
+// device at 6), within the label scratch's slots: every launched thread
+// needs a slot, so the grid is capped at slots / LDS_BLOCK workgroups.  A
+// small scanner (slots_b < LDS_BLOCK at 6 rows) takes 2 rows per thread,
+// whose slots are smaller; if even one 2-row workgroup does not fit, the
+// launch fails with CUDASP_ERR_CAPACITY instead of writing past the scratch.
 int launch_match_lds(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int64_t* outputs, const uint32_t* offs,
                      const uint32_t* lens, uint8_t* flags, uint32_t* match_rows, uint32_t* match_count,
                      int64_t* values, hipStream_t st) {
@@ -1087,11 +1140,23 @@ int launch_match_lds(cudasp_scanner* s, const uint32_t* t, uint32_t n, const int
   const uint32_t N = K * n;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
-  const int r = s->rows_b_force ? s->rows_b_force
-                                : ((N + ROWS_B - 1) / ROWS_B >= (uint32_t)cus * LDS_BLOCK ? ROWS_B : 2);
+  int r = s->rows_b_force ? s->rows_b_force
+                          : ((N + ROWS_B - 1) / ROWS_B >= (uint32_t)cus * LDS_BLOCK ? ROWS_B : 2);
+  auto cap_for = [s](int rows) {
+    return (uint64_t)s->slots_b * lscratch_words(s->label_cap) /
+           ((uint64_t)lscratch_words(s->label_count, rows) * LDS_BLOCK);
+  };
+  uint64_t cap = cap_for(r);
+  if (cap == 0 && r != 2) {
+    r = 2;
+    cap = cap_for(r);
+  }
+  if (cap == 0)
+    return set_error(CUDASP_ERR_CAPACITY,
+                     "scanner too small for the LDS fixed-base width: %u scratch slots, a %d-thread workgroup "
+                     "needs more; create it with more max_rows or use a 22/26-bit width",
+                     s->slots_b, LDS_BLOCK);
   uint64_t blocks = ((N + r - 1) / (uint32_t)r + LDS_BLOCK - 1) / LDS_BLOCK;
-  const uint64_t cap = (uint64_t)s->slots_b * lscratch_words(s->label_cap) /
-                       ((uint64_t)lscratch_words(s->label_count, r) * LDS_BLOCK);
   if (blocks > cap) blocks = cap;
   if (blocks > MAX_BLOCKS) blocks = MAX_BLOCKS;
   if (blocks == 0) blocks = 1;
@@ -1241,14 +1306,20 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
   if (blocks == 0) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the multi-batch path");
   const uint64_t need_words = blocks * BLOCK * words;
   if (need_words > s->mscratch_words) {
+    // Sized for the blocks this launch runs (a 300k-row fused batch: ~293 of
+    // the 768 persistent blocks), grown when a later launch runs more.  An
+    // allocation failure is reported as CUDASP_ERR_CAPACITY before anything
+    // is queued, so launch_pipeline can fall back to the stage kernels.
     HIP_TRY(hipStreamSynchronize(st));  // no kernel of this scanner still uses the old scratch
     if (s->d_mscratch) HIP_TRY(hipFree(s->d_mscratch));
     s->d_mscratch = nullptr;
     s->mscratch_words = 0;
-    // sized for the full grid, so later calls with more rows reuse it
-    const uint64_t full = std::min<uint64_t>(full_blocks, cap_blocks) * BLOCK * words;
-    HIP_TRY(hipMalloc(&s->d_mscratch, (size_t)full * 4));
-    s->mscratch_words = full;
+    if (hipMalloc(&s->d_mscratch, (size_t)need_words * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      s->d_mscratch = nullptr;
+      return set_error(CUDASP_ERR_CAPACITY, "cannot allocate %.1f MB of k_scan_multi scratch", need_words * 4 / 1e6);
+    }
+    s->mscratch_words = need_words;
   }
   // d_multi itself is reused in stream order: launches of one scanner run on
   // one stream (include/cudasp_abi.h), so this upload lands after the
@@ -1280,8 +1351,13 @@ int launch_pipeline(cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, c
     // thread throughout, one wave per chunk
     std::vector<MultiBatch> md(1, multi_desc(tx, ty, outputs, offs, lens, n, flags, match_rows, match_count, 0));
     const uint64_t wr = (n + 63u) / 64u;
-    return launch_multi(s, md, wr, st, ROWS_A, 0, 0, (wr + ROWS_A * 4 - 1) / (ROWS_A * 4));
+    const int rc = launch_multi(s, md, wr, st, ROWS_A, 0, 0, (wr + ROWS_A * 4 - 1) / (ROWS_A * 4));
+    // CUDASP_ERR_CAPACITY: no scratch for the fused launch and nothing queued;
+    // the two stage kernels below give the same results
+    if (rc != CUDASP_ERR_CAPACITY) return rc;
   }
+  const int brc = ensure_stage_buffers(s);
+  if (brc != CUDASP_OK) return brc;
   uint32_t* t = t_out ? t_out : s->d_t;
   launch_a(s, tx, ty, n, t, st);
   HIP_TRY(hipGetLastError());
@@ -1297,6 +1373,9 @@ const char* cudasp_last_error(void) { return g_last_error.c_str(); }
 // Used by the table-function host (csrc/host) to report through the same
 // thread-local message; not part of the public header.
 void cudasp_internal_set_error(const char* msg) { g_last_error = msg ? msg : ""; }
+// The table-function host's device feeds launch each batch's copies and
+// kernels on the stream of the scanner that scans it; not public either.
+void* cudasp_internal_scanner_stream(cudasp_scanner* s) { return s ? (void*)s->stream : nullptr; }
 
 const char* cudasp_version(void) { return CUDASP_VERSION_STRING; }
 
@@ -1389,10 +1468,8 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
   } while (0)
   ALLOC(s->d_naf, naf.size());
   ALLOC(s->d_labels, labels.size() * 4);
-  ALLOC(s->d_t, (size_t)8 * max_rows * 4);
-  ALLOC(s->d_vscratch, (size_t)VSCRATCH_WORDS * s->slots_a * 4);
-  ALLOC(s->d_lscratch, (size_t)lscratch_words(label_count) * s->slots_b * 4);
 #undef ALLOC
+  // d_t / d_vscratch / d_lscratch: on first stage-kernel use (ensure_stage_buffers)
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     free_scanner(s);
@@ -1429,20 +1506,21 @@ int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32
   DeviceGuard g(s->device);
   HIP_TRY(hipStreamSynchronize(s->stream));
   if (label_count > s->label_cap) {
-    // grow the label keys and the label scratch (same slot count when it fits)
+    // grow the label keys and the label scratch (same slot count when it fits;
+    // the scratch only if the stage buffers exist yet)
     uint32_t* d_labels = nullptr;
     uint32_t* d_lscratch = nullptr;
     uint64_t words = lscratch_words(label_count);
     uint64_t cap_slots = ((1ull << 32) - 1) / (words * 4 * BLOCK) * BLOCK;
     uint32_t slots_b = (uint32_t)(s->slots_b < cap_slots ? s->slots_b : cap_slots);
     HIP_TRY(hipMalloc(&d_labels, labels.size() * 4));
-    hipError_t e = hipMalloc(&d_lscratch, (size_t)words * slots_b * 4);
+    hipError_t e = s->d_lscratch ? hipMalloc(&d_lscratch, (size_t)words * slots_b * 4) : hipSuccess;
     if (e != hipSuccess) {
       (void)hipFree(d_labels);
       return set_error(CUDASP_ERR_HIP, "hipMalloc failed: %s", hipGetErrorString(e));
     }
     (void)hipFree(s->d_labels);
-    (void)hipFree(s->d_lscratch);
+    if (s->d_lscratch) (void)hipFree(s->d_lscratch);
     s->d_labels = d_labels;
     s->d_lscratch = d_lscratch;
     s->slots_b = slots_b;
@@ -1472,7 +1550,9 @@ int cudasp_scanner_set_options(cudasp_scanner* s, const cudasp_scan_options* opt
     return set_error(CUDASP_ERR_CAPACITY, "output_count %u x capacity %u exceeds 2^32 virtual rows", K, s->capacity);
   DeviceGuard g(s->device);
   HIP_TRY(hipStreamSynchronize(s->stream));
-  if (K > s->t_cap_k) {
+  if (K > s->t_cap_k && !s->d_t) {
+    s->t_cap_k = K;  // the stage buffers do not exist yet: sized at first use
+  } else if (K > s->t_cap_k) {
     uint32_t* d_t = nullptr;
     uint8_t* d_vflags = nullptr;
     HIP_TRY(hipMalloc(&d_t, (size_t)8 * K * s->capacity * 4));
@@ -1694,6 +1774,8 @@ int cudasp_stage_shared_secret_device(cudasp_scanner* s, const uint32_t* d_tweak
   if (!d_tweak_x || !d_tweak_y || !d_t) return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
   DeviceGuard g(s->device);
+  const int brc = ensure_stage_buffers(s);
+  if (brc != CUDASP_OK) return brc;
   hipStream_t st = scanner_stream(s, stream);
   launch_a(s, d_tweak_x, d_tweak_y, n, d_t, st);
   HIP_TRY(hipGetLastError());
@@ -1709,6 +1791,8 @@ int cudasp_stage_match_device(cudasp_scanner* s, const uint32_t* d_t, const int6
     return set_error(CUDASP_ERR_INVALID_ARG, "null device buffer");
   if (n > s->capacity) return set_error(CUDASP_ERR_CAPACITY, "batch of %u rows exceeds scanner capacity %u", n, s->capacity);
   DeviceGuard g(s->device);
+  const int brc = ensure_stage_buffers(s);
+  if (brc != CUDASP_OK) return brc;
   hipStream_t st = scanner_stream(s, stream);
   bool compact = d_match_rows && d_match_count;
   return launch_match(s, d_t, n, d_outputs, d_output_offsets, d_output_lengths, d_match_flags,

@@ -88,6 +88,27 @@ class _Columns(ctypes.Structure):
     ]
 
 
+class _Stats(ctypes.Structure):
+    _fields_ = [
+        ("feeds", ctypes.c_uint32),
+        ("streams_per_feed", ctypes.c_uint32),
+        ("max_streams_per_device", ctypes.c_uint32),
+        ("hw_queues", ctypes.c_uint32),
+        ("launches", ctypes.c_uint64),
+        ("rows", ctypes.c_uint64),
+        ("harvest_wait_s", ctypes.c_double),
+    ]
+
+
+def _read_stats(lib, g, stats):
+    """Fill the dict `stats` from cudasp_tf_get_stats (after the last final)."""
+    if stats is None:
+        return
+    st = _Stats()
+    _native.check(lib.cudasp_tf_get_stats(g, ctypes.byref(st)))
+    stats.update({name: getattr(st, name) for name, _ in _Stats._fields_})
+
+
 _P = ctypes.c_void_p
 _HOST_SIGNATURES = {
     "cudasp_tf_bind": (ctypes.c_int, [ctypes.c_uint32, _BlobArg, _BlobArg, ctypes.c_int, ctypes.POINTER(_BlobArg),
@@ -110,6 +131,7 @@ _HOST_SIGNATURES = {
     "cudasp_tf_function": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Chunk)]),
     "cudasp_tf_final": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Output)]),
     "cudasp_tf_function_columns": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Columns)]),
+    "cudasp_tf_get_stats": (ctypes.c_int, [_P, ctypes.POINTER(_Stats)]),
 }
 
 _host = None
@@ -257,7 +279,8 @@ def release_pool():
 
 
 def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size=None, threads=1,
-                chunk_rows=VECTOR_SIZE, output_count=None, label_negation=None, full_x=None, assignments=None):
+                chunk_rows=VECTOR_SIZE, output_count=None, label_negation=None, full_x=None, assignments=None,
+                stats=None):
     """Run the table function over `rows` with `threads` executor threads.
     Chunks are dealt round-robin to the threads, as DuckDB's parallel scan
     would hand out morsels; each thread gets its own local state (and GPU,
@@ -265,7 +288,9 @@ def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size
     label_negation / full_x: the protocol-variant named parameters
     (cudasp_tf_bind_options); with full_x the outputs are lists of 32-byte
     x-only keys.  assignments: if a list, receives (logical GPU, HIP device)
-    of each thread's local state."""
+    of each thread's local state.  stats: if a dict, receives the query's
+    host statistics (cudasp_tf_get_stats: feeds, streams, launches, rows,
+    harvest wait)."""
     lib = _lib()
     bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size, output_count=output_count,
                       label_negation=label_negation, full_x=full_x)
@@ -314,6 +339,7 @@ def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size
             th.join()
         if errors:
             raise errors[0]
+        _read_stats(lib, g, stats)
         return results
     finally:
         for l in locals_:
@@ -395,15 +421,16 @@ def _columns(txid, height, tweak, outs):
 
 
 def cudasp_scan_arrow(data, scan_private_key, spend_public_key, label_keys, batch_size=None, threads=1,
-                      piece_rows=65536, output_count=None, label_negation=None, full_x=None):
+                      piece_rows=65536, output_count=None, label_negation=None, full_x=None, stats=None):
     """cudasp_scan over Arrow data (a pyarrow Table / RecordBatch / iterable of
     record batches, e.g. pyarrow.parquet.read_table(...) or DuckDB's
     .arrow()), with the same four columns by position.  Rows reach the
     batch buffers through cudasp_tf_function_columns (bulk copies from the
     Arrow buffers); the semantics and batches equal cudasp_scan's.  Returns a
     pyarrow Table (txid binary, height int32, tweak_key binary) in unspecified
-    row order, like the reference.  output_count / label_negation / full_x as
-    for cudasp_scan (full_x: outputs list<binary> or list<fixed_size_binary(32)>)."""
+    row order, like the reference.  output_count / label_negation / full_x /
+    stats as for cudasp_scan (full_x: outputs list<binary> or
+    list<fixed_size_binary(32)>)."""
     import pyarrow as pa
     lib = _lib()
     bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size, output_count=output_count,
@@ -449,6 +476,7 @@ def cudasp_scan_arrow(data, scan_private_key, spend_public_key, label_keys, batc
             th.join()
         if errors:
             raise errors[0]
+        _read_stats(lib, g, stats)
         return pa.table({"txid": pa.array([r[0] for r in results], pa.binary()),
                          "height": pa.array([r[1] for r in results], pa.int32()),
                          "tweak_key": pa.array([r[2] for r in results], pa.binary())})

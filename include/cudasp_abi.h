@@ -62,9 +62,13 @@ typedef struct cudasp_scanner cudasp_scanner;
  * label_count 64-byte keys back to back (may be NULL when label_count is 0).
  * max_rows bounds the rows of any later batch.  The first scanner on a device
  * also builds that device's fixed-base table for the default window width
- * (cudasp_default_fixed_base_bits: 22-bit windows, 1.5 GiB, unless the
- * environment sets CUDASP_FB_BITS=26, 21.5 GB), kept for the process; tables
- * of different devices build in parallel.
+ * (cudasp_default_fixed_base_bits: 26-bit windows, 21.5 GB, on devices with
+ * >= 128 GiB such as MI355X, else 22-bit, 1.5 GiB; CUDASP_FB_BITS=22|26 in the
+ * environment overrides), kept for the process; tables of different devices
+ * build in parallel.  Device memory of a scanner: the key constants, plus the
+ * scratch of the launches it runs (k_scan_multi: ~2 KB + 216 B per label per
+ * launched thread; the stage kernels' buffers only once a stage-kernel path
+ * runs -- the protocol variants, the values/stage entry points, the LDS width).
  * Fails with CUDASP_ERR_INVALID_ARG for a scan key that is 0 mod n. */
 int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const uint8_t spend_public_key[64],
                           const uint8_t* label_keys, uint32_t label_count, uint32_t max_rows,
@@ -84,7 +88,8 @@ int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32
  * additions fewer per row, ~1.5% faster end to end) and 7 bits (37 windows,
  * 151.5 KB, staged into each workgroup's LDS -- measured slower: 36 mixed
  * additions per row).  Same results at every width.  The process default is
- * CUDASP_FB_BITS from the environment (22 or 26), else 22.  set_fixed_base_bits (0 = the default) switches a scanner's
+ * CUDASP_FB_BITS from the environment (22 or 26), else 26 on a device with
+ * >= 128 GiB, else 22.  set_fixed_base_bits (0 = the default) switches a scanner's
  * table, building it on first use; not concurrent with work in flight on the
  * scanner.  table_bytes returns 0 for an unsupported width. */
 int cudasp_default_fixed_base_bits(void);

@@ -73,15 +73,48 @@ int cudasp_tf_bind_options(cudasp_tf_bind_data* b, int has_output_count, int64_t
 void cudasp_tf_bind_free(cudasp_tf_bind_data* b);
 uint64_t cudasp_tf_bind_batch_size(const cudasp_tf_bind_data* b);
 
-/* Global state (one per query): detects the devices. */
+/* Global state (one per query): detects the devices.
+ *
+ * Batching: every GPU (logical GPU, see below) gets one *device feed* per
+ * query -- a ring of pinned batch slots that all executor threads fill
+ * together, and 2..4 streams, each with its own scanner, that run the closed
+ * slots (H2D, transpose, one fused k_scan_multi launch, D2H of the flags).  A
+ * slot closes once it holds >= batch_size rows (the reference's trigger,
+ * src/cudasp_extension.cu:416-418, applied to a device's rows instead of one
+ * thread's) or runs out of output/txid space, and is launched by the last
+ * thread still copying into it.  The last thread to finish launches the
+ * partial slots, waits for all batches and emits the matches.  Batch
+ * composition therefore differs from the reference's per-thread batches; the
+ * emitted multiset of rows does not.
+ *
+ * A warning goes to stderr (once per process) when a query's streams on one
+ * device exceed GPU_MAX_HW_QUEUES (read from the environment; HIP's default
+ * is 4): streams sharing a hardware queue serialize their kernels. */
 int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out);
 void cudasp_tf_global_free(cudasp_tf_global* g);
 int cudasp_tf_num_gpus(const cudasp_tf_global* g);
 
-/* Local state (one per executor thread): round-robin GPU.  local_gpu is the
- * logical GPU index (0 .. num_gpus-1), local_device the HIP device it runs on
- * (the same unless the test hook CUDASP_TF_DEVICE_MAP="d0,d1,..." maps the
- * logical GPUs to devices, e.g. "0,0" for two logical GPUs on one card). */
+/* What a query's host did (for benchmarks and diagnostics; read after the
+ * last cudasp_tf_final, before cudasp_tf_global_free). */
+typedef struct {
+  uint32_t feeds;                  /* logical GPUs that received rows */
+  uint32_t streams_per_feed;       /* streams (= scanners) per device feed */
+  uint32_t max_streams_per_device; /* streams on the busiest HIP device */
+  uint32_t hw_queues;              /* GPU_MAX_HW_QUEUES seen at cudasp_tf_init (4 if unset) */
+  uint64_t launches;               /* batches launched, all feeds */
+  uint64_t rows;                   /* rows launched, all feeds */
+  double harvest_wait_s;           /* executor-thread time blocked on GPU completion */
+} cudasp_tf_stats;
+int cudasp_tf_get_stats(cudasp_tf_global* g, cudasp_tf_stats* out);
+
+/* Local state (one per executor thread).  local_gpu is the logical GPU index
+ * (0 .. num_gpus-1) assigned round-robin over threads
+ * (src/cudasp_extension.cu:523-529): the GPU of the thread's first chunk; its
+ * later chunks continue round-robin over the logical GPUs, so any number of
+ * threads feeds any number of GPUs.  local_device is the HIP device of
+ * local_gpu (the same unless the test hook CUDASP_TF_DEVICE_MAP="d0,d1,..."
+ * maps the logical GPUs to devices, e.g. "0,0,0,0" for four logical GPUs on
+ * one card, each with its own feed). */
 int cudasp_tf_local_init(cudasp_tf_global* g, cudasp_tf_local** out);
 void cudasp_tf_local_free(cudasp_tf_local* l);
 int cudasp_tf_local_gpu(const cudasp_tf_local* l);
@@ -90,9 +123,10 @@ int cudasp_tf_local_device(const cudasp_tf_local* l);
  * executor thread in the host, src/cudasp_extension.cu:523-529; a batch of
  * the table in bench.py) goes to GPU ordinal mod num_gpus.  Host-only. */
 uint32_t cudasp_assign_gpu(uint64_t ordinal, uint32_t num_gpus);
-/* The GPU state of a freed local state (scanner, stream, pinned and device
- * batch buffers) is kept in a process-wide pool (at most 64 entries) and
- * reused by later queries with the same device and batch capacity.
+/* The GPU resources of a finished query's device feeds (scanners, streams,
+ * pinned and device batch slots) are kept in a process-wide pool (at most 64
+ * entries) and reused by later queries with the same device, batch capacity
+ * and stream count; a later query only rebinds the keys.
  * cudasp_tf_release_pool frees every pooled entry; cudasp_tf_pool_size
  * reports how many are parked. */
 void cudasp_tf_release_pool(void);
@@ -124,7 +158,9 @@ typedef struct {
   const uint32_t* child_blob_size;
 } cudasp_tf_chunk;
 
-/* in_out_function: accumulate, run a batch once batch_size rows are held.
+/* in_out_function: copy the chunk's rows into a device feed (the next
+ * logical GPU of this thread's round-robin); a slot that reaches batch_size
+ * rows is launched.  May block while every slot of the feed is in flight.
  * Returns CUDASP_TF_NEED_MORE_INPUT or a negative error code (message via
  * cudasp_last_error()). */
 int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
@@ -144,8 +180,9 @@ int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp
  *            has its own offset and validity)
  * Row semantics are those of cudasp_tf_function (NULL txid/height/tweak rows
  * skipped, tweak length 64 enforced, NULL list = no outputs, NULL elements
- * dropped); rows are consumed in 2048-row pieces with the same batch trigger,
- * so batches are identical to feeding the same rows as DuckDB chunks. */
+ * dropped); rows are consumed in 2048-row pieces, each fed like one DuckDB
+ * chunk, so the results equal feeding the same rows through
+ * cudasp_tf_function. */
 typedef struct {
   uint64_t count;
   const int32_t* txid_offsets;
@@ -187,8 +224,9 @@ typedef struct {
   uint32_t tweak_size[CUDASP_TF_VECTOR_SIZE];
 } cudasp_tf_output;
 
-/* in_out_function_final: flush this thread's rows; the last thread to finish
- * emits all matches.  Returns CUDASP_TF_FINISHED (0) or
+/* in_out_function_final: the last thread to finish launches the feeds'
+ * partial slots, waits for every batch and emits all matches.  Returns
+ * CUDASP_TF_FINISHED (0) or
  * CUDASP_TF_HAVE_MORE_OUTPUT (1), or a negative error code. */
 int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l, cudasp_tf_output* out);
 

@@ -1,8 +1,8 @@
 """GPU: stage B's fixed-base window widths give identical results.
 
 The width of the t*G table is a per-scanner runtime choice
-(cudasp_scanner_set_fixed_base_bits): 22-bit windows (1.5 GiB HBM table, the
-library default), 26-bit (21.5 GB HBM) and 7-bit staged into LDS
+(cudasp_scanner_set_fixed_base_bits): 22-bit windows (1.5 GiB HBM table),
+26-bit (21.5 GB HBM, the default on MI355X) and 7-bit staged into LDS
 (k_match_lds).  All must produce the oracle's compare values and flags
 bit for bit, with labels and at a launch large enough to use the 6-rows-per-
 thread shapes."""
@@ -82,5 +82,32 @@ def test_lds_width_full_batch(torch):
             c = int(cnt.item())
             assert sorted(rows[:c].cpu().tolist()) == planted.cpu().tolist()
             res.append(flags.cpu().numpy())
+    for r in res[1:]:
+        assert (r == res[0]).all()
+
+
+@pytest.mark.parametrize("max_rows", [300, 2000])
+def test_lds_width_small_scanner(torch, max_rows):
+    """A scanner too small for one 768-thread LDS workgroup at 6 rows per
+    thread (its label scratch holds 256 / 512 slots at max_rows 300 / 2000;
+    one workgroup needs 768): the launch takes 2 rows per thread, whose slots are
+    smaller, instead of writing past the scratch.  Flags equal the HBM
+    width's; also with 6 rows per thread forced."""
+    from test_gpu_synth import _plant, synth
+    from cudasp_amd import Scanner
+    import bench
+    n = max_rows
+    x, y, outs, offs, lens = synth(torch, 9001, n)
+    planted = _plant(torch, x, y, outs, [], every=50)
+    res = []
+    with Scanner(bench.SCAN_KEY, bench.SPEND_KEY, [bench.TEST_LABEL], max_rows=n) as s:
+        for bits, rb in ((22, 0), (7, 6), (7, 0)):
+            s.set_fixed_base_bits(bits)
+            s.set_rows_per_thread(0, rb)
+            flags = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            s.scan_device(x, y, outs, offs, lens, flags)
+            s.sync()
+            res.append(flags.cpu().numpy())
+    assert sorted(np.nonzero(res[0])[0].tolist()) == planted.cpu().tolist()
     for r in res[1:]:
         assert (r == res[0]).all()

@@ -317,3 +317,58 @@ def test_many_small_batches(torch, monkeypatch):
                 assert sorted(rows[:c].cpu().tolist()) == np.nonzero(want[a:a + n])[0].tolist()
                 found += c
             assert found == int(want.sum()) > 0
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+@pytest.mark.parametrize("g1,g2", [("100000", "100000"), ("100", "0")])
+def test_multi_exceptional_label_sums(torch, monkeypatch, pipe, g1, g2):
+    """k_scan_multi -- the kernel of every default batch -- with label keys
+    that make a row's label sum exceptional inside a thread's piece: rows 5,
+    69 and 133 sit in one lane of consecutive wave-rows (one thread's piece in
+    the all-6-row regime), with L_0 = F(row 5) (the sum doubles), L_2 =
+    -F(row 69) (the sum is the point at infinity) and L_3 = F(row 133), next
+    to an ordinary label and ordinary rows.  Row 5 carries the doubled sum's
+    value and must match; row 69 carries INT64_MIN and 0 and must not (a label
+    at infinity never matches).  Pipelined and two-inversion schedules
+    (CUDASP_MULTI_PIPE), all-6-row and adaptive pieces, and the two stage
+    kernels as control: flags equal the oracle's, which follows the
+    reference's Python oracle there (scripts/compute_bip352_expected.py:42-46)."""
+    import variants as V
+    from oracle import oracle
+    monkeypatch.setenv("CUDASP_MULTI_PIPE", pipe)
+    monkeypatch.setenv("CUDASP_MULTI_G1", g1)
+    monkeypatch.setenv("CUDASP_MULTI_G2", g2)
+    n = 64 * 6 * 2 + 17
+    b = make_batch(torch, 31337, n)
+    xs = b["tweak_x"].cpu().numpy().view(np.uint32)
+    ys = b["tweak_y"].cpu().numpy().view(np.uint32)
+    tw = np.ascontiguousarray(np.concatenate([xs.T, ys.T], axis=1).astype("<u4")).view(np.uint8).reshape(n, 64)
+    ra, rb, rc = 5, 5 + 64, 5 + 128
+    F = [V.row(SCAN, SPEND, [], bytes(tw[i]))[0][0][0] for i in (ra, rb, rc)]
+    labels = [V.point_blob(F[0]), LABEL, V.point_blob(V.neg(F[1])), V.point_blob(F[2])]
+    _, vals = oracle.scan(SCAN, SPEND, labels, tw, want_values=True)
+    assert vals[rb, 3] == oracle.LABEL_INFINITY
+    outs = b["outputs"].cpu().numpy()
+    offs = b["offsets"][:n].cpu().numpy().view(np.uint32)
+    lens = b["lengths"][:n].cpu().numpy().view(np.uint32)
+    assert (lens == 2).all()
+    for i in range(n):
+        if i in (ra, rb, rc):
+            continue
+        if i % 11 == 0:
+            outs[offs[i]] = vals[i, 0]       # base
+        elif i % 9 == 0:
+            outs[offs[i] + 1] = vals[i, 2]   # the ordinary label
+    outs[offs[ra]] = vals[ra, 1]             # F + L_0 = 2F
+    outs[offs[rb]] = oracle.LABEL_INFINITY   # F + L_2 = infinity: never a match
+    outs[offs[rb] + 1] = 0
+    outs[offs[rc] + 1] = vals[rc, 4]         # F + L_3 = 2F as well
+    b["outputs"] = torch.from_numpy(outs).cuda()
+    want, _ = oracle.scan(SCAN, SPEND, labels, tw, outs, offs, lens, threads=16)
+    assert want[ra] == 1 and want[rb] == 0 and want[rc] == 1
+    got = run_multi(torch, [b], labels)[0]
+    assert (got[0] == want).all()
+    assert got[1] == np.nonzero(want)[0].tolist()
+    same([got], run_per_batch(torch, [b], labels))  # the fused single-batch launch
+    monkeypatch.setenv("CUDASP_FUSED_SINGLE", "0")
+    same([got], run_per_batch(torch, [b], labels))  # the two stage kernels

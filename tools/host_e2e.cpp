@@ -1,13 +1,31 @@
 // End-to-end rate of the table-function host (include/cudasp_host.h): a
-// synthetic columnar table in host memory is fed to T executor threads in
-// DuckDB-sized chunks (<= 2048 rows, handed out like morsels), through bind ->
-// local init -> in_out_function -> in_out_function_final, exactly the calls a
-// DuckDB executor makes (duckdb_ext/cudasp_extension.cpp).  This is the
-// PCIe-inclusive counterpart of bench.py's device-resident number (it includes
-// host accumulation, H2D of tweaks and outputs, D2H of flags and the emit).
+// synthetic table in host memory is fed to T executor threads in DuckDB-sized
+// chunks (<= 2048 rows, handed out like morsels), through bind -> local init
+// -> in_out_function -> in_out_function_final, exactly the calls a DuckDB
+// executor makes (duckdb_ext/cudasp_extension.cpp).  This is the
+// PCIe-inclusive counterpart of bench.py's device-resident number: it includes
+// the host copies into the batch slots, H2D of tweaks and outputs, D2H of the
+// flags and the emit.  The host uses every visible GPU (or the logical GPUs of
+// CUDASP_TF_DEVICE_MAP).
 //
-//   host_e2e [rows] [threads] [batch_size] [labels] [outputs_per_row]
-// Prints one JSON line.
+// The table is bench.py's: T_g = (s0 + g) G, txid = BE64(g)
+// padded to 32 bytes, height 800000 + g / 4000, outputs from the library's
+// own generators (cudasp_synth_outputs: k per row; cudasp_synth_output_lengths
+// / _values: 1..kmax per row, mean (kmax + 1) / 2).  Planted matches: the
+// true base value on every row g = 0 mod 1000 and, with L labels, label
+// j = (g / 1000) mod L's value on row g = 1 mod 1000 (every label index of
+// the reference's label loop, src/cudasp_gpu.cu:153-172), computed by the
+// product's values path (which the test suite pins to the oracle), written
+// into the first slot of the row's outputs list.  A query passes when the
+// emitted rows are exactly the planted ones (decoded from the txids).
+//
+//   host_e2e [--rows N] [--threads T] [--batch B] [--labels L --labels-file F]
+//            [--outputs K | --outputs-max KMAX] [--input rows|columns]
+//            [--reps R]
+// Label keys: F holds L 64-byte keys (x || y, little-endian, bench.label_keys);
+// without F, L must be 0 or 1 (the SQL test's label, test/sql/cudasp.test:104).
+// Prints one JSON line; exit 0 iff every timed query emitted exactly the
+// planted rows.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -16,6 +34,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -27,19 +46,14 @@ static const char* SPEND_HEX =
     "36cf8fcd4d4890ab6c1083aeb5b50c260c20acda7839120e3575836f6d85c95ce0d705e31ff9fdcce67a8f3598871c6dfbe6bcde8a51cb7b48b0f95be0ea94de";
 static const char* LABEL_HEX =
     "cd63f9212a2deebde8a71e9ea23f6f958c47c41d2ed74b9617fe6fb554d1524e292fabddbdcbb643eafc328875c46d75a1d697b2b31c42d38aa93f85eab34bc1";
-// SHA256("cudasp-synth-v1") mod n, little-endian (same s0 as bench.py)
-static void synth_s0(uint8_t out[32]);
+// int.from_bytes(sha256(b"cudasp-synth-v1"), "big") % n, little-endian (bench.synth_s0)
+static const char* S0_LE_HEX = "f59571862b00db0109281d9bf2326d7eaf05b1b837ccafce4c2e335f439cf6ab";
+static const uint64_t OUTPUT_SEED = 0xC0DA5EEDull;
+static const uint64_t PLANT_EVERY = 1000;
 
 static void hex2bin(const char* h, uint8_t* out) {
   size_t n = strlen(h) / 2;
   for (size_t i = 0; i < n; i++) sscanf(h + 2 * i, "%2hhx", &out[i]);
-}
-
-static uint64_t splitmix64(uint64_t z) {
-  z += 0x9e3779b97f4a7c15ull;
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  return z ^ (z >> 31);
 }
 
 #define CK(x)                                                                             \
@@ -59,237 +73,381 @@ static uint64_t splitmix64(uint64_t z) {
     }                                                                                     \
   } while (0)
 
-int main(int argc, char** argv) {
-  // As the DuckDB extension does when it loads (duckdb_ext/cudasp_extension.cpp):
-  // 16 hardware queues unless the environment sets a value; before any HIP call.
-  setenv("GPU_MAX_HW_QUEUES", "16", 0);
-  uint64_t rows = argc > 1 ? strtoull(argv[1], 0, 10) : 32700000ull;
-  int threads = argc > 2 ? atoi(argv[2]) : 16;
-  int64_t batch = argc > 3 ? atoll(argv[3]) : 300000;
-  int nlabels = argc > 4 ? atoi(argv[4]) : 0;
-  int k = argc > 5 ? atoi(argv[5]) : 2;
-  // "rows": DuckDB-style 2048-row chunks of per-row pointers (cudasp_tf_function);
-  // "columns": Arrow-layout column runs (cudasp_tf_function_columns).
-  const bool columnar = argc > 6 && strcmp(argv[6], "columns") == 0;
-  uint8_t scan[32], spend[64], label[64];
-  hex2bin(SCAN_HEX, scan);
-  hex2bin(SPEND_HEX, spend);
-  hex2bin(LABEL_HEX, label);
-  std::vector<uint8_t> labels;
-  for (int j = 0; j < nlabels; j++) labels.insert(labels.end(), label, label + 64);  // same key repeated
+struct Args {
+  uint64_t rows = 32700000ull;
+  int threads = 8;
+  int64_t batch = 300000;
+  int labels = 0;
+  std::string labels_file;
+  int k = 2;     // fixed outputs per row
+  int kmax = 0;  // > 0: 1..kmax outputs per row
+  bool columnar = false;
+  int reps = 1;
+};
 
-  // ---------------- synthetic table (generation not timed) -----------------
-  auto g0 = std::chrono::steady_clock::now();
-  std::vector<uint8_t> tweaks(rows * 64);
-  std::vector<uint8_t> txids(rows * 32, 0);
-  std::vector<int32_t> heights(rows);
-  std::vector<int64_t> outputs(rows * (uint64_t)k);
-  std::vector<uint64_t> list_off(rows), list_len(rows, (uint64_t)k);
-  // Arrow-layout offsets for the columnar mode (int32, rows + 1 entries)
-  std::vector<int32_t> txid_offsets(rows + 1), list_off32(rows + 1);
-  for (uint64_t i = 0; i <= rows; i++) {
-    txid_offsets[i] = (int32_t)(i * 32);
-    list_off32[i] = (int32_t)(i * k);
+static Args parse(int argc, char** argv) {
+  Args a;
+  for (int i = 1; i < argc; i++) {
+    std::string s = argv[i];
+    auto val = [&]() -> const char* {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "%s needs a value\n", s.c_str());
+        exit(1);
+      }
+      return argv[++i];
+    };
+    if (s == "--rows") a.rows = strtoull(val(), 0, 10);
+    else if (s == "--threads") a.threads = atoi(val());
+    else if (s == "--batch") a.batch = atoll(val());
+    else if (s == "--labels") a.labels = atoi(val());
+    else if (s == "--labels-file") a.labels_file = val();
+    else if (s == "--outputs") a.k = atoi(val());
+    else if (s == "--outputs-max") a.kmax = atoi(val());
+    else if (s == "--input") a.columnar = std::string(val()) == "columns";
+    else if (s == "--reps") a.reps = std::max(1, atoi(val()));
+    else {
+      fprintf(stderr, "unknown argument %s\n", s.c_str());
+      exit(1);
+    }
   }
+  if (a.threads < 1 || a.rows == 0 || (a.kmax == 0 && a.k < 1) || a.kmax < 0 || a.labels < 0) {
+    fprintf(stderr, "bad arguments\n");
+    exit(1);
+  }
+  return a;
+}
+
+struct Table {
+  uint64_t rows = 0;
+  std::vector<uint8_t> tweaks, txids;
+  std::vector<int32_t> heights;
+  std::vector<int64_t> outputs;
+  std::vector<uint64_t> list_off, list_len;         // rows-mode list entries
+  std::vector<int32_t> txid_offsets, list_off32;    // Arrow offsets (rows + 1)
+  std::vector<uint64_t> planted;                    // planted row indices, sorted
+  uint32_t labels_planted_mask = 0;                 // label indices planted (bit j)
+};
+
+static void generate(const Args& a, const uint8_t scan[32], const uint8_t spend[64],
+                     const std::vector<uint8_t>& labels, Table& t) {
+  const uint64_t rows = t.rows = a.rows;
+  t.tweaks.resize(rows * 64);
+  t.txids.assign(rows * 32, 0);
+  t.heights.resize(rows);
+  t.list_off.resize(rows);
+  t.list_len.resize(rows);
   uint8_t s0[32];
-  synth_s0(s0);
+  hex2bin(S0_LE_HEX, s0);
   const uint32_t chunk = 1u << 22;
-  uint32_t *d_x, *d_y;
-  int64_t* d_vals;
+  const uint32_t kcap = a.kmax ? (uint32_t)a.kmax : (uint32_t)a.k;
+  uint32_t *d_x, *d_y, *d_offs, *d_lens;
+  int64_t* d_outs;
   HK(hipMalloc(&d_x, (size_t)chunk * 32));
   HK(hipMalloc(&d_y, (size_t)chunk * 32));
-  std::vector<uint32_t> hx((size_t)chunk * 8), hy((size_t)chunk * 8);
+  HK(hipMalloc(&d_offs, (size_t)chunk * 4));
+  HK(hipMalloc(&d_lens, (size_t)chunk * 4));
+  HK(hipMalloc(&d_outs, (size_t)chunk * kcap * 8));
+  std::vector<uint32_t> hx((size_t)chunk * 8), hy((size_t)chunk * 8), hl(chunk), ho(chunk);
+  t.outputs.reserve(a.kmax ? rows * (a.kmax + 1) / 2 + rows / 8 : rows * a.k);
   for (uint64_t base = 0; base < rows; base += chunk) {
-    uint32_t m = (uint32_t)std::min<uint64_t>(chunk, rows - base);
+    const uint32_t m = (uint32_t)std::min<uint64_t>(chunk, rows - base);
     CK(cudasp_synth_tweak_columns(0, s0, base, m, d_x, d_y, nullptr));
+    if (a.kmax) {
+      CK(cudasp_synth_output_lengths(OUTPUT_SEED, base, m, (uint32_t)a.kmax, d_lens, nullptr));
+      HK(hipDeviceSynchronize());
+      HK(hipMemcpy(hl.data(), d_lens, (size_t)m * 4, hipMemcpyDeviceToHost));
+      uint32_t acc = 0;
+      for (uint32_t i = 0; i < m; i++) {
+        ho[i] = acc;
+        acc += hl[i];
+      }
+      HK(hipMemcpy(d_offs, ho.data(), (size_t)m * 4, hipMemcpyHostToDevice));
+      CK(cudasp_synth_output_values(OUTPUT_SEED, base, m, d_offs, d_lens, d_outs, nullptr));
+    } else {
+      CK(cudasp_synth_outputs(OUTPUT_SEED, base, m, (uint32_t)a.k, d_outs, d_offs, d_lens, nullptr));
+      HK(hipDeviceSynchronize());
+      HK(hipMemcpy(hl.data(), d_lens, (size_t)m * 4, hipMemcpyDeviceToHost));
+      HK(hipMemcpy(ho.data(), d_offs, (size_t)m * 4, hipMemcpyDeviceToHost));
+    }
     HK(hipDeviceSynchronize());
     HK(hipMemcpy(hx.data(), d_x, (size_t)m * 32, hipMemcpyDeviceToHost));
     HK(hipMemcpy(hy.data(), d_y, (size_t)m * 32, hipMemcpyDeviceToHost));
+    const uint64_t nouts = (uint64_t)ho[m - 1] + hl[m - 1];
+    const size_t out0 = t.outputs.size();
+    t.outputs.resize(out0 + nouts);
+    HK(hipMemcpy(t.outputs.data() + out0, d_outs, nouts * 8, hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < m; i++) {
-      uint32_t* row = (uint32_t*)(tweaks.data() + (base + i) * 64);
+      const uint64_t g = base + i;
+      uint32_t* row = (uint32_t*)(t.tweaks.data() + g * 64);
       for (int j = 0; j < 8; j++) {
         row[j] = hx[(size_t)j * m + i];
         row[8 + j] = hy[(size_t)j * m + i];
       }
+      for (int b = 0; b < 8; b++) t.txids[g * 32 + 31 - b] = (uint8_t)(g >> (8 * b));
+      t.heights[g] = 800000 + (int32_t)(g / 4000);
+      t.list_off[g] = out0 + ho[i];
+      t.list_len[g] = hl[i];
     }
   }
-  for (uint64_t i = 0; i < rows; i++) {
-    for (int b = 0; b < 8; b++) txids[i * 32 + 31 - b] = (uint8_t)(i >> (8 * b));
-    heights[i] = 800000 + (int32_t)(i / 4000);
-    list_off[i] = i * k;
-    for (int j = 0; j < k; j++) outputs[i * k + j] = (int64_t)splitmix64(0xC0DA5EEDull ^ (i * k + j));
+  HK(hipFree(d_x));
+  HK(hipFree(d_y));
+  HK(hipFree(d_offs));
+  HK(hipFree(d_lens));
+  HK(hipFree(d_outs));
+  if (t.outputs.size() >= (1ull << 31) || rows >= (1ull << 31) / 32) {
+    fprintf(stderr, "table too large for int32 Arrow offsets\n");
+    exit(1);
   }
-  // plant the true base value on every 1000th row (computed by the kernels)
-  uint64_t planted = 0;
-  {
-    cudasp_scanner* sc;
-    std::vector<uint64_t> idx;
-    for (uint64_t i = 0; i < rows; i += 1000) idx.push_back(i);
-    uint32_t m = (uint32_t)idx.size();
-    CK(cudasp_scanner_create(0, scan, spend, labels.data(), nlabels, m, &sc));
-    std::vector<uint32_t> px((size_t)m * 8), py((size_t)m * 8);
-    for (uint32_t r = 0; r < m; r++) {
-      const uint32_t* row = (const uint32_t*)(tweaks.data() + idx[r] * 64);
-      for (int j = 0; j < 8; j++) {
-        px[(size_t)j * m + r] = row[j];
-        py[(size_t)j * m + r] = row[8 + j];
-      }
-    }
-    uint32_t *dpx, *dpy, *dt;
-    HK(hipMalloc(&dpx, (size_t)m * 32));
-    HK(hipMalloc(&dpy, (size_t)m * 32));
-    HK(hipMalloc(&dt, (size_t)m * 32));
-    HK(hipMalloc(&d_vals, (size_t)m * 8 * (1 + nlabels)));
-    HK(hipMemcpy(dpx, px.data(), (size_t)m * 32, hipMemcpyHostToDevice));
-    HK(hipMemcpy(dpy, py.data(), (size_t)m * 32, hipMemcpyHostToDevice));
-    CK(cudasp_row_values_device(sc, dpx, dpy, m, dt, d_vals, nullptr));
-    CK(cudasp_scanner_sync(sc));
-    std::vector<int64_t> vals(m);
-    HK(hipMemcpy(vals.data(), d_vals, (size_t)m * 8, hipMemcpyDeviceToHost));
-    for (uint32_t r = 0; r < m; r++) outputs[idx[r] * k] = vals[r];
-    planted = m;
-    cudasp_scanner_destroy(sc);
+  t.txid_offsets.resize(rows + 1);
+  t.list_off32.resize(rows + 1);
+  for (uint64_t i = 0; i <= rows; i++) {
+    t.txid_offsets[i] = (int32_t)(i * 32);
+    t.list_off32[i] = (int32_t)(i < rows ? t.list_off[i] : t.outputs.size());
   }
-  double gen_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - g0).count();
 
-  // ---------------- the query --------------------------------------------
-  char stats[512] = "";
-  auto run = [&](double* secs, uint64_t* found) {
-    cudasp_tf_blob_arg a_scan{scan, 32, 1}, a_spend{spend, 64, 1};
-    std::vector<cudasp_tf_blob_arg> a_lab(nlabels);
-    for (int j = 0; j < nlabels; j++) a_lab[j] = {labels.data() + 64 * j, 64, 1};
-    cudasp_tf_bind_data* bd;
-    char err[512];
-    if (cudasp_tf_bind(4, a_scan, a_spend, 1, a_lab.data(), nlabels, 1, 1, batch, &bd, err, sizeof(err)) != 0) {
-      fprintf(stderr, "bind: %s\n", err);
-      exit(1);
+  // ---- planted values: base on g = 0 mod 1000, label j on g = 1 mod 1000
+  const int L = a.labels;
+  std::vector<uint64_t> idx;
+  std::vector<int> lab;  // -1 = base, else label index
+  for (uint64_t g = 0; g < rows; g += PLANT_EVERY) {
+    idx.push_back(g);
+    lab.push_back(-1);
+    if (L && g + 1 < rows) {
+      idx.push_back(g + 1);
+      lab.push_back((int)((g / PLANT_EVERY) % L));
     }
-    cudasp_tf_global* gs;
-    CK(cudasp_tf_init(bd, &gs));
-    std::vector<cudasp_tf_local*> ls(threads);
-    for (int t = 0; t < threads; t++) CK(cudasp_tf_local_init(gs, &ls[t]));
-    std::atomic<uint64_t> next{0};
-    std::atomic<uint64_t> emitted{0};
-    // per thread: seconds inside the table-function calls, inside final (the
-    // last batch and the wait for it), and until the thread is done
-    std::vector<double> t_calls(threads, 0.0), t_final(threads, 0.0), t_done(threads, 0.0), t_long(threads, 0.0);
-    auto t0 = std::chrono::steady_clock::now();
-    auto now_s = [&t0]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
-    std::vector<std::thread> th;
-    for (int t = 0; t < threads && columnar; t++) {
-      th.emplace_back([&, t]() {
+  }
+  const uint32_t m = (uint32_t)idx.size();
+  cudasp_scanner* sc;
+  CK(cudasp_scanner_create(0, scan, spend, L ? labels.data() : nullptr, (uint32_t)L, m, &sc));
+  std::vector<uint32_t> px((size_t)m * 8), py((size_t)m * 8);
+  for (uint32_t r = 0; r < m; r++) {
+    const uint32_t* row = (const uint32_t*)(t.tweaks.data() + idx[r] * 64);
+    for (int j = 0; j < 8; j++) {
+      px[(size_t)j * m + r] = row[j];
+      py[(size_t)j * m + r] = row[8 + j];
+    }
+  }
+  uint32_t *dpx, *dpy, *dt;
+  int64_t* dv;
+  HK(hipMalloc(&dpx, (size_t)m * 32));
+  HK(hipMalloc(&dpy, (size_t)m * 32));
+  HK(hipMalloc(&dt, (size_t)m * 32));
+  HK(hipMalloc(&dv, (size_t)m * 8 * (1 + L)));
+  HK(hipMemcpy(dpx, px.data(), (size_t)m * 32, hipMemcpyHostToDevice));
+  HK(hipMemcpy(dpy, py.data(), (size_t)m * 32, hipMemcpyHostToDevice));
+  CK(cudasp_row_values_device(sc, dpx, dpy, m, dt, dv, nullptr));
+  CK(cudasp_scanner_sync(sc));
+  std::vector<int64_t> vals((size_t)m * (1 + L));
+  HK(hipMemcpy(vals.data(), dv, vals.size() * 8, hipMemcpyDeviceToHost));
+  for (uint32_t r = 0; r < m; r++) {
+    const int v = lab[r] < 0 ? 0 : 1 + lab[r];  // values row: 0 = base, 1 + j = label j
+    t.outputs[t.list_off[idx[r]]] = vals[(size_t)v * m + r];
+    if (lab[r] >= 0) t.labels_planted_mask |= 1u << (lab[r] & 31);
+  }
+  t.planted = idx;
+  std::sort(t.planted.begin(), t.planted.end());
+  HK(hipFree(dpx));
+  HK(hipFree(dpy));
+  HK(hipFree(dt));
+  HK(hipFree(dv));
+  cudasp_scanner_destroy(sc);
+}
+
+struct QueryResult {
+  double secs = 0;
+  uint64_t emitted = 0;
+  bool exact = false;  // emitted rows == planted rows
+  cudasp_tf_stats stats{};
+  double call_s_mean = 0, final_s_mean = 0, done_min = 0, done_max = 0;
+};
+
+static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_t spend[64],
+                             const std::vector<uint8_t>& labels, const Table& t) {
+  const int L = a.labels, T = a.threads;
+  const uint64_t rows = t.rows;
+  cudasp_tf_blob_arg a_scan{scan, 32, 1}, a_spend{spend, 64, 1};
+  std::vector<cudasp_tf_blob_arg> a_lab(std::max(1, L));
+  for (int j = 0; j < L; j++) a_lab[j] = {labels.data() + 64 * j, 64, 1};
+  cudasp_tf_bind_data* bd;
+  char err[512];
+  if (cudasp_tf_bind(4, a_scan, a_spend, 1, a_lab.data(), (uint32_t)L, 1, 1, a.batch, &bd, err, sizeof(err)) != 0) {
+    fprintf(stderr, "bind: %s\n", err);
+    exit(1);
+  }
+  cudasp_tf_global* gs;
+  CK(cudasp_tf_init(bd, &gs));
+  std::vector<cudasp_tf_local*> ls(T);
+  for (int i = 0; i < T; i++) CK(cudasp_tf_local_init(gs, &ls[i]));
+  std::atomic<uint64_t> next{0};
+  std::vector<uint64_t> got;  // emitted row indices (from the txids)
+  std::vector<double> t_calls(T, 0.0), t_final(T, 0.0), t_done(T, 0.0);
+  const auto t0 = std::chrono::steady_clock::now();
+  auto now_s = [&t0]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+  auto finish = [&](int th) {
+    const double f0 = now_s();
+    cudasp_tf_output* out = new cudasp_tf_output;
+    for (;;) {
+      const int rc = cudasp_tf_final(bd, gs, ls[th], out);
+      CK(rc);
+      for (uint32_t i = 0; i < out->count; i++) {
+        uint64_t g = 0;
+        for (int b = 0; b < 8; b++) g |= (uint64_t)out->txid_data[i][31 - b] << (8 * b);
+        got.push_back(g);  // only the output thread gets here
+      }
+      if (rc != CUDASP_TF_HAVE_MORE_OUTPUT) break;
+    }
+    delete out;
+    t_final[th] = now_s() - f0;
+    t_done[th] = now_s();
+  };
+  std::vector<std::thread> th;
+  for (int i = 0; i < T; i++) {
+    th.emplace_back([&, i]() {
+      if (a.columnar) {
         const uint64_t piece = 65536;
         for (;;) {
-          uint64_t c0 = next.fetch_add(piece);
+          const uint64_t c0 = next.fetch_add(piece);
           if (c0 >= rows) break;
           cudasp_tf_columns c{};
           c.count = std::min<uint64_t>(piece, rows - c0);
-          c.txid_offsets = txid_offsets.data();
-          c.txid_data = txids.data();
+          c.txid_offsets = t.txid_offsets.data();
+          c.txid_data = t.txids.data();
           c.txid_offset = c0;
-          c.height = heights.data();
+          c.height = t.heights.data();
           c.height_offset = c0;
-          c.tweak_data = tweaks.data();
+          c.tweak_data = t.tweaks.data();
           c.tweak_fixed_width = 64;
           c.tweak_offset = c0;
-          c.list_offsets = list_off32.data();
+          c.list_offsets = t.list_off32.data();
           c.list_offset = c0;
-          c.child_values = outputs.data();
-          const double c0s = now_s();
-          CK(cudasp_tf_function_columns(bd, gs, ls[t], &c));
-          const double dt = now_s() - c0s;
-          t_calls[t] += dt;
-          if (dt > 5e-4) t_long[t] += dt;  // calls that launched a batch / waited for one
+          c.child_values = t.outputs.data();
+          const double s = now_s();
+          CK(cudasp_tf_function_columns(bd, gs, ls[i], &c));
+          t_calls[i] += now_s() - s;
         }
-        const double f0s = now_s();
-        cudasp_tf_output* out = new cudasp_tf_output;
-        for (;;) {
-          int rc = cudasp_tf_final(bd, gs, ls[t], out);
-          CK(rc);
-          emitted += out->count;
-          if (rc != CUDASP_TF_HAVE_MORE_OUTPUT) break;
-        }
-        delete out;
-        t_final[t] = now_s() - f0s;
-        t_done[t] = now_s();
-      });
-    }
-    for (int t = 0; t < threads && !columnar; t++) {
-      th.emplace_back([&, t]() {
+      } else {
         std::vector<const uint8_t*> txp(CUDASP_TF_VECTOR_SIZE), twp(CUDASP_TF_VECTOR_SIZE);
         std::vector<uint32_t> txs(CUDASP_TF_VECTOR_SIZE, 32), tws(CUDASP_TF_VECTOR_SIZE, 64);
         std::vector<uint64_t> loff(CUDASP_TF_VECTOR_SIZE);
         for (;;) {
-          uint64_t c0 = next.fetch_add(CUDASP_TF_VECTOR_SIZE);
+          const uint64_t c0 = next.fetch_add(CUDASP_TF_VECTOR_SIZE);
           if (c0 >= rows) break;
-          uint32_t cnt = (uint32_t)std::min<uint64_t>(CUDASP_TF_VECTOR_SIZE, rows - c0);
-          for (uint32_t i = 0; i < cnt; i++) {
-            txp[i] = txids.data() + (c0 + i) * 32;
-            twp[i] = tweaks.data() + (c0 + i) * 64;
-            loff[i] = list_off[c0 + i] - list_off[c0];
+          const uint32_t cnt = (uint32_t)std::min<uint64_t>(CUDASP_TF_VECTOR_SIZE, rows - c0);
+          for (uint32_t r = 0; r < cnt; r++) {
+            txp[r] = t.txids.data() + (c0 + r) * 32;
+            twp[r] = t.tweaks.data() + (c0 + r) * 64;
+            loff[r] = t.list_off[c0 + r] - t.list_off[c0];
           }
           cudasp_tf_chunk c{};
           c.count = cnt;
           c.txid_data = txp.data();
           c.txid_size = txs.data();
-          c.height = heights.data() + c0;
+          c.height = t.heights.data() + c0;
           c.tweak_data = twp.data();
           c.tweak_size = tws.data();
           c.list_offset = loff.data();
-          c.list_length = list_len.data() + c0;
-          c.child_values = outputs.data() + list_off[c0];
-          const double c0s = now_s();
-          CK(cudasp_tf_function(bd, gs, ls[t], &c));
-          const double dt = now_s() - c0s;
-          t_calls[t] += dt;
-          if (dt > 5e-4) t_long[t] += dt;  // calls that launched a batch / waited for one
+          c.list_length = t.list_len.data() + c0;
+          c.child_values = t.outputs.data() + t.list_off[c0];
+          const double s = now_s();
+          CK(cudasp_tf_function(bd, gs, ls[i], &c));
+          t_calls[i] += now_s() - s;
         }
-        const double f0s = now_s();
-        cudasp_tf_output* out = new cudasp_tf_output;
-        for (;;) {
-          int rc = cudasp_tf_final(bd, gs, ls[t], out);
-          CK(rc);
-          emitted += out->count;
-          if (rc != CUDASP_TF_HAVE_MORE_OUTPUT) break;
-        }
-        delete out;
-        t_final[t] = now_s() - f0s;
-        t_done[t] = now_s();
-      });
-    }
-    for (auto& x : th) x.join();
-    *secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    *found = emitted.load();
-    auto mean = [](const std::vector<double>& v) { double a = 0; for (double x : v) a += x; return a / v.size(); };
-    snprintf(stats, sizeof(stats),
-             "\"thread_call_s_mean\": %.4f, \"thread_long_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
-             "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f",
-             mean(t_calls), mean(t_long), mean(t_final), *std::min_element(t_done.begin(), t_done.end()),
-             *std::max_element(t_done.begin(), t_done.end()));
-    for (auto* l : ls) cudasp_tf_local_free(l);
-    cudasp_tf_global_free(gs);
-    cudasp_tf_bind_free(bd);
+      }
+      finish(i);
+    });
+  }
+  for (auto& x : th) x.join();
+  QueryResult q;
+  q.secs = now_s();
+  CK(cudasp_tf_get_stats(gs, &q.stats));
+  for (auto* l : ls) cudasp_tf_local_free(l);
+  cudasp_tf_global_free(gs);
+  cudasp_tf_bind_free(bd);
+  q.emitted = got.size();
+  std::sort(got.begin(), got.end());
+  q.exact = got == t.planted;
+  auto mean = [](const std::vector<double>& v) {
+    double s = 0;
+    for (double x : v) s += x;
+    return s / v.size();
   };
-  double warm_s;
-  uint64_t warm_found;
-  run(&warm_s, &warm_found);  // warm-up (scanner creation, table build)
-  double secs;
-  uint64_t found;
-  run(&secs, &found);
-  printf("{\"what\": \"table-function host end-to-end (host memory -> matches, PCIe-inclusive)\", \"input\": \"%s\", "
-         "\"rows\": %llu, \"threads\": %d, \"batch_size\": %lld, \"labels\": %d, \"outputs_per_row\": %d, "
-         "\"seconds\": %.4f, \"tx_per_s\": %.1f, \"matches\": %llu, \"planted\": %llu, \"warmup_seconds\": %.3f, "
-         "\"generate_seconds\": %.2f, \"devices\": %d, \"gpu_max_hw_queues\": \"%s\", %s}\n",
-         columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)rows, threads, (long long)batch, nlabels,
-         k, secs, rows / secs,
-         (unsigned long long)found, (unsigned long long)planted, warm_s, gen_s, cudasp_device_count(),
-         getenv("GPU_MAX_HW_QUEUES") ? getenv("GPU_MAX_HW_QUEUES") : "", stats);
-  return found == planted ? 0 : 2;
+  q.call_s_mean = mean(t_calls);
+  q.final_s_mean = mean(t_final);
+  q.done_min = *std::min_element(t_done.begin(), t_done.end());
+  q.done_max = *std::max_element(t_done.begin(), t_done.end());
+  return q;
 }
 
-// SHA-256 of "cudasp-synth-v1" reduced mod n (precomputed by bench.py's formula).
-static void synth_s0(uint8_t out[32]) {
-  // int.from_bytes(sha256(b"cudasp-synth-v1"), "big") % n, little-endian
-  static const char* S0_LE_HEX = "f59571862b00db0109281d9bf2326d7eaf05b1b837ccafce4c2e335f439cf6ab";
-  hex2bin(S0_LE_HEX, out);
+int main(int argc, char** argv) {
+  const Args a = parse(argc, argv);
+  uint8_t scan[32], spend[64];
+  hex2bin(SCAN_HEX, scan);
+  hex2bin(SPEND_HEX, spend);
+  std::vector<uint8_t> labels;
+  if (!a.labels_file.empty()) {
+    FILE* fp = fopen(a.labels_file.c_str(), "rb");
+    if (!fp) {
+      fprintf(stderr, "cannot open %s\n", a.labels_file.c_str());
+      return 1;
+    }
+    labels.resize((size_t)64 * a.labels);
+    const size_t got = fread(labels.data(), 1, labels.size(), fp);
+    fclose(fp);
+    if (got != labels.size()) {
+      fprintf(stderr, "%s: %zu bytes, %zu expected for %d labels\n", a.labels_file.c_str(), got, labels.size(),
+              a.labels);
+      return 1;
+    }
+  } else if (a.labels == 1) {
+    labels.resize(64);
+    hex2bin(LABEL_HEX, labels.data());
+  } else if (a.labels > 1) {
+    fprintf(stderr, "--labels %d needs --labels-file (bench.label_keys)\n", a.labels);
+    return 1;
+  }
+
+  const auto g0 = std::chrono::steady_clock::now();
+  Table t;
+  generate(a, scan, spend, labels, t);
+  const double gen_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - g0).count();
+
+  const QueryResult warm = run_query(a, scan, spend, labels, t);  // scanners, slots, tables
+  std::vector<QueryResult> qs;
+  for (int r = 0; r < a.reps; r++) qs.push_back(run_query(a, scan, spend, labels, t));
+  std::vector<double> secs;
+  bool all_exact = warm.exact;
+  for (const auto& q : qs) {
+    secs.push_back(q.secs);
+    all_exact = all_exact && q.exact;
+  }
+  std::vector<double> sorted = secs;
+  std::sort(sorted.begin(), sorted.end());
+  const double med = sorted[sorted.size() / 2];
+  const QueryResult& q = qs[std::find(secs.begin(), secs.end(), med) - secs.begin()];
+  std::string all = "[";
+  for (size_t i = 0; i < secs.size(); i++) all += (i ? ", " : "") + std::to_string(secs[i]);
+  all += "]";
+  int planted_labels = 0;
+  for (int j = 0; j < 32; j++) planted_labels += (t.labels_planted_mask >> j) & 1;
+  const char* hq = getenv("GPU_MAX_HW_QUEUES");
+  printf("{\"what\": \"table-function host end-to-end (host memory -> matches, PCIe-inclusive)\", \"input\": \"%s\", "
+         "\"rows\": %llu, \"threads\": %d, \"batch_size\": %lld, \"labels\": %d, \"outputs_per_row\": %s, "
+         "\"outputs_total\": %llu, \"reps\": %d, \"seconds\": %.5f, \"seconds_all\": %s, \"seconds_min\": %.5f, "
+         "\"tx_per_s\": %.1f, \"matches\": %llu, \"planted\": %llu, \"label_indices_planted\": %d, "
+         "\"emitted_equal_planted\": %s, \"warmup_seconds\": %.3f, \"generate_seconds\": %.2f, \"devices\": %d, "
+         "\"feeds\": %u, \"streams_per_feed\": %u, \"max_streams_per_device\": %u, \"gpu_max_hw_queues\": %u, "
+         "\"gpu_max_hw_queues_env\": \"%s\", \"launches\": %llu, \"rows_per_launch\": %.0f, "
+         "\"harvest_wait_s\": %.4f, \"thread_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
+         "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f}\n",
+         a.columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)t.rows, a.threads, (long long)a.batch,
+         a.labels,
+         a.kmax ? ("\"1.." + std::to_string(a.kmax) + "\"").c_str() : std::to_string(a.k).c_str(),
+         (unsigned long long)t.outputs.size(), a.reps, med, all.c_str(), sorted[0], t.rows / med,
+         (unsigned long long)q.emitted, (unsigned long long)t.planted.size(), planted_labels,
+         all_exact ? "true" : "false", warm.secs, gen_s, cudasp_device_count(), q.stats.feeds,
+         q.stats.streams_per_feed, q.stats.max_streams_per_device, q.stats.hw_queues, hq ? hq : "",
+         (unsigned long long)q.stats.launches, q.stats.launches ? (double)q.stats.rows / q.stats.launches : 0.0,
+         q.stats.harvest_wait_s, q.call_s_mean, q.final_s_mean, q.done_min, q.done_max);
+  return all_exact ? 0 : 2;
 }
