@@ -26,8 +26,9 @@
 //         the devices round-robin (chunk c of thread t to logical GPU
 //         (t + c) mod num_gpus), so any thread count feeds any GPU count; a
 //         thread's "assigned GPU" (:523-529) is where its chunks start;
-//       - the streams in flight per device are the feed's (at most 4: the
-//         HIP runtime's default GPU_MAX_HW_QUEUES), not one per thread.
+//       - the streams in flight per device are the feed's (2 to 4, within
+//         the hardware queues HIP gives the process: 3 at the default
+//         GPU_MAX_HW_QUEUES = 4), not one per thread.
 //     Batch composition therefore differs from the reference; the emitted
 //     rows (a multiset -- the reference's order is unspecified) do not.
 //   * Flat columns instead of two heap strings per row (:202-204), no host
@@ -129,16 +130,24 @@ struct DeviceSet {
 };
 
 // Streams (= scanners) of a device feed: enough 4-row-per-thread launches of
-// batch_size rows in flight to cover the GPU's wave slots, 2 to 4
-// (CUDASP_TF_STREAMS = 1..4 overrides).
-int feed_streams_for(uint64_t batch_size) {
+// batch_size rows in flight to cover the GPU's wave slots (plus one for a
+// slot being refilled), 2 to 4 -- but no more than the hardware queues the
+// HIP runtime gives the feed: a process's streams on a device share
+// GPU_MAX_HW_QUEUES queues (4 by default), one of them taken by the null
+// stream, and kernels of streams that share a queue run one after another
+// (measured: 4 streams at 4 queues map onto 3 queues, 132 M tx/s end to end;
+// 3 streams, 158 M).  feeds_on_device: feeds of this query on the same HIP
+// device (CUDASP_TF_DEVICE_MAP).  CUDASP_TF_STREAMS = 1..4 overrides.
+int feed_streams_for(uint64_t batch_size, int hw_queues, int feeds_on_device) {
   if (const char* e = getenv("CUDASP_TF_STREAMS")) {
     const int v = atoi(e);
     if (v >= 1 && v <= FEED_MAX_STREAMS) return v;
   }
-  // launches that fill the GPU, plus one to cover a slot being refilled
   const uint64_t k = (GPU_FILL_ROWS + batch_size - 1) / (batch_size ? batch_size : 1) + 1;
-  return k < 2 ? 2 : (k > (uint64_t)FEED_MAX_STREAMS ? FEED_MAX_STREAMS : (int)k);
+  int want = k < 2 ? 2 : (k > (uint64_t)FEED_MAX_STREAMS ? FEED_MAX_STREAMS : (int)k);
+  const int budget = (hw_queues - 1) / (feeds_on_device > 0 ? feeds_on_device : 1);
+  if (want > budget) want = budget;
+  return want < 1 ? 1 : want;
 }
 
 enum SlotState { SLOT_FREE, SLOT_FILLING, SLOT_CLOSED, SLOT_BUSY, SLOT_LAUNCHED };
@@ -240,6 +249,20 @@ void pool_put(FeedRes* r) {
   release_res(r);
 }
 
+// Flags of the batch slots' pinned host buffers: the HIP default, or
+// CUDASP_TF_PINNED = noncoherent / coherent / portable (measurement knob).
+unsigned pinned_flags() {
+  static const unsigned flags = [] {
+    const char* e = getenv("CUDASP_TF_PINNED");
+    if (!e) return (unsigned)hipHostMallocDefault;
+    if (!strcmp(e, "noncoherent")) return (unsigned)hipHostMallocNonCoherent;
+    if (!strcmp(e, "coherent")) return (unsigned)hipHostMallocCoherent;
+    if (!strcmp(e, "portable")) return (unsigned)hipHostMallocPortable;
+    return (unsigned)hipHostMallocDefault;
+  }();
+  return flags;
+}
+
 // Pinned/device buffers of a slot for cap_rows rows, at least `words` output
 // words and `txid` txid bytes.  Called with the slot owned by the caller
 // (state BUSY): no reservation, copy or launch touches it.
@@ -247,9 +270,9 @@ int prepare_slot(FeedSlot& s, int device, uint32_t cap_rows, size_t words, size_
   DeviceSet dg(device);
   if (!s.allocated) {
     const size_t n = cap_rows;
-    HOST_HIP(hipHostMalloc((void**)&s.h_tweaks, n * 64, hipHostMallocDefault));
-    HOST_HIP(hipHostMalloc((void**)&s.h_offs, n * 4, hipHostMallocDefault));
-    HOST_HIP(hipHostMalloc((void**)&s.h_lens, n * 4, hipHostMallocDefault));
+    HOST_HIP(hipHostMalloc((void**)&s.h_tweaks, n * 64, pinned_flags()));
+    HOST_HIP(hipHostMalloc((void**)&s.h_offs, n * 4, pinned_flags()));
+    HOST_HIP(hipHostMalloc((void**)&s.h_lens, n * 4, pinned_flags()));
     HOST_HIP(hipHostMalloc((void**)&s.h_flags, n, hipHostMallocDefault));
     HOST_HIP(hipMalloc((void**)&s.d_rows, n * 64));
     HOST_HIP(hipMalloc((void**)&s.d_tx, n * 32));
@@ -269,7 +292,7 @@ int prepare_slot(FeedSlot& s, int device, uint32_t cap_rows, size_t words, size_
     if (s.h_outputs) (void)hipHostFree(s.h_outputs);
     s.h_outputs = nullptr;
     s.outputs_cap = 0;
-    HOST_HIP(hipHostMalloc((void**)&s.h_outputs, cap * sizeof(int64_t), hipHostMallocDefault));
+    HOST_HIP(hipHostMalloc((void**)&s.h_outputs, cap * sizeof(int64_t), pinned_flags()));
     s.outputs_cap = cap;
   }
   if (txid > s.txid_bytes.size()) s.txid_bytes.resize(txid);
@@ -292,12 +315,15 @@ struct Feed {
   // txid space before batch_size rows: long output lists, long txids)
   double words_per_row = 2.0;
   double txid_per_row = 32.0;
+  bool ramp = false;     // CUDASP_TF_RAMP=1 (close_at)
+  uint32_t closed = 0;   // slots closed so far
   int error = CUDASP_OK;
   std::string error_msg;
   std::mutex stream_mu[FEED_MAX_STREAMS];  // a scanner's host state is not re-entrant
   // statistics (under mu)
   uint64_t launches = 0, rows = 0;
   double harvest_wait_s = 0;
+  double reserve_s = 0, copy_s = 0, launch_s = 0;
 };
 
 struct cudasp_tf_global {
@@ -355,6 +381,7 @@ int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   const uint32_t n = s.rows;
   const size_t words = s.words;
   lk.unlock();
+  const double t0 = now_s();
   int rc = CUDASP_OK;
   {
     std::lock_guard<std::mutex> sl(f.stream_mu[s.stream]);
@@ -387,7 +414,9 @@ int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
     };
     rc = run();
   }
+  const double spent = now_s() - t0;
   lk.lock();
+  f.launch_s += spent;
   if (rc != CUDASP_OK) {
     s.state = SLOT_FREE;  // its rows are lost; the query fails with rc
     feed_fail(f, rc);
@@ -437,9 +466,19 @@ int harvest_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
 int close_open_locked(Feed& f, std::unique_lock<std::mutex>& lk) {
   FeedSlot& s = f.res->slots[f.open];
   s.state = SLOT_CLOSED;
+  f.closed++;
   f.open = (f.open + 1) % f.res->nslots();
   if (s.writers == 0) return launch_locked(f, s, lk);
   return CUDASP_OK;
+}
+
+// Rows at which the open slot closes: batch_size; with the ramp
+// (CUDASP_TF_RAMP=1) the feed's first slots close at batch_size / 8, / 4,
+// / 2 so the GPU starts before a whole batch has been read.
+uint64_t close_at(const Feed& f) {
+  if (!f.ramp || f.closed >= 3) return f.batch_size;
+  const uint64_t r = f.batch_size >> (3 - f.closed);
+  return r < CUDASP_TF_VECTOR_SIZE ? std::min<uint64_t>(f.batch_size, CUDASP_TF_VECTOR_SIZE) : r;
 }
 
 struct Reservation {
@@ -490,8 +529,9 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
           s.txid_used += ntx;
           s.writers++;
           // >= batch_size (:416-418): closed now, launched by its last writer
-          if (s.rows >= f.batch_size) {
+          if (s.rows >= close_at(f)) {
             s.state = SLOT_CLOSED;
+            f.closed++;
             f.open = (f.open + 1) % r.nslots();
           }
           return CUDASP_OK;
@@ -532,8 +572,10 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
 }
 
 // A reservation's copy is done; the last writer of a closed slot launches it.
-int feed_commit(Feed& f, FeedSlot& s) {
+int feed_commit(Feed& f, FeedSlot& s, double reserve_s, double copy_s) {
   std::unique_lock<std::mutex> lk(f.mu);
+  f.reserve_s += reserve_s;
+  f.copy_s += copy_s;
   s.writers--;
   if (s.state == SLOT_CLOSED && s.writers == 0) return launch_locked(f, s, lk);
   return CUDASP_OK;
@@ -617,6 +659,7 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
   f->batch_size = b.batch_size;
   f->ow = out_words(b);
   f->words_per_row = 2.0 * f->ow;
+  if (const char* e = getenv("CUDASP_TF_RAMP")) f->ramp = atoi(e) != 0;
   *out = f.get();
   g.feeds[lg] = std::move(f);
   g.feed_ptr[lg].store(*out, std::memory_order_release);
@@ -632,10 +675,72 @@ int next_feed_index(const cudasp_tf_global& g, cudasp_tf_local& l) {
 // AccumulateInput (src/cudasp_extension.cu:154-224) for one DuckDB chunk:
 // count and validate the rows (NULL txid/height/tweak rows skipped, NULL list
 // = no outputs, NULL elements dropped, :195-221), reserve, copy, commit.
+// A chunk without NULLs (no validity arrays) and with int64 outputs: one
+// pass to validate and count, then bulk copies where DuckDB's vectors are
+// contiguous (heights; the list children when the lists are back to back).
+int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l,
+                     const cudasp_tf_chunk& c) {
+  const uint32_t n = c.count;
+  size_t nouts = 0, ntx = 0;
+  bool lists_contiguous = true;
+  const uint64_t first = n ? c.list_offset[0] : 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (c.tweak_size[i] != TWEAK_KEY_SIZE)
+      return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", c.tweak_size[i]);
+    ntx += c.txid_size[i];
+    lists_contiguous &= c.list_offset[i] == first + nouts;
+    nouts += c.list_length[i];
+  }
+  Feed* f = nullptr;
+  int rc = feed_for(g, b, next_feed_index(g, l), &f);
+  if (rc != CUDASP_OK) return rc;
+  Reservation res;
+  const double t0 = now_s();
+  rc = feed_reserve(*f, n, nouts, ntx, &res);
+  if (rc != CUDASP_OK) return rc;
+  const double t1 = now_s();
+  FeedSlot& s = *res.slot;
+  const uint32_t r0 = res.row0;
+  memcpy(s.heights.data() + r0, c.height, (size_t)n * sizeof(int32_t));
+  uint8_t* tw = s.h_tweaks + (size_t)r0 * TWEAK_KEY_SIZE;
+  for (uint32_t i = 0; i < n; i++) memcpy(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak_data[i], TWEAK_KEY_SIZE);
+  size_t tx = res.tx0;
+  uint8_t* txb = s.txid_bytes.data();
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t sz = c.txid_size[i];
+    s.txid_off[r0 + i] = tx;
+    s.txid_size[r0 + i] = sz;
+    if (sz == 32)
+      memcpy(txb + tx, c.txid_data[i], 32);
+    else if (sz)
+      memcpy(txb + tx, c.txid_data[i], sz);
+    tx += sz;
+  }
+  size_t o = res.word0;  // one word per output (no full_x here)
+  if (lists_contiguous) {
+    if (nouts) memcpy(s.h_outputs + o, c.child_values + first, nouts * sizeof(int64_t));
+    for (uint32_t i = 0; i < n; i++) {
+      s.h_offs[r0 + i] = (uint32_t)(o + (c.list_offset[i] - first));
+      s.h_lens[r0 + i] = (uint32_t)c.list_length[i];
+    }
+  } else {
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t len = (uint32_t)c.list_length[i];
+      s.h_offs[r0 + i] = (uint32_t)o;
+      s.h_lens[r0 + i] = len;
+      if (len) memcpy(s.h_outputs + o, c.child_values + c.list_offset[i], (size_t)len * sizeof(int64_t));
+      o += len;
+    }
+  }
+  return feed_commit(*f, s, t1 - t0, now_s() - t1);
+}
+
 int feed_chunk(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l, const cudasp_tf_chunk& c) {
   const size_t ow = out_words(b);
   if (b.opt.full_x && c.count > 0 && (!c.child_blob_data || !c.child_blob_size))
     return host_fail(CUDASP_ERR_INVALID_ARG, "full_x needs the outputs column as BLOB[] (child_blob_data)");
+  if (!b.opt.full_x && !c.txid_valid && !c.height_valid && !c.tweak_valid && !c.list_valid && !c.child_valid)
+    return feed_chunk_dense(b, g, l, c);
   uint32_t nrows = 0;
   size_t nouts = 0, ntx = 0;
   for (uint32_t i = 0; i < c.count; i++) {
@@ -659,8 +764,10 @@ int feed_chunk(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_loca
   int rc = feed_for(g, b, next_feed_index(g, l), &f);
   if (rc != CUDASP_OK) return rc;
   Reservation res;
+  const double t0 = now_s();
   rc = feed_reserve(*f, nrows, nouts * ow, ntx, &res);
   if (rc != CUDASP_OK) return rc;
+  const double t1 = now_s();
   FeedSlot& s = *res.slot;
   uint32_t r = res.row0;
   size_t o = res.word0 / ow;  // output index
@@ -690,7 +797,7 @@ int feed_chunk(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_loca
     s.h_lens[r] = len;
     r++;
   }
-  return feed_commit(*f, s);
+  return feed_commit(*f, s, t1 - t0, now_s() - t1);
 }
 
 // Columnar rows [r0, r1) of `c` (Arrow layout, cudasp_tf_columns), same row
@@ -769,8 +876,10 @@ int feed_columns(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_lo
   int rc = feed_for(g, b, next_feed_index(g, l), &f);
   if (rc != CUDASP_OK) return rc;
   Reservation res;
+  const double t0 = now_s();
   rc = feed_reserve(*f, nrows, nouts * ow, ntx, &res);
   if (rc != CUDASP_OK) return rc;
+  const double t1 = now_s();
   FeedSlot& s = *res.slot;
   const uint32_t rbase = res.row0;
   const size_t obase = res.word0 / ow;
@@ -793,7 +902,7 @@ int feed_columns(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_lo
       s.h_offs[row] = (uint32_t)(obase + ((uint64_t)lo[i] - first));
       s.h_lens[row] = (uint32_t)(lo[i + 1] - lo[i]);
     }
-    return feed_commit(*f, s);
+    return feed_commit(*f, s, t1 - t0, now_s() - t1);
   }
   uint32_t r = rbase;
   size_t o = obase, tx = res.tx0;
@@ -826,7 +935,7 @@ int feed_columns(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_lo
     s.h_lens[r] = len;
     r++;
   }
-  return feed_commit(*f, s);
+  return feed_commit(*f, s, t1 - t0, now_s() - t1);
 }
 
 // Drain a query's feeds (work still in flight after an error or an aborted
@@ -989,28 +1098,35 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
     }
   }
   g->bind = b;
-  g->feed_streams = feed_streams_for(b->batch_size);
+  const char* hq = getenv("GPU_MAX_HW_QUEUES");
+  g->hw_queues = hq && atoi(hq) > 0 ? atoi(hq) : 4;
+  int feeds_per_device = 0;
+  for (int d : g->device_map) {
+    int m = 0;
+    for (int e : g->device_map) m += e == d;
+    feeds_per_device = std::max(feeds_per_device, m);
+  }
+  g->feed_streams = feed_streams_for(b->batch_size, g->hw_queues, feeds_per_device);
   g->feeds.resize(g->num_gpus);
   g->feed_ptr.reset(new std::atomic<Feed*>[g->num_gpus]);
   for (int lg = 0; lg < g->num_gpus; lg++) g->feed_ptr[lg].store(nullptr);
   g->feed_create_mu.reset(new std::mutex[g->num_gpus]);
   // The HIP runtime maps a process's streams on a device onto
-  // GPU_MAX_HW_QUEUES hardware queues (4 unless set before HIP initialises);
-  // streams sharing a queue serialize their kernels.  Report the setting and
-  // warn when this query's streams on one device exceed it.
-  const char* hq = getenv("GPU_MAX_HW_QUEUES");
-  g->hw_queues = hq && atoi(hq) > 0 ? atoi(hq) : 4;
+  // GPU_MAX_HW_QUEUES hardware queues (4 unless set before HIP initialises),
+  // one of them the null stream's; streams sharing a queue serialize their
+  // kernels.  Report the setting and warn when this query's streams on one
+  // device exceed the queues left (only with CUDASP_TF_STREAMS set).
   for (int lg = 0; lg < g->num_gpus; lg++) {
     int on_dev = 0;
     for (int d : g->device_map) on_dev += d == g->device_map[lg] ? g->feed_streams : 0;
     if (on_dev > g->max_streams_per_device) g->max_streams_per_device = on_dev;
   }
   static std::atomic<bool> warned{false};
-  if (g->max_streams_per_device > g->hw_queues && !warned.exchange(true))
+  if (g->max_streams_per_device > g->hw_queues - 1 && !warned.exchange(true))
     fprintf(stderr,
-            "cudasp_scan: %d streams per device exceed GPU_MAX_HW_QUEUES=%d; streams that share a hardware queue "
-            "run their kernels one after another\n",
-            g->max_streams_per_device, g->hw_queues);
+            "cudasp_scan: %d streams per device exceed the %d hardware queues GPU_MAX_HW_QUEUES=%d leaves beside the "
+            "null stream; streams that share a hardware queue run their kernels one after another\n",
+            g->max_streams_per_device, g->hw_queues - 1, g->hw_queues);
   *out = g;
   return CUDASP_OK;
 }
@@ -1036,6 +1152,9 @@ int cudasp_tf_get_stats(cudasp_tf_global* g, cudasp_tf_stats* out) {
     out->launches += fp->launches;
     out->rows += fp->rows;
     out->harvest_wait_s += fp->harvest_wait_s;
+    out->reserve_s += fp->reserve_s;
+    out->copy_s += fp->copy_s;
+    out->launch_s += fp->launch_s;
   }
   return CUDASP_OK;
 }

@@ -1349,9 +1349,12 @@ int launch_pipeline(cudasp_scanner* s, const uint32_t* tx, const uint32_t* ty, c
   if (s->fused_single && !values && !t_out && flags && multi_ok(s) && !s->rows_a_force && !s->rows_b_force) {
     // both stages in one k_scan_multi launch over this batch: ROWS_A rows per
     // thread throughout, one wave per chunk
+    // (R = rows_a_for: 4, or 2 / 1 for a launch too small to fill a quarter
+    // of the device at 4, so the tail batch of a query runs 2-4x shorter)
     std::vector<MultiBatch> md(1, multi_desc(tx, ty, outputs, offs, lens, n, flags, match_rows, match_count, 0));
     const uint64_t wr = (n + 63u) / 64u;
-    const int rc = launch_multi(s, md, wr, st, ROWS_A, 0, 0, (wr + ROWS_A * 4 - 1) / (ROWS_A * 4));
+    const uint32_t R = (uint32_t)rows_a_for(s, n);
+    const int rc = launch_multi(s, md, wr, st, R, 0, 0, (wr + R * 4 - 1) / (R * 4));
     // CUDASP_ERR_CAPACITY: no scratch for the fused launch and nothing queued;
     // the two stage kernels below give the same results
     if (rc != CUDASP_ERR_CAPACITY) return rc;

@@ -97,6 +97,9 @@ class _Stats(ctypes.Structure):
         ("launches", ctypes.c_uint64),
         ("rows", ctypes.c_uint64),
         ("harvest_wait_s", ctypes.c_double),
+        ("reserve_s", ctypes.c_double),
+        ("copy_s", ctypes.c_double),
+        ("launch_s", ctypes.c_double),
     ]
 
 

@@ -77,8 +77,10 @@ uint64_t cudasp_tf_bind_batch_size(const cudasp_tf_bind_data* b);
  *
  * Batching: every GPU (logical GPU, see below) gets one *device feed* per
  * query -- a ring of pinned batch slots that all executor threads fill
- * together, and 2..4 streams, each with its own scanner, that run the closed
- * slots (H2D, transpose, one fused k_scan_multi launch, D2H of the flags).  A
+ * together, and 1..4 streams, each with its own scanner, that run the closed
+ * slots (H2D, transpose, one fused k_scan_multi launch, D2H of the flags): as
+ * many as fill the GPU, within the hardware queues HIP leaves the feed beside
+ * the null stream's (3 at the default GPU_MAX_HW_QUEUES = 4).  A
  * slot closes once it holds >= batch_size rows (the reference's trigger,
  * src/cudasp_extension.cu:416-418, applied to a device's rows instead of one
  * thread's) or runs out of output/txid space, and is launched by the last
@@ -88,8 +90,9 @@ uint64_t cudasp_tf_bind_batch_size(const cudasp_tf_bind_data* b);
  * emitted multiset of rows does not.
  *
  * A warning goes to stderr (once per process) when a query's streams on one
- * device exceed GPU_MAX_HW_QUEUES (read from the environment; HIP's default
- * is 4): streams sharing a hardware queue serialize their kernels. */
+ * device exceed GPU_MAX_HW_QUEUES - 1 (read from the environment; HIP's
+ * default is 4; only possible with the CUDASP_TF_STREAMS override): streams
+ * sharing a hardware queue serialize their kernels. */
 int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out);
 void cudasp_tf_global_free(cudasp_tf_global* g);
 int cudasp_tf_num_gpus(const cudasp_tf_global* g);
@@ -104,6 +107,9 @@ typedef struct {
   uint64_t launches;               /* batches launched, all feeds */
   uint64_t rows;                   /* rows launched, all feeds */
   double harvest_wait_s;           /* executor-thread time blocked on GPU completion */
+  double reserve_s;                /* executor-thread time getting room in a slot (harvests and waits included) */
+  double copy_s;                   /* executor-thread time copying rows into the slots */
+  double launch_s;                 /* executor-thread time issuing the batches' copies and kernels */
 } cudasp_tf_stats;
 int cudasp_tf_get_stats(cudasp_tf_global* g, cudasp_tf_stats* out);
 

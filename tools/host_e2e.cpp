@@ -122,8 +122,7 @@ struct Table {
   std::vector<uint8_t> tweaks, txids;
   std::vector<int32_t> heights;
   std::vector<int64_t> outputs;
-  std::vector<uint64_t> list_off, list_len;         // rows-mode list entries
-  std::vector<int32_t> txid_offsets, list_off32;    // Arrow offsets (rows + 1)
+  std::vector<uint64_t> list_off, list_len;         // list entries (offset into outputs, length)
   std::vector<uint64_t> planted;                    // planted row indices, sorted
   uint32_t labels_planted_mask = 0;                 // label indices planted (bit j)
 };
@@ -194,16 +193,6 @@ static void generate(const Args& a, const uint8_t scan[32], const uint8_t spend[
   HK(hipFree(d_offs));
   HK(hipFree(d_lens));
   HK(hipFree(d_outs));
-  if (t.outputs.size() >= (1ull << 31) || rows >= (1ull << 31) / 32) {
-    fprintf(stderr, "table too large for int32 Arrow offsets\n");
-    exit(1);
-  }
-  t.txid_offsets.resize(rows + 1);
-  t.list_off32.resize(rows + 1);
-  for (uint64_t i = 0; i <= rows; i++) {
-    t.txid_offsets[i] = (int32_t)(i * 32);
-    t.list_off32[i] = (int32_t)(i < rows ? t.list_off[i] : t.outputs.size());
-  }
 
   // ---- planted values: base on g = 0 mod 1000, label j on g = 1 mod 1000
   const int L = a.labels;
@@ -305,23 +294,28 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
   for (int i = 0; i < T; i++) {
     th.emplace_back([&, i]() {
       if (a.columnar) {
+        // Arrow record batches of 65536 rows: int32 offsets per batch, the
+        // buffers starting at the batch's first row (a 100M-row table has
+        // more than 2^31 txid bytes in all)
         const uint64_t piece = 65536;
+        std::vector<int32_t> txo(piece + 1), lo(piece + 1);
         for (;;) {
           const uint64_t c0 = next.fetch_add(piece);
           if (c0 >= rows) break;
+          const uint64_t m = std::min<uint64_t>(piece, rows - c0);
+          for (uint64_t r = 0; r <= m; r++) {
+            txo[r] = (int32_t)(r * 32);
+            lo[r] = (int32_t)((c0 + r < rows ? t.list_off[c0 + r] : t.outputs.size()) - t.list_off[c0]);
+          }
           cudasp_tf_columns c{};
-          c.count = std::min<uint64_t>(piece, rows - c0);
-          c.txid_offsets = t.txid_offsets.data();
-          c.txid_data = t.txids.data();
-          c.txid_offset = c0;
-          c.height = t.heights.data();
-          c.height_offset = c0;
-          c.tweak_data = t.tweaks.data();
+          c.count = m;
+          c.txid_offsets = txo.data();
+          c.txid_data = t.txids.data() + c0 * 32;
+          c.height = t.heights.data() + c0;
+          c.tweak_data = t.tweaks.data() + c0 * 64;
           c.tweak_fixed_width = 64;
-          c.tweak_offset = c0;
-          c.list_offsets = t.list_off32.data();
-          c.list_offset = c0;
-          c.child_values = t.outputs.data();
+          c.list_offsets = lo.data();
+          c.child_values = t.outputs.data() + t.list_off[c0];
           const double s = now_s();
           CK(cudasp_tf_function_columns(bd, gs, ls[i], &c));
           t_calls[i] += now_s() - s;
@@ -438,7 +432,8 @@ int main(int argc, char** argv) {
          "\"emitted_equal_planted\": %s, \"warmup_seconds\": %.3f, \"generate_seconds\": %.2f, \"devices\": %d, "
          "\"feeds\": %u, \"streams_per_feed\": %u, \"max_streams_per_device\": %u, \"gpu_max_hw_queues\": %u, "
          "\"gpu_max_hw_queues_env\": \"%s\", \"launches\": %llu, \"rows_per_launch\": %.0f, "
-         "\"harvest_wait_s\": %.4f, \"thread_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
+         "\"harvest_wait_s\": %.4f, \"reserve_s\": %.4f, \"copy_s\": %.4f, \"launch_s\": %.4f, "
+         "\"thread_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
          "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f}\n",
          a.columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)t.rows, a.threads, (long long)a.batch,
          a.labels,
@@ -448,6 +443,6 @@ int main(int argc, char** argv) {
          all_exact ? "true" : "false", warm.secs, gen_s, cudasp_device_count(), q.stats.feeds,
          q.stats.streams_per_feed, q.stats.max_streams_per_device, q.stats.hw_queues, hq ? hq : "",
          (unsigned long long)q.stats.launches, q.stats.launches ? (double)q.stats.rows / q.stats.launches : 0.0,
-         q.stats.harvest_wait_s, q.call_s_mean, q.final_s_mean, q.done_min, q.done_max);
+         q.stats.harvest_wait_s, q.stats.reserve_s, q.stats.copy_s, q.stats.launch_s, q.call_s_mean, q.final_s_mean, q.done_min, q.done_max);
   return all_exact ? 0 : 2;
 }
