@@ -647,13 +647,45 @@ def alu_roofline(path, value_per_gpu, multi=False):
         wi_per_row = (a + bm) / rpl
         per64 = dict(k_shared_secret=a / rpl * 64, k_match=bm / rpl * 64)
     achieved_wi = wi_per_row * value_per_gpu
-    return dict(bound="valu", unit="wave-instr/s per GPU", achieved=achieved_wi, peak=VALU_WAVE_INSTR_PEAK,
-                frac=achieved_wi / VALU_WAVE_INSTR_PEAK, measured_vop3_issue_rate=VOP3_WAVE_INSTR_MEASURED,
-                frac_of_measured_vop3_rate=achieved_wi / VOP3_WAVE_INSTR_MEASURED,
-                valu_wave_instr_per_64_rows=per64,
-                source=os.path.relpath(path, ROOT),
-                note="SQ_INSTS_VALU per row of a run of this shape (%s); peak = nominal VALU issue rate; VOP3 "
-                     "integer ops issue at about half of it on gfx950" % sq.get("shape", "see source"))
+    out = dict(bound="valu", unit="wave-instr/s per GPU", achieved=achieved_wi, peak=VALU_WAVE_INSTR_PEAK,
+               frac=achieved_wi / VALU_WAVE_INSTR_PEAK, measured_vop3_issue_rate=VOP3_WAVE_INSTR_MEASURED,
+               frac_of_measured_vop3_rate=achieved_wi / VOP3_WAVE_INSTR_MEASURED,
+               valu_wave_instr_per_64_rows=per64,
+               source=os.path.relpath(path, ROOT),
+               note="SQ_INSTS_VALU per row of a run of this shape (%s); peak = nominal VALU issue rate; VOP3 "
+                    "integer ops issue at about half of it on gfx950" % sq.get("shape", "see source"))
+    mix = mix_ceiling(achieved_wi)
+    if mix:
+        out["mix_ceiling"] = mix
+    return out
+
+
+VALU_CEILING_PROFILE = os.path.join(ROOT, "profiles", "r03_valu_ceiling.json")
+
+
+def mix_ceiling(achieved_wi):
+    """The issue ceiling of the scan's own instruction mix at the 2.4 GHz
+    peak clock (profiles/r03_valu_ceiling.json, tools/valu_ceiling.py): the
+    kernel's stage-A ladder (126 doublings + 39 mixed additions, ~88% of its
+    VALU) run as register-resident loops at the kernel's 3 waves per SIMD
+    issues U_ladder VALU wave-instructions per 4 SIMD cycles; x 1024 SIMDs x
+    2.4 GHz / 4 is the rate this mix sustains when nothing else limits it.
+    frac > 1 within a few percent means the kernel is at that ceiling (its
+    other ~12% of instructions issue a little faster than the ladder's)."""
+    if not os.path.exists(VALU_CEILING_PROFILE):
+        return None
+    with open(VALU_CEILING_PROFILE) as f:
+        vc = json.load(f)
+    u = vc.get("ladder_mix_U")
+    if not u:
+        return None
+    ceiling = u * 1024 * 2.4e9 / 4
+    k = vc.get("k_scan_multi_L0", {})
+    return dict(ladder_mix_U=u, ceiling_wave_instr_per_s_at_peak_clock=ceiling, frac=achieved_wi / ceiling,
+                kernel_U_measured=k.get("U"), kernel_frac_of_ladder_mix_measured=k.get("frac_of_ladder_mix_ceiling"),
+                source=os.path.relpath(VALU_CEILING_PROFILE, ROOT),
+                note="U = VALU wave-instructions per 4 SIMD cycles (PMC); the kernel's own U over the ladder loops' "
+                     "U is clock-independent; frac here also assumes the peak clock")
 
 
 def timed_steps(step, steps, warmup, device, barrier, counter=None):

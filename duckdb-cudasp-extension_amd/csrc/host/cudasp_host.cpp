@@ -315,7 +315,7 @@ struct Feed {
   // txid space before batch_size rows: long output lists, long txids)
   double words_per_row = 2.0;
   double txid_per_row = 32.0;
-  bool ramp = false;     // CUDASP_TF_RAMP=1 (close_at)
+  bool ramp = true;      // close_at; CUDASP_TF_RAMP=0 turns it off
   uint32_t closed = 0;   // slots closed so far
   int error = CUDASP_OK;
   std::string error_msg;
@@ -472,9 +472,11 @@ int close_open_locked(Feed& f, std::unique_lock<std::mutex>& lk) {
   return CUDASP_OK;
 }
 
-// Rows at which the open slot closes: batch_size; with the ramp
-// (CUDASP_TF_RAMP=1) the feed's first slots close at batch_size / 8, / 4,
-// / 2 so the GPU starts before a whole batch has been read.
+// Rows at which the open slot closes: batch_size, except that a feed's first
+// three slots close at batch_size / 8, / 4 and / 2 (the ramp), so the GPU
+// starts before a whole batch has been read: +6% end to end at 1M rows, +2%
+// at 9.4M, within the spread at 32.7M (profiles/r03_e2e_ramp_ab.txt).
+// CUDASP_TF_RAMP=0 turns it off.
 uint64_t close_at(const Feed& f) {
   if (!f.ramp || f.closed >= 3) return f.batch_size;
   const uint64_t r = f.batch_size >> (3 - f.closed);

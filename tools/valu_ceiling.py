@@ -1,24 +1,28 @@
-"""The VALU ceiling of a kernel's own instruction mix, from rocprofv3 PMC
-passes (tools/r03/gpu_valu_ceiling.sh writes the directory this reads).
+"""The VALU ceiling of k_scan_multi's own instruction mix, from rocprofv3
+PMC passes (tools/r03/gpu_valu_ceiling.sh writes the directory this reads).
 
-For every dispatch of the calibration microbenchmark
-(tools/microbench/int_throughput: issue-bound loops of one opcode each) and
-of k_scan_multi it reports, per kernel (median over its dispatches):
+Per dispatch (median over a kernel's dispatches):
+  cycles C   GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs)
+  clock f    C / kernel-trace duration (same dispatch ordinal, separate
+             --kernel-trace run)
+  U          4 x SQ_INSTS_VALU / (C x SIMDs): VALU issue in units of one
+             wave-instruction per 4 SIMD cycles.  (SQ_ACTIVE_INST_VALU reads
+             exactly one quad-cycle per VALU instruction on gfx950 -- the
+             calibration shows it -- so it is an instruction count here, not
+             the pipe's occupancy, and the ceiling has to be measured.)
 
-  cycles C        GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs)
-  clock f         C / kernel-trace duration (the same dispatch ordinal of a
-                  separate --kernel-trace run)
-  U               VALU busy fraction = 4 SQ_ACTIVE_INST_VALU / (C x SIMDs):
-                  SQ_ACTIVE_INST_VALU counts quad-cycles in which a wave issues
-                  a VALU instruction (MI355X_MICROARCH.md, PMC units)
-  c               SIMD cycles per VALU wave-instruction = 4 A / SQ_INSTS_VALU
-
-The calibration loops saturate the VALU by construction, so their U says what
-the counter reads at the issue limit (U_sat); a kernel's fraction of its own
-mix ceiling is U / U_sat -- the share of SIMD cycles its VALU instructions
-could have filled that they did fill, at the clock it ran.  The ceiling in
-wave-instructions/s is then achieved / (U / U_sat), and at the 2.4 GHz peak
-clock ceiling x 2.4 GHz / f.
+The ceiling is measured, not assumed: issue-bound loops with no memory
+traffic -- one opcode each (tools/microbench/int_throughput: VOP3 ops read
+U ~ 0.95-0.97, v_add_u32 1.70, v_addc with an SGPR carry-in 0.66) and the
+kernel's own group operations (tools/microbench/group_ops: the ladder's
+doubling and mixed addition, register-resident, 1-4 waves per SIMD).  The
+ladder mix (126 doublings x 893 + 39 mixed additions x 1576 VALU, ~88% of
+k_scan_multi's instructions) at 3 waves per SIMD -- the kernel's occupancy --
+gives U_ladder, the issue rate this instruction mix sustains when nothing
+else limits it.  k_scan_multi's fraction of that ceiling is U / U_ladder
+(the other ~12% of its instructions -- inversion, SHA-256, stage B -- are
+taken at the ladder's rate), and the ceiling in wave-instructions/s is
+achieved / fraction (x 2.4 GHz / f at the peak clock).
 
   python tools/valu_ceiling.py DIR [--json OUT]
 """
@@ -39,12 +43,21 @@ XCDS = 8
 PEAK_HZ = 2.4e9
 
 
+def key_of(r):
+    """Kernel name without arguments; the calibration loops also by grid
+    (group_ops runs one kernel at 1..4 waves per SIMD)."""
+    k = kernel_key(r["Kernel_Name"])
+    if k.startswith("void loop<"):
+        k += " grid %s" % (r.get("Grid_Size") or r.get("Grid_Size_X"))
+    return k
+
+
 def counters(path_glob):
     """{kernel: [ {counter: value} per dispatch, in dispatch order ]}."""
     out = collections.defaultdict(dict)
     for p in glob.glob(path_glob):
         for r in csv.DictReader(open(p)):
-            k = kernel_key(r["Kernel_Name"])
+            k = key_of(r)
             d = int(r["Dispatch_Id"])
             e = out[k].setdefault(d, collections.defaultdict(float))
             e[r["Counter_Name"]] += float(r["Counter_Value"])
@@ -56,7 +69,7 @@ def durations(path_glob):
     for p in glob.glob(path_glob):
         rows = sorted(csv.DictReader(open(p)), key=lambda r: int(r["Dispatch_Id"]))
         for r in rows:
-            out[kernel_key(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+            out[key_of(r)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     return out
 
 
@@ -74,9 +87,10 @@ def analyse(sq, grbm, kt, skip_first):
             cyc = g[i]["GRBM_GUI_ACTIVE"] / XCDS
             a = c.get("SQ_ACTIVE_INST_VALU", 0.0)
             row = dict(cycles=cyc, valu=c["SQ_INSTS_VALU"], active_valu=a,
-                       U=4 * a / (cyc * SIMDS) if cyc else None, c=4 * a / c["SQ_INSTS_VALU"],
+                       U=4 * c["SQ_INSTS_VALU"] / (cyc * SIMDS) if cyc else None, c=4 * a / c["SQ_INSTS_VALU"],
                        any_U=4 * c.get("SQ_ACTIVE_INST_ANY", 0.0) / (cyc * SIMDS) if cyc else None,
-                       busy=c.get("SQ_BUSY_CYCLES"), wave_cycles=c.get("SQ_WAVE_CYCLES"))
+                       busy=c.get("SQ_BUSY_CYCLES"), wave_cycles=c.get("SQ_WAVE_CYCLES"),
+                       int64=c.get("SQ_INSTS_VALU_INT64"), int32=c.get("SQ_INSTS_VALU_INT32"))
             if i < len(t) and t[i] > 0:
                 row["seconds"] = t[i]
                 row["clock_hz"] = cyc / t[i]
@@ -84,10 +98,16 @@ def analyse(sq, grbm, kt, skip_first):
             rows.append(row)
         if rows:
             med = {key: statistics.median([r[key] for r in rows if r.get(key) is not None])
-                   for key in rows[0] if any(r.get(key) is not None for r in rows)}
+                   for key in set().union(*rows) if any(r.get(key) is not None for r in rows)}
             med["dispatches"] = len(rows)
             res[k] = med
     return res
+
+
+# Stage A's ladder for the bench's scan key after the digit search: 126
+# doublings and 39 mixed additions of 893 and 1576 VALU;
+# ~88% of k_scan_multi's instructions.
+LADDER = ((126 * 893, "dbl"), (39 * 1576, "madd"))
 
 
 def main():
@@ -96,16 +116,32 @@ def main():
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     d = a.dir
+    out = {}
     mb = analyse(counters(d + "/mb_sq/*counter_collection.csv"), counters(d + "/mb_grbm/*counter_collection.csv"),
                  durations(d + "/mb_kt/*kernel_trace.csv"), skip_first=True)
-    print("calibration (issue-bound one-opcode loops):")
+    print("one-opcode loops (int_throughput; U = 4 x VALU instructions / SIMD cycles, 1.0 = one per 4 cycles):")
     for k, r in sorted(mb.items()):
-        print("  %-24s U %.3f  cycles/VALU-instr %.2f  clock %.2f GHz" % (k, r["U"], r["c"], r.get("clock_hz", 0) / 1e9))
-    sat = [r["U"] for r in mb.values() if r.get("U")]
-    u_sat = max(sat) if sat else 1.0
-    print("U at saturation (max over the loops): %.3f" % u_sat)
-    out = dict(u_saturated=u_sat, calibration={k: dict(U=r["U"], cycles_per_valu=r["c"],
-                                                        clock_hz=r.get("clock_hz")) for k, r in mb.items()})
+        print("  %-24s U %.3f  clock %.2f GHz" % (k, r["U"], r.get("clock_hz", 0) / 1e9))
+    out["one_opcode_loops"] = {k: dict(U=r["U"], clock_hz=r.get("clock_hz")) for k, r in mb.items()}
+    go = analyse(counters(d + "/go_sq/*counter_collection.csv"), counters(d + "/go_grbm/*counter_collection.csv"),
+                 durations(d + "/go_kt/*kernel_trace.csv"), skip_first=False)
+    names = {"void loop<0>": "dbl", "void loop<1>": "madd", "void loop<2>": "mul", "void loop<3>": "sqr"}
+    print("group-operation loops (group_ops: register-resident, issue-bound; by waves per SIMD):")
+    gu = {}
+    for k, r in sorted(go.items()):
+        base, grid = k.split(" grid ")
+        w = int(grid) // (256 * 256)
+        nm = names.get(base, base)
+        gu[(nm, w)] = r["U"]
+        print("  %-6s %d waves/SIMD  U %.3f  int64 share %.2f  clock %.2f GHz"
+              % (nm, w, r["U"], r.get("int64", 0) / r["valu"] if r.get("int64") else 0, r.get("clock_hz", 0) / 1e9))
+    out["group_op_loops"] = {"%s_w%d" % k: v for k, v in gu.items()}
+    u_ladder = None
+    if ("dbl", 3) in gu and ("madd", 3) in gu:
+        tot = sum(n for n, _ in LADDER)
+        u_ladder = tot / sum(n / gu[(op, 3)] for n, op in LADDER)
+        print("ladder mix at 3 waves/SIMD (126 dbl x 893 + 39 madd x 1576 VALU): U %.3f" % u_ladder)
+    out["ladder_mix_U"] = u_ladder
     for L in (0, 16):
         sc = analyse(counters(d + "/scan_sq_L%d/*counter_collection.csv" % L),
                      counters(d + "/scan_grbm_L%d/*counter_collection.csv" % L),
@@ -113,19 +149,19 @@ def main():
         r = sc.get("k_scan_multi")
         if not r:
             continue
-        frac = r["U"] / u_sat
-        ach = r.get("valu_per_s")
-        ceiling = ach / frac if ach else None
         f = r.get("clock_hz")
-        print("k_scan_multi, %d labels: U %.3f -> %.3f of the mix ceiling; cycles/VALU-instr %.2f; clock %.2f GHz; "
-              "achieved %.3e wave-instr/s; ceiling %.3e at this clock, %.3e at 2.4 GHz"
-              % (L, r["U"], frac, r["c"], (f or 0) / 1e9, ach or 0, ceiling or 0,
-                 (ceiling * PEAK_HZ / f) if (ceiling and f) else 0))
-        out["k_scan_multi_L%d" % L] = dict(U=r["U"], frac_of_mix_ceiling=frac, cycles_per_valu=r["c"], clock_hz=f,
-                                           achieved_wave_instr_per_s=ach, mix_ceiling_wave_instr_per_s=ceiling,
+        ach = r.get("valu_per_s")
+        frac = r["U"] / u_ladder if u_ladder else None
+        ceiling = ach / frac if (ach and frac) else None
+        print("k_scan_multi, %d labels: U %.3f; clock %.2f GHz; achieved %.3e wave-instr/s; frac of the ladder-mix "
+              "ceiling %s; ceiling %s wave-instr/s at this clock, %s at 2.4 GHz"
+              % (L, r["U"], (f or 0) / 1e9, ach or 0, "%.3f" % frac if frac else "-",
+                 "%.3e" % ceiling if ceiling else "-", "%.3e" % (ceiling * PEAK_HZ / f) if (ceiling and f) else "-"))
+        out["k_scan_multi_L%d" % L] = dict(U=r["U"], clock_hz=f, achieved_wave_instr_per_s=ach,
+                                           frac_of_ladder_mix_ceiling=frac,
+                                           mix_ceiling_wave_instr_per_s=ceiling,
                                            mix_ceiling_at_peak_clock=(ceiling * PEAK_HZ / f) if (ceiling and f) else None,
-                                           any_issue_U=r.get("any_U"), valu_per_dispatch=r["valu"],
-                                           seconds=r.get("seconds"))
+                                           valu_per_dispatch=r["valu"], seconds=r.get("seconds"))
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(out, fh, indent=1)
