@@ -175,7 +175,8 @@ struct FeedSlot {
   uint8_t* d_flags = nullptr;
   int64_t* d_outputs = nullptr;
   size_t d_outputs_cap = 0;  // words
-  hipEvent_t done = nullptr;
+  hipEvent_t done = nullptr;    // the batch's flags are on the host
+  hipEvent_t copied = nullptr;  // the batch's H2D upload is done
   bool allocated = false;
   // fill state, guarded by Feed::mu
   SlotState state = SLOT_FREE;
@@ -205,6 +206,7 @@ void free_slot(FeedSlot& s) {
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (s.done) (void)hipEventDestroy(s.done);
+  if (s.copied) (void)hipEventDestroy(s.copied);
   s = FeedSlot();
 }
 
@@ -281,6 +283,7 @@ int prepare_slot(FeedSlot& s, int device, uint32_t cap_rows, size_t words, size_
     HOST_HIP(hipMalloc((void**)&s.d_lens, n * 4));
     HOST_HIP(hipMalloc((void**)&s.d_flags, n));
     HOST_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    HOST_HIP(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
     s.txid_off.resize(n);
     s.txid_size.resize(n);
     s.heights.resize(n);
@@ -316,6 +319,7 @@ struct Feed {
   double words_per_row = 2.0;
   double txid_per_row = 32.0;
   bool ramp = true;      // close_at; CUDASP_TF_RAMP=0 turns it off
+  bool upload_null = true;  // H2D on the null stream; CUDASP_TF_UPLOAD=stream: on the scan stream (A/B)
   uint32_t closed = 0;   // slots closed so far
   int error = CUDASP_OK;
   std::string error_msg;
@@ -396,11 +400,22 @@ int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
         HOST_HIP(hipMalloc((void**)&s.d_outputs, s.outputs_cap * sizeof(int64_t)));
         s.d_outputs_cap = s.outputs_cap;
       }
-      HOST_HIP(hipMemcpyAsync(s.d_rows, s.h_tweaks, (size_t)n * 64, hipMemcpyHostToDevice, st));
-      HOST_HIP(hipMemcpyAsync(s.d_offs, s.h_offs, (size_t)n * 4, hipMemcpyHostToDevice, st));
-      HOST_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, st));
+      // The upload goes on the device's null stream (its hardware queue is
+      // otherwise idle) and the scan stream waits for it: on the scan stream
+      // itself a batch's H2D would queue behind that stream's running kernel,
+      // and each stream would spend ~0.8 ms of every ~6 ms launch cycle with
+      // no kernel in flight (kernel + copy trace, profiles/r03_e2e_trace.txt).
+      // The slot's device buffers are free: its previous batch was harvested.
+      hipStream_t up = f.upload_null ? (hipStream_t)0 : st;
+      HOST_HIP(hipMemcpyAsync(s.d_rows, s.h_tweaks, (size_t)n * 64, hipMemcpyHostToDevice, up));
+      HOST_HIP(hipMemcpyAsync(s.d_offs, s.h_offs, (size_t)n * 4, hipMemcpyHostToDevice, up));
+      HOST_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, up));
       if (words)
-        HOST_HIP(hipMemcpyAsync(s.d_outputs, s.h_outputs, words * sizeof(int64_t), hipMemcpyHostToDevice, st));
+        HOST_HIP(hipMemcpyAsync(s.d_outputs, s.h_outputs, words * sizeof(int64_t), hipMemcpyHostToDevice, up));
+      if (up != st) {
+        HOST_HIP(hipEventRecord(s.copied, up));
+        HOST_HIP(hipStreamWaitEvent(st, s.copied, 0));
+      }
       int rc2 = cudasp_tweaks_to_columns(s.d_rows, n, s.d_tx, s.d_ty, st);
       if (rc2 == CUDASP_OK)
         rc2 = cudasp_scan_device(sc, s.d_tx, s.d_ty, s.d_outputs, s.d_offs, s.d_lens, n, s.d_flags, nullptr, nullptr,
@@ -662,6 +677,7 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
   f->ow = out_words(b);
   f->words_per_row = 2.0 * f->ow;
   if (const char* e = getenv("CUDASP_TF_RAMP")) f->ramp = atoi(e) != 0;
+  if (const char* e = getenv("CUDASP_TF_UPLOAD")) f->upload_null = strcmp(e, "stream") != 0;
   *out = f.get();
   g.feeds[lg] = std::move(f);
   g.feed_ptr[lg].store(*out, std::memory_order_release);
