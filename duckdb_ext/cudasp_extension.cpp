@@ -254,13 +254,9 @@ static OperatorFinalizeResultType CudaspScanFinalFunction(ExecutionContext &cont
 }
 
 static void LoadInternal(ExtensionLoader &loader) {
-	// One stream per executor thread: with the HIP runtime's default of 4
-	// hardware queues per process, the threads' batches serialize on shared
-	// queues (end to end at batch 300k: 136-152 M tx/s with 4 queues, 151-154
-	// with 16; at 75k rows: 65-84 vs 91-98). The runtime reads
-	// this once, when HIP initialises -- on the first scan, after this load --
-	// so it is set here, unless the user chose a value.
-	setenv("GPU_MAX_HW_QUEUES", "16", 0);
+	// No process settings are needed: the host's device feeds size their
+	// streams from the hardware queues the HIP runtime gives the process
+	// (GPU_MAX_HW_QUEUES, 4 by default).
 	TableFunction func("cudasp_scan",
 	                   {LogicalType::TABLE, LogicalType::BLOB, LogicalType::BLOB, LogicalType::LIST(LogicalType::BLOB)},
 	                   nullptr, CudaspScanBind, CudaspScanInit, CudaspScanLocalInit);
