@@ -1,3 +1,4 @@
+# (The merged-launch build this recipe measured was reverted after the A/B; CUDASP_TF_MERGE has no effect now.)
 # Round 3: merged launches (CUDASP_TF_MERGE=1: 2 streams, an idle stream takes
 # all ready slots, up to 4, in one cudasp_scan_device_batches launch) -- the
 # host GPU tests under it first, then e2e A/B interleaved on one box.
