@@ -38,7 +38,9 @@ L labels the next row gets label j's value, j cycling over all L labels, so the
 expected match count is known exactly and checked after the run.
 
 Only the cpu_baseline leg touches oracle/ (the C restatement, timed on a
-bounded sample on this box's host cores, and checked against the GPU flags).
+bounded sample on this box's host cores, and checked against the GPU flags;
+it also recomputes the planted values of 256 planted rows spread over the
+whole rank table: `planted_oracle_check`).
 """
 import argparse
 import hashlib
@@ -185,6 +187,7 @@ class Table:
         self.expected = 0
         self.expected_per_batch = [0] * self.nb
         self.planted_labels = set()
+        self.plant_log = []  # (batch, row in batch, values column: 0 = base, 1 + j = label j)
         L = len(labels)
         per_batch = 2 * ((batch + PLANT_EVERY - 1) // PLANT_EVERY) + 2
         planter = Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=per_batch, device=device)
@@ -213,6 +216,9 @@ class Table:
                 self.outs[b].index_copy_(0, pos[nbase:], vals[1 + jt, cols])
             self.expected += len(idx)
             self.expected_per_batch[b] = len(idx)
+            self.plant_log += [(b, i, 0) for i in base_idx]
+            if lab_idx:
+                self.plant_log += [(b, i, 1 + j) for i, j in zip(lab_idx, js)]
         planter.close()
         torch.cuda.synchronize(dev)
 
@@ -556,6 +562,32 @@ def cpu_baseline(smp, labels, threads, output_count=1, label_negation=False):
                        "pthreads" % (smp["rows"], smp["batches"], len(labels), threads),
                 seconds=round(dt, 3), flags_match_gpu=bool(np.array_equal(flags, smp["gpu_flags"])),
                 sample_matches=int(flags.sum()))
+
+
+def planted_oracle_check(tab, labels, threads, count=256):
+    """The planted values (computed by the product's values path) of `count`
+    planted rows spread over the whole rank table, recomputed by the C oracle:
+    ties the full table's expected match count -- not only the CPU sample's
+    first rows -- to the oracle.  Checker use of oracle/, in the CPU leg."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle
+    log = tab.plant_log
+    if not log:
+        return dict(rows=0)
+    pick = [log[int(i * len(log) / min(count, len(log)))] for i in range(min(count, len(log)))]
+    tw, want_col, planted = [], [], []
+    for b, i, col in pick:
+        x = tab.cols(tab.tx, b)[:, i].cpu().numpy().view(np.uint32)
+        y = tab.cols(tab.ty, b)[:, i].cpu().numpy().view(np.uint32)
+        tw.append(np.concatenate([x, y]).astype("<u4").view(np.uint8))
+        want_col.append(col)
+        planted.append(int(tab.outs[b][int(tab.offs[b][i].item())].item()))
+    _, vals = oracle.scan(SCAN_KEY, SPEND_KEY, labels, np.stack(tw), threads=threads, want_values=True)
+    got = [int(vals[r, c]) for r, c in enumerate(want_col)]
+    return dict(rows=len(pick), of_planted=len(log), equal=int(sum(g == p for g, p in zip(got, planted))),
+                batches=len({b for b, _, _ in pick}), label_columns=sorted({c for c in want_col if c}),
+                note="planted values of rows spread over every batch of the rank table, recomputed by "
+                     "oracle/cudasp_oracle.c")
 
 
 def cpu_baseline_optimized(smp, labels, threads):
@@ -931,6 +963,7 @@ def main():
                                              omp_num_threads=os.environ.get("OMP_NUM_THREADS"))
         result["cpu_baseline"] = cpu_baseline(smp, labels, threads, args.output_count, args.label_negation)
         result["cpu_baseline"]["host_cpus_visible"] = visible
+        result["planted_oracle_check"] = planted_oracle_check(tab, labels, threads)
         if args.output_count == 1 and not args.label_negation:
             result["cpu_baseline_optimized"] = cpu_baseline_optimized(smp, labels, threads)
             if args.cpu_sweep_rows:
