@@ -643,14 +643,19 @@ def cpu_port_sweep(smp, labels, cores, rows):
 def sq_profile_path(args):
     """The PMC instruction-count summary matching this run's shape (launch
     mode, labels, outputs per row, fixed-base width, variants):
-    profiles/r02_pmc_sq_[multi_]L<labels>_k<outputs>_w<bits>[_neg][_K<k>].json."""
+    profiles/r0N_pmc_sq_[multi_]L<labels>_k<outputs>_w<bits>[_neg][_K<k>].json,
+    this round's (r03) when it has one, else round 2's."""
     kdesc = "1-%d" % args.outputs_max if args.outputs_max else str(args.outputs_per_row)
-    name = "r02_pmc_sq_%sL%d_k%s_w%d" % ("multi_" if args.launch == "multi" else "", args.labels, kdesc, args.fb_bits)
+    name = "pmc_sq_%sL%d_k%s_w%d" % ("multi_" if args.launch == "multi" else "", args.labels, kdesc, args.fb_bits)
     if args.label_negation:
         name += "_neg"
     if args.output_count != 1:
         name += "_K%d" % args.output_count
-    return os.path.join(ROOT, "profiles", name + ".json")
+    for rnd in ("r03", "r02"):
+        path = os.path.join(ROOT, "profiles", "%s_%s.json" % (rnd, name))
+        if os.path.exists(path):
+            return path
+    return os.path.join(ROOT, "profiles", "r03_%s.json" % name)
 
 
 def alu_roofline(path, value_per_gpu, multi=False):
@@ -792,14 +797,14 @@ def main():
                     help="GPU_MAX_HW_QUEUES for the e2e child; 0 = the environment's (HIP default 4)")
     ap.add_argument("--e2e-timeout", type=int, default=600)
     ap.add_argument("--pmc-summary", default="",
-                    help="HBM traffic summary (default: profiles/r02_pmc_hbm_multi.json with --launch multi, "
+                    help="HBM traffic summary (default: profiles/r03_pmc_hbm_multi.json with --launch multi, "
                          "profiles/r02_pmc_hbm_k_shared_secret.json with --launch batches)")
     ap.add_argument("--pmc-sq", default="", help="SQ counter summary (default: the file matching this run's shape)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) for the barrier/max; gloo to rehearse "
                     "several ranks on one GPU")
     args = ap.parse_args()
     if not args.pmc_summary:
-        args.pmc_summary = os.path.join(ROOT, "profiles", "r02_pmc_hbm_multi.json" if args.launch == "multi"
+        args.pmc_summary = os.path.join(ROOT, "profiles", "r03_pmc_hbm_multi.json" if args.launch == "multi"
                                         else "r02_pmc_hbm_k_shared_secret.json")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

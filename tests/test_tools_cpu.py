@@ -46,7 +46,7 @@ def test_committed_multi_profiles_have_bench_keys():
     """The summaries bench.py reads by default with --launch multi (the
     default): k_scan_multi's VALU count per launch with its rows, and its HBM
     traffic per row."""
-    sq = json.load(open(os.path.join(ROOT, "profiles", "r02_pmc_sq_multi_L0_k2_w26.json")))
+    sq = json.load(open(os.path.join(ROOT, "profiles", "r03_pmc_sq_multi_L0_k2_w26.json")))
     assert sq["per_kernel"]["k_scan_multi"]["SQ_INSTS_VALU"] > 0 and sq["multi_rows_per_launch"] > 0
-    hbm = json.load(open(os.path.join(ROOT, "profiles", "r02_pmc_hbm_multi.json")))
+    hbm = json.load(open(os.path.join(ROOT, "profiles", "r03_pmc_hbm_multi.json")))
     assert hbm["multi_hbm_bytes_per_row"] > 0
