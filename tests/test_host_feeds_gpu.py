@@ -168,3 +168,22 @@ def test_host_e2e_tool_config5_shape(torch, keys, tmp_path):  # noqa: F811
         assert res["matches"] == res["planted"] == 1400
         assert res["label_indices_planted"] == 16
         assert res["launches"] >= 3
+
+
+def test_host_error_mid_query_then_pool_reuse(table16, keys):  # noqa: F811
+    """A 63-byte tweak in a late chunk of a 3-thread query: the query fails
+    with an error (the reference reads 64 bytes regardless,
+    src/cudasp_extension.cu:59-75) while the other threads' batches are in
+    flight; freeing the global state drains them and parks the feed, and the
+    next query on the pooled resources emits exactly the oracle's rows."""
+    from cudasp_amd import CudaspError, cudasp_scan, pool_size
+    rows, expected = table16
+    scan, spend, labels = keys
+    bad = list(rows[:12000])
+    t = bad[9000]
+    bad[9000] = (t[0], t[1], t[2][:63], t[3])
+    with pytest.raises(CudaspError):
+        cudasp_scan(bad, scan, spend, labels, batch_size=2500, threads=3)
+    assert pool_size() > 0
+    out = cudasp_scan(rows, scan, spend, labels, batch_size=2500, threads=3)
+    assert _heights(out) == expected
