@@ -623,6 +623,40 @@ def cpu_baseline_optimized(smp, labels, threads):
                 sample_matches=int(flags.sum()))
 
 
+def cpu_baseline_openssl(smp, labels, threads, rows):
+    """`openssl`: the reference's row pipeline on OpenSSL 3's secp256k1
+    arithmetic (tools/cpu_openssl) -- the third-party library baseline
+    SURVEY.md §8(d) names while libsecp256k1 is absent from the image --
+    timed on the first `rows` rows of the sample and the same cores; flags
+    compared with the GPU's.  OpenSSL's generic prime-field EC code is not
+    libsecp256k1 (~10x slower per SURVEY.md §8(d)), hence the label."""
+    import ctypes
+    lib_path = os.path.join(ROOT, "tools", "cpu_openssl", "libcudasp_cpu_openssl.so")
+    if not os.path.exists(lib_path):
+        return dict(error="tools/cpu_openssl not built")
+    lib = ctypes.CDLL(lib_path)
+    P = ctypes.c_void_p
+    lib.cudasp_cpu_openssl_scan.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint32, P, P, P, P, ctypes.c_int]
+    lib.cudasp_cpu_openssl_scan.restype = ctypes.c_int
+    n = min(rows, smp["rows"])
+    used = int(smp["offs"][n - 1]) + int(smp["lens"][n - 1]) if n else 0
+    flags = np.zeros(n, dtype=np.uint8)
+    outs = np.ascontiguousarray(smp["outs"][:used], dtype=np.int64)
+    lab = b"".join(labels) if labels else None
+    t0 = time.perf_counter()
+    rc = lib.cudasp_cpu_openssl_scan(SCAN_KEY, SPEND_KEY, lab, len(labels), smp["tweaks"].ctypes.data, n,
+                                     outs.ctypes.data if outs.size else None, smp["offs"].ctypes.data,
+                                     smp["lens"].ctypes.data, flags.ctypes.data, threads)
+    dt = time.perf_counter() - t0
+    if rc < 0:
+        return dict(error="cudasp_cpu_openssl_scan returned %d" % rc)
+    return dict(value=n / dt, unit="tx/s", cores=threads, kind="openssl",
+                sample="first %d rows of the rank-0 table, %d labels, OpenSSL 3 EC_POINT_mul/EC_POINT_add "
+                       "(NID_secp256k1) + EVP SHA-256 on %d threads (tools/cpu_openssl)" % (n, len(labels), threads),
+                seconds=round(dt, 3), rows_refused=rc,
+                flags_match_gpu=bool(np.array_equal(flags, smp["gpu_flags"][:n])), sample_matches=int(flags.sum()))
+
+
 def cpu_port_sweep(smp, labels, cores, rows):
     """port-optimized at a few thread counts (cores/4, cores/2, cores; never
     more threads than the allotted cores) over the first `rows` rows of the
@@ -787,6 +821,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this process may use")
     ap.add_argument("--cpu-sweep-rows", type=int, default=200000,
                     help="rows of the port-optimized thread sweep (0 = no sweep)")
+    ap.add_argument("--cpu-openssl-rows", type=int, default=100000,
+                    help="rows of the OpenSSL baseline (about 1 ms per row per thread; 0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layout-probe", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -973,6 +1009,8 @@ def main():
             result["cpu_baseline_optimized"] = cpu_baseline_optimized(smp, labels, threads)
             if args.cpu_sweep_rows:
                 result["cpu_baseline_optimized_sweep"] = cpu_port_sweep(smp, labels, use, args.cpu_sweep_rows)
+            if args.cpu_openssl_rows:
+                result["cpu_baseline_openssl"] = cpu_baseline_openssl(smp, labels, threads, args.cpu_openssl_rows)
         del smp
     for s in scanners:
         s.close()

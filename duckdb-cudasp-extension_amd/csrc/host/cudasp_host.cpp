@@ -516,7 +516,8 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
     FeedSlot& s = r.slots[f.open];
     switch (s.state) {
       case SLOT_FREE: {
-        const size_t want_words = std::max((size_t)(f.words_per_row * r.cap_rows), nwords);
+        const size_t want_words = std::max(
+            std::min((size_t)(f.words_per_row * r.cap_rows), (size_t)UINT32_MAX * f.ow), nwords);
         const size_t want_tx = std::max((size_t)(f.txid_per_row * r.cap_rows), ntx);
         if (!s.allocated || s.outputs_cap < want_words || s.txid_bytes.size() < want_tx) {
           s.state = SLOT_BUSY;
@@ -535,7 +536,12 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
         continue;
       }
       case SLOT_FILLING: {
-        if (s.rows + nrows <= r.cap_rows && s.words + nwords <= s.outputs_cap &&
+        // output offsets are u32 (as the reference's h_output_offsets)
+        const bool offs_fit = (s.words + nwords) / f.ow <= UINT32_MAX;
+        if (!offs_fit && s.rows == 0)
+          return feed_fail(f, host_fail(CUDASP_ERR_CAPACITY, "a chunk of %u rows holds %zu outputs: more than a "
+                                        "batch's u32 output offsets address", nrows, nwords / f.ow));
+        if (offs_fit && s.rows + nrows <= r.cap_rows && s.words + nwords <= s.outputs_cap &&
             s.txid_used + ntx <= s.txid_bytes.size()) {
           out->slot = &s;
           out->row0 = s.rows;
@@ -975,6 +981,9 @@ void feeds_release(cudasp_tf_global& g) {
     {
       DeviceSet dg(r->device);
       for (int k = 0; k < r->nstreams; k++) ok = cudasp_scanner_sync(r->scanners[k]) == CUDASP_OK && ok;
+      // a launch that failed after queueing its uploads left them on the
+      // null stream, still reading the slot's pinned buffers
+      if (!ok) (void)hipStreamSynchronize((hipStream_t)0);
     }
     fp.reset();
     if (ok)
