@@ -7,15 +7,18 @@ Contract (see DESIGN.md "Measurement"):
   torch.distributed.run; ranks read RANK / LOCAL_RANK / WORLD_SIZE.
 
 Workload (BASELINE.json metric "tx/sec through cudasp_scan on 32M-row tweak
-table at 1/2/4/8 MI355X", configs[3]): ONE 32.7M-row synthetic table, cut into
-batches of the reference's default batch_size 300000 at every N (BASELINE.md
-section 3 row 4); batch b is scanned by rank b mod N (the product's
-assignment, cudasp_assign_gpu; the reference round-robins its executor
-threads over GPUs, src/cudasp_extension.cu:523-529), so the total work is
-fixed as N grows (`--shard weak` gives every rank its own table instead).  At
-N > 1 a secondary line re-cuts the same table into equal batch counts per
-rank (balanced_batch_size) and reports it as `value_balanced`, never as the
-headline.  Each rank's batches are resident in HBM, tweak limbs
+table at 1/2/4/8 MI355X", configs[3]): ONE 32.7M-row synthetic table and the
+reference's default batch_size 300000 at every N (BASELINE.md section 3 row
+4).  Every GPU scans its contiguous 1/N share of the rows, batched at
+batch_size with one partial last batch (`--shard rows`): that is how batches
+form per GPU in the reference (each executor thread batches the rows it is
+handed, src/cudasp_extension.cu:416-418, and threads round-robin over the
+GPUs, :523-529) and in the product's host (one device feed per GPU), so the
+total work is fixed as N grows.  At N > 1 a secondary line cuts the same table
+into global 300000-row batches dealt round-robin (batch b on rank b mod N,
+cudasp_assign_gpu) and reports it as `value_roundrobin`, never as the
+headline (`--shard roundrobin` makes it the headline; `--shard weak` gives
+every rank its own table).  Each rank's batches are resident in HBM, tweak limbs
 column-major per batch.  A step is one pass of the hot path over the rank's
 batches: by default (`--launch multi`) one cudasp_scan_device_batches call
 over all of them -- one persistent kernel (k_scan_multi) runs both stages
@@ -254,7 +257,7 @@ def shard_first_row(rank, rows_per_rank):
 
 
 def balanced_batch_size(rows, world, cap=300_000):
-    """The bench's default batch_size for the round-robin table: the largest
+    """`--batch-size 0` (not the default): the largest
     size <= cap (the reference's default batch_size) whose batch count is a
     multiple of `world`, so that round-robin gives every rank the same number
     of batches.  At N = 1 this is cap itself (109 batches of 300000 rows);
@@ -269,15 +272,39 @@ def balanced_batch_size(rows, world, cap=300_000):
     return -(-rows // nb)
 
 
+SHARD_DESC = dict(
+    rows="every GPU scans its contiguous 1/N share of the rows in batch_size-row batches (BASELINE.json "
+         "configs[3]; per-GPU batching as in the reference and the product host)",
+    roundrobin="global batch_size-row batches dealt round-robin over the ranks (batch b on rank b mod N)",
+    weak="every rank scans its own table (weak)")
+
+
+def rank_rows(rows, rank, world):
+    """A rank's contiguous share [first, last) of the table's rows (shares
+    differ by at most one row)."""
+    return rank * rows // world, (rank + 1) * rows // world
+
+
 def rank_batches(shard, rows, batch, rank, world, assign):
     """The (first global row, rows) batches a rank scans.
 
-    roundrobin (config 4, the default): ONE table of `rows` rows cut into
-    batch_size-row batches; batch b goes to rank assign(b, world), the
-    product's own assignment (cudasp_assign_gpu: b mod N, as the reference
-    round-robins its executor threads over GPUs, src/cudasp_extension.cu:523-529).
+    rows (config 4, the default): ONE table of `rows` rows; every GPU scans
+    its contiguous 1/N share, batched at batch_size rows with one partial
+    last batch.  That is how batches form per GPU both in the reference (each
+    executor thread batches the rows it was handed, `>= batch_size` at
+    src/cudasp_extension.cu:416-418, its remainder in the final call; threads
+    round-robin over the GPUs, :523-529, and DuckDB deals the table's row
+    groups over the threads) and in the product's host (one device feed per
+    GPU; the threads' chunks round-robin over the GPUs), and it is SURVEY.md
+    §8(e)'s "contiguous ranges".
+    roundrobin: the same table cut into global batch_size-row batches; batch b
+    goes to rank assign(b, world) (cudasp_assign_gpu: b mod N) -- whole
+    batches, so the largest share (14 of 109 at N = 8) sets the job time.
     weak: every rank scans its own `rows`-row table (global rows
     [rank * rows, (rank + 1) * rows))."""
+    if shard == "rows":
+        first, last = rank_rows(rows, rank, world)
+        return [(b, min(batch, last - b)) for b in range(first, last, batch)]
     if shard == "roundrobin":
         nb = (rows + batch - 1) // batch
         return [(b * batch, min(batch, rows - b * batch)) for b in range(nb) if assign(b, world) == rank]
@@ -789,15 +816,17 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rows", type=int, default=32_700_000,
-                    help="rows of the table (roundrobin) or of each rank's table (weak)")
-    ap.add_argument("--shard", choices=["roundrobin", "weak"], default="roundrobin",
-                    help="roundrobin: ONE table, batch b on rank b mod N (BASELINE configs[3], strong scaling); "
+                    help="rows of the table (rows, roundrobin) or of each rank's table (weak)")
+    ap.add_argument("--shard", choices=["rows", "roundrobin", "weak"], default="rows",
+                    help="rows: ONE table, every GPU scans its contiguous 1/N share in batch_size-row batches "
+                         "(BASELINE configs[3], strong scaling; the reference's and the host's per-GPU batching); "
+                         "roundrobin: ONE table cut into global batches, batch b on rank b mod N; "
                          "weak: every rank scans its own table")
     ap.add_argument("--batch-size", type=int, default=300_000,
                     help="rows per batch (the reference's default 300000, BASELINE.md section 3, at every N); "
                          "0 = balanced: the largest size <= 300000 giving every rank the same batch count")
-    ap.add_argument("--no-balanced", action="store_true",
-                    help="at N > 1, skip the secondary value_balanced line (equal batch counts per rank)")
+    ap.add_argument("--no-secondary", "--no-balanced", dest="no_secondary", action="store_true",
+                    help="at N > 1, skip the secondary value_roundrobin line (whole global batches dealt b mod N)")
     ap.add_argument("--labels", type=int, default=0)
     ap.add_argument("--output-count", type=int, default=1,
                     help="protocol variant: output indices k = 0..K-1 per row (1 = the reference)")
@@ -847,7 +876,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.batch_size <= 0:
-        args.batch_size = balanced_batch_size(args.rows, world) if args.shard == "roundrobin" else 300_000
+        args.batch_size = balanced_batch_size(args.rows, world) if args.shard != "weak" else 300_000
     if args.fb_bits in (22, 26):
         # the process default for every scanner and the synthetic-table
         # generator (read once by the library); 0 keeps the product default
@@ -958,15 +987,14 @@ def main():
     result = dict(
         metric=METRIC, value=value, unit="tx/s", n_gpus=world, steps=args.steps, warmup=args.warmup,
         ms_per_step=ms_per_step, higher_is_better=True,
-        scaling="strong" if args.shard == "roundrobin" else "weak", vs_baseline=None,
+        scaling="weak" if args.shard == "weak" else "strong", vs_baseline=None,
         dtype="u32", data="synthetic",
         config=dict(workload="%.1fM-row synthetic tweak table%s, %d labels, %s outputs/row, batch_size %d, "
                              "device-resident; %s" % (
-                                 args.rows / 1e6, "" if args.shard == "roundrobin" else " per rank", args.labels,
+                                 args.rows / 1e6, " per rank" if args.shard == "weak" else "", args.labels,
                                  ("1..%d (mean %.2f)" % (args.outputs_max, mean_k)) if args.outputs_max
                                  else str(args.outputs_per_row), args.batch_size,
-                                 "batches round-robin over the ranks (BASELINE.json configs[3])"
-                                 if args.shard == "roundrobin" else "every rank scans its own table (weak)"),
+                                 SHARD_DESC[args.shard]),
                     rows=args.rows, shard=args.shard, batch_size=args.batch_size, labels=args.labels,
                     output_count=args.output_count, label_negation=args.label_negation,
                     outputs_per_row=round(mean_k, 3), fixed_base_bits=args.fb_bits,
@@ -1012,34 +1040,31 @@ def main():
             if args.cpu_openssl_rows:
                 result["cpu_baseline_openssl"] = cpu_baseline_openssl(smp, labels, threads, args.cpu_openssl_rows)
         del smp
-    for s in scanners:
-        s.close()
 
-    # Secondary line at N > 1: the same table in equal batch counts per rank.
-    if world > 1 and args.shard == "roundrobin" and not args.no_balanced:
-        bb = balanced_batch_size(args.rows, world)
+    # Secondary line at N > 1: the same table and batch_size, cut into global
+    # batches dealt round-robin (whole batches: the largest share sets the
+    # job time).  Never the headline.
+    if world > 1 and args.shard == "rows" and multi and not args.no_secondary:
         del descs, tab
         torch.cuda.empty_cache()
-        btab = Table(lib, device, rank_batches("roundrobin", args.rows, bb, rank, world, assign_gpu), bb,
-                     args.outputs_per_row, labels, dev_stream=gen_stream, kmax=args.outputs_max)
-        bsc = Scanner(SCAN_KEY, SPEND_KEY, labels, max_rows=bb, device=device)
-        bsc.set_fixed_base_bits(args.fb_bits)
-        bdescs = multi_descs(btab)
-        btimes, _, _ = timed_steps(lambda ev=None: run_step_multi(btab, bsc, streams[0], bdescs, ev), args.steps,
-                                   args.warmup, device, barrier)
-        bfound = int(btab.match_count.sum().item())
-        bt, bfound, _, bexp = aggregate(world, args.dist_backend, float(np.sum(btimes)), bfound, 0, btab.expected)
-        result["value_balanced"] = args.rows * args.steps / bt
-        result["balanced"] = dict(batch_size=bb, batches=-(-args.rows // bb), ms_per_step=bt / args.steps * 1e3,
-                                  found=bfound, expected_planted=bexp,
-                                  note="secondary: the table re-cut so every rank gets the same batch count; the "
-                                       "headline `value` keeps batch_size %d at every N" % args.batch_size)
-        bsc.close()
-        del bdescs, btab
+        rtab = Table(lib, device, rank_batches("roundrobin", args.rows, args.batch_size, rank, world, assign_gpu),
+                     args.batch_size, args.outputs_per_row, labels, dev_stream=gen_stream, kmax=args.outputs_max)
+        rdescs = multi_descs(rtab)
+        rtimes, _, _ = timed_steps(lambda ev=None: run_step_multi(rtab, scanners[0], streams[0], rdescs, ev),
+                                   args.steps, args.warmup, device, barrier)
+        rfound = int(rtab.match_count.sum().item())
+        rt, rfound, _, rexp = aggregate(world, args.dist_backend, float(np.sum(rtimes)), rfound, 0, rtab.expected)
+        result["value_roundrobin"] = args.rows * args.steps / rt
+        result["roundrobin"] = dict(batch_size=args.batch_size, batches=-(-args.rows // args.batch_size),
+                                    batches_rank0=rtab.nb, ms_per_step=rt / args.steps * 1e3, found=rfound,
+                                    expected_planted=rexp, note="secondary: " + SHARD_DESC["roundrobin"])
+        del rdescs, rtab
         torch.cuda.empty_cache()
     else:
         del descs, tab
         torch.cuda.empty_cache()
+    for s in scanners:
+        s.close()
 
     if not args.no_e2e and args.output_count == 1 and not args.label_negation:
         # After the device-resident legs: rank 0 starts the end-to-end child

@@ -1,7 +1,12 @@
 """CPU, world_size 2 over gloo: the benchmark's multi-GPU sharding and
 cross-rank reduction, with the C oracle standing in for each rank's GPU scan.
 
-* roundrobin (BASELINE configs[3], the N > 1 headline): ONE table cut into
+* rows (BASELINE configs[3], the bench default): ONE table, every rank scans
+  its contiguous 1/N share of the rows in batch_size-row batches (a partial
+  last batch per rank) -- the per-GPU batching of the reference's executor
+  threads and of the product host's device feeds.  The ranks' rows must
+  partition the table and the union of their matches equal a single scan.
+* roundrobin (the N > 1 secondary line): ONE table cut into
   batch_size-row batches, batch b scanned by rank cudasp_assign_gpu(b, N) --
   the product's own assignment function from libcudasp_amd.so (host-only
   code, the round-robin of src/cudasp_extension.cu:523-529).  The ranks'
@@ -59,7 +64,7 @@ def _worker(rank, world, port, shard, q):
     _paths()
     import bench
     from cudasp_amd import assign_gpu
-    rows = ROWS if shard == "roundrobin" else ROWS_PER_RANK
+    rows = ROWS_PER_RANK if shard == "weak" else ROWS
     batches = bench.rank_batches(shard, rows, BATCH, rank, world, assign_gpu)
     global_rows = [g0 + i for g0, m in batches for i in range(m)]
     flags, planted = _scan_rows(global_rows)
@@ -111,6 +116,43 @@ def test_two_rank_roundrobin_equals_single_scan():
     assert found == flagged == int(flags_all.sum()) == planted_all == expected
 
 
+def test_two_rank_row_shares_equal_single_scan():
+    t, found, flagged, expected, gathered = _run("rows")
+    assert gathered[0] == list(range(ROWS // 2)) and gathered[1] == list(range(ROWS // 2, ROWS))
+    flags_all, planted_all = _scan_rows(list(range(ROWS)))
+    assert t == 2.0
+    assert found == flagged == int(flags_all.sum()) == planted_all == expected
+
+
+def test_row_shares_cover_config4_table():
+    """The default bench shape: 32.7M rows over 1, 2, 4 and 8 ranks with
+    batch_size 300000 at every N: contiguous shares partition the table,
+    differ by at most one row, and every batch holds <= 300000 rows with only
+    each rank's last batch short; at N = 1 the batches are the round-robin
+    cut's (109 full batches)."""
+    _paths()
+    import bench
+    from cudasp_amd import assign_gpu
+    rows, batch = 32_700_000, 300_000
+    assert bench.rank_batches("rows", rows, batch, 0, 1, assign_gpu) == \
+        bench.rank_batches("roundrobin", rows, batch, 0, 1, assign_gpu)
+    for world in (1, 2, 3, 4, 8):
+        per = [bench.rank_batches("rows", rows, batch, r, world, assign_gpu) for r in range(world)]
+        covered = []
+        for p in per:
+            assert all(m == batch for _, m in p[:-1]) and 0 < p[-1][1] <= batch
+            for (g0, m), (g1, _) in zip(p, p[1:]):
+                assert g1 == g0 + m
+            covered.append((p[0][0], p[-1][0] + p[-1][1]))
+        assert covered[0][0] == 0 and covered[-1][1] == rows
+        assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+        shares = [e - b for b, e in covered]
+        assert max(shares) - min(shares) <= 1
+    # N = 8: 4,087,500 rows per GPU = 13 full batches + 187,500
+    p = bench.rank_batches("rows", rows, batch, 7, 8, assign_gpu)
+    assert len(p) == 14 and p[-1][1] == 187_500
+
+
 def test_two_rank_weak_shards_equal_single_scan():
     t, found, flagged, expected, gathered = _run("weak")
     assert gathered[0] == list(range(ROWS_PER_RANK))
@@ -138,7 +180,7 @@ def test_rank_batches_cover_config4_table():
 
 
 def test_balanced_batch_size_equal_rank_shares():
-    """The bench's default batch_size: 300000 at N = 1 (the reference's
+    """`--batch-size 0` (balanced): 300000 at N = 1 (the reference's
     default); at N = 2/4/8 every rank gets the same number of batches, the
     batches cover the table exactly, and rank row counts differ by less than
     one batch (only the short last batch differs)."""
