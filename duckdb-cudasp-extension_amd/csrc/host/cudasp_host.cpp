@@ -63,7 +63,12 @@ constexpr uint64_t TWEAK_KEY_SIZE = 64;  // CudaspScanBindData::TWEAK_KEY_SIZE
 constexpr uint64_t SCALAR_SIZE = 32;     // CudaspScanBindData::SCALAR_SIZE
 constexpr uint32_t XONLY_SIZE = 32;      // full_x outputs: x-only keys
 constexpr int FEED_MAX_STREAMS = 4;
-constexpr int FEED_MAX_SLOTS = FEED_MAX_STREAMS + 2;
+// A streaming feed (one persistent kernel, cudasp_stream_*) keeps more slots
+// in flight: the kernel's waves hold up to ~1.2M rows at once in 6-row
+// pieces, so 8 slots of 300k rows keep published work ahead of them while
+// the executor threads fill the next ones.
+constexpr int FEED_STREAM_SLOTS = 8;
+constexpr int FEED_MAX_SLOTS = FEED_STREAM_SLOTS > FEED_MAX_STREAMS + 2 ? FEED_STREAM_SLOTS : FEED_MAX_STREAMS + 2;
 // Rows resident on the GPU at once in k_scan_multi launches of 4 rows per
 // thread: 256 CUs x 4 SIMDs x 3 waves x 64 lanes x 4 rows.
 constexpr uint64_t GPU_FILL_ROWS = 786432;
@@ -185,6 +190,7 @@ struct FeedSlot {
   size_t txid_used = 0;  // txid bytes reserved
   int writers = 0;       // reservations still copying
   int stream = 0;        // stream (scanner) of its launch
+  uint64_t seq = 0;      // streaming feed: the batch's sequence number in the stream
 };
 
 // The GPU resources of a device feed, kept in a process-wide pool between
@@ -195,8 +201,22 @@ struct FeedRes {
   int nstreams = 0;
   cudasp_scanner* scanners[FEED_MAX_STREAMS] = {};
   FeedSlot slots[FEED_MAX_SLOTS];
-  int nslots() const { return nstreams + 2; }
+  // Streaming feed: one scanner, one persistent kernel (cudasp_stream_*)
+  // reading the slots' coherent pinned buffers in place.  Buffers it
+  // outgrows are freed only after the stream's kernel has ended (freeing
+  // device or pinned memory waits for the device, hence for that kernel).
+  cudasp_stream* stream = nullptr;
+  uint32_t stream_blocks = 0;
+  std::vector<void*> stale_host, stale_dev;
+  int nslots() const { return stream ? FEED_STREAM_SLOTS : nstreams + 2; }
 };
+
+void free_stale(FeedRes& r) {
+  for (void* p : r.stale_host) (void)hipHostFree(p);
+  for (void* p : r.stale_dev) (void)hipFree(p);
+  r.stale_host.clear();
+  r.stale_dev.clear();
+}
 
 void free_slot(FeedSlot& s) {
   void* host[] = {s.h_tweaks, s.h_offs, s.h_lens, s.h_flags, s.h_outputs};
@@ -212,8 +232,13 @@ void free_slot(FeedSlot& s) {
 
 void release_res(FeedRes* r) {
   if (!r) return;
+  if (r->stream) {
+    cudasp_stream_destroy(r->stream);  // closes it and waits for its kernel
+    r->stream = nullptr;
+  }
   {
     DeviceSet dg(r->device);
+    free_stale(*r);
     for (int k = 0; k < r->nstreams; k++)
       if (r->scanners[k]) (void)cudasp_scanner_sync(r->scanners[k]);
     for (FeedSlot& s : r->slots) free_slot(s);
@@ -227,11 +252,12 @@ constexpr size_t POOL_MAX = 64;
 std::mutex g_pool_mu;
 std::vector<FeedRes*> g_pool;
 
-FeedRes* pool_take(int device, uint32_t cap_rows, int nstreams) {
+FeedRes* pool_take(int device, uint32_t cap_rows, int nstreams, uint32_t stream_blocks) {
   std::lock_guard<std::mutex> lock(g_pool_mu);
   for (size_t i = 0; i < g_pool.size(); i++) {
     FeedRes* r = g_pool[i];
-    if (r->device == device && r->cap_rows == cap_rows && r->nstreams == nstreams) {
+    if (r->device == device && r->cap_rows == cap_rows && r->nstreams == nstreams &&
+        (r->stream ? r->stream_blocks : 0u) == stream_blocks) {
       g_pool[i] = g_pool.back();
       g_pool.pop_back();
       return r;
@@ -268,6 +294,8 @@ unsigned pinned_flags() {
 // Pinned/device buffers of a slot for cap_rows rows, at least `words` output
 // words and `txid` txid bytes.  Called with the slot owned by the caller
 // (state BUSY): no reservation, copy or launch touches it.
+int prepare_slot_streaming(FeedRes& r, FeedSlot& s, size_t words, size_t txid);
+
 int prepare_slot(FeedSlot& s, int device, uint32_t cap_rows, size_t words, size_t txid) {
   DeviceSet dg(device);
   if (!s.allocated) {
@@ -296,6 +324,42 @@ int prepare_slot(FeedSlot& s, int device, uint32_t cap_rows, size_t words, size_
     s.h_outputs = nullptr;
     s.outputs_cap = 0;
     HOST_HIP(hipHostMalloc((void**)&s.h_outputs, cap * sizeof(int64_t), pinned_flags()));
+    s.outputs_cap = cap;
+  }
+  if (txid > s.txid_bytes.size()) s.txid_bytes.resize(txid);
+  return CUDASP_OK;
+}
+
+// A streaming feed's slot: coherent pinned buffers the kernel reads in place
+// (cudasp_host_alloc) and, with labels, the device mirror of the outputs.
+// Nothing is freed while the feed's kernel may run: outgrown buffers wait in
+// the feed's stale lists.
+int prepare_slot_streaming(FeedRes& r, FeedSlot& s, size_t words, size_t txid) {
+  DeviceSet dg(r.device);
+  const size_t n = r.cap_rows;
+  auto host = [&](void** p, size_t bytes) -> int {
+    const int rc = cudasp_host_alloc(p, bytes);
+    return rc == CUDASP_OK ? rc : host_fail(rc, "pinned slot allocation failed: %s", cudasp_last_error());
+  };
+  if (!s.allocated) {
+    int rc = host((void**)&s.h_tweaks, n * 64);
+    if (rc == CUDASP_OK) rc = host((void**)&s.h_offs, n * 4);
+    if (rc == CUDASP_OK) rc = host((void**)&s.h_lens, n * 4);
+    if (rc == CUDASP_OK) rc = host((void**)&s.h_flags, n);
+    if (rc != CUDASP_OK) return rc;
+    s.txid_off.resize(n);
+    s.txid_size.resize(n);
+    s.heights.resize(n);
+    s.allocated = true;
+  }
+  if (words > s.outputs_cap) {
+    size_t cap = s.outputs_cap ? s.outputs_cap : 4096;
+    while (cap < words) cap *= 2;
+    if (s.h_outputs) r.stale_host.push_back(s.h_outputs);
+    s.h_outputs = nullptr;
+    s.outputs_cap = 0;
+    const int rc = host((void**)&s.h_outputs, cap * sizeof(int64_t));
+    if (rc != CUDASP_OK) return rc;
     s.outputs_cap = cap;
   }
   if (txid > s.txid_bytes.size()) s.txid_bytes.resize(txid);
@@ -353,6 +417,10 @@ struct cudasp_tf_global {
   std::unique_ptr<std::mutex[]> feed_create_mu;
   int hw_queues = 0;  // GPU_MAX_HW_QUEUES at init (HIP's default 4 when unset)
   int max_streams_per_device = 0;
+  // Streaming feeds (one persistent kernel per feed, cudasp_stream_*): with
+  // the default options and one feed per device; CUDASP_TF_MODE=launch
+  // selects the per-slot launches.
+  bool streaming = false;
 };
 
 struct cudasp_tf_local {
@@ -387,7 +455,31 @@ int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   lk.unlock();
   const double t0 = now_s();
   int rc = CUDASP_OK;
-  {
+  if (r.stream) {
+    // Streaming feed: publish the slot to the feed's kernel, which reads it
+    // in place (no copies, no launch).  With labels the kernel copies each
+    // row's outputs to the slot's device mirror, grown here (the old one is
+    // freed after the kernel ends).
+    DeviceSet dg(r.device);
+    if (f.g->bind->label_keys_data.size() && words > s.d_outputs_cap) {
+      if (s.d_outputs) r.stale_dev.push_back(s.d_outputs);
+      s.d_outputs = nullptr;
+      s.d_outputs_cap = 0;
+      if (hipMalloc((void**)&s.d_outputs, s.outputs_cap * sizeof(int64_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        rc = host_fail(CUDASP_ERR_HIP, "outputs mirror of %zu words on device %d: allocation failed", s.outputs_cap,
+                       r.device);
+      } else {
+        s.d_outputs_cap = s.outputs_cap;
+      }
+    }
+    if (rc == CUDASP_OK) {
+      rc = cudasp_stream_publish(r.stream, s.h_tweaks, s.h_outputs, s.h_offs, s.h_lens, n, s.h_flags, s.d_outputs,
+                                 &s.seq);
+      if (rc != CUDASP_OK)
+        rc = host_fail(rc, "cudasp_scan batch of %u rows on device %d failed: %s", n, r.device, cudasp_last_error());
+    }
+  } else {
     std::lock_guard<std::mutex> sl(f.stream_mu[s.stream]);
     cudasp_scanner* sc = r.scanners[s.stream];
     hipStream_t st = (hipStream_t)cudasp_internal_scanner_stream(sc);
@@ -451,9 +543,18 @@ int harvest_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   lk.unlock();
   const double t0 = now_s();
   hipError_t e;
+  std::string stream_err;
   {
     DeviceSet dg(f.res->device);
-    e = hipEventSynchronize(s.done);
+    if (f.res->stream) {
+      e = hipSuccess;
+      if (cudasp_stream_wait(f.res->stream, s.seq) != CUDASP_OK) {
+        e = hipErrorUnknown;
+        stream_err = cudasp_last_error();
+      }
+    } else {
+      e = hipEventSynchronize(s.done);
+    }
   }
   const double waited = now_s() - t0;
   if (e == hipSuccess) {
@@ -472,7 +573,7 @@ int harvest_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   f.cv.notify_all();
   if (e != hipSuccess)
     return feed_fail(f, host_fail(CUDASP_ERR_HIP, "batch on device %d failed: %s", f.res->device,
-                                  hipGetErrorString(e)));
+                                  stream_err.empty() ? hipGetErrorString(e) : stream_err.c_str()));
   return CUDASP_OK;
 }
 
@@ -522,7 +623,8 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
         if (!s.allocated || s.outputs_cap < want_words || s.txid_bytes.size() < want_tx) {
           s.state = SLOT_BUSY;
           lk.unlock();
-          const int rc = prepare_slot(s, r.device, r.cap_rows, want_words, want_tx);
+          const int rc = r.stream ? prepare_slot_streaming(r, s, want_words, want_tx)
+                                  : prepare_slot(s, r.device, r.cap_rows, want_words, want_tx);
           lk.lock();
           s.state = SLOT_FREE;
           f.cv.notify_all();
@@ -564,7 +666,8 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
           f.txid_per_row = std::max(f.txid_per_row, (double)ntx / r.cap_rows);
           s.state = SLOT_BUSY;
           lk.unlock();
-          const int rc = prepare_slot(s, r.device, r.cap_rows, nwords, ntx);
+          const int rc = r.stream ? prepare_slot_streaming(r, s, nwords, ntx)
+                                  : prepare_slot(s, r.device, r.cap_rows, nwords, ntx);
           lk.lock();
           s.state = SLOT_FILLING;
           f.cv.notify_all();
@@ -636,6 +739,15 @@ int feeds_flush(cudasp_tf_global& g) {
     }
     if (rc == CUDASP_OK && f.error != CUDASP_OK) rc = feed_error(f);
   }
+  // streaming feeds: every batch is done; close the streams so their kernels
+  // end (and the streams are ready for the next query)
+  for (auto& fp : g.feeds) {
+    if (!fp || !fp->res->stream) continue;
+    DeviceSet dg(fp->res->device);
+    const int r2 = cudasp_stream_finish(fp->res->stream);
+    if (r2 != CUDASP_OK && rc == CUDASP_OK) rc = feed_fail(*fp, host_fail(r2, "%s", cudasp_last_error()));
+    free_stale(*fp->res);
+  }
   return rc;
 }
 
@@ -651,7 +763,15 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
   const auto* spend = (const uint8_t*)b.spend_public_key_data.data();
   const auto* labels = (const uint8_t*)b.label_keys_flat.data();
   const auto nlabels = (uint32_t)b.label_keys_data.size();
-  FeedRes* r = pool_take(device, cap_rows, g.feed_streams);
+  // a streaming feed's grid: its share of the device's wave slots
+  uint32_t blocks = 0;
+  if (g.streaming) {
+    int cus = 0, on_dev = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    for (int d : g.device_map) on_dev += d == device;
+    blocks = (uint32_t)(cus * 3 / (on_dev > 0 ? on_dev : 1));
+  }
+  FeedRes* r = pool_take(device, cap_rows, g.streaming ? 1 : g.feed_streams, blocks);
   if (r) {
     for (int k = 0; k < r->nstreams; k++) {
       int rc = cudasp_scanner_set_keys(r->scanners[k], scan, spend, labels, nlabels);
@@ -665,10 +785,21 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
     r = new FeedRes();
     r->device = device;
     r->cap_rows = cap_rows;
-    r->nstreams = g.feed_streams;
-    for (int k = 0; k < r->nstreams; k++) {
+    r->nstreams = g.streaming ? 1 : g.feed_streams;
+    for (int k = 0; k < FEED_MAX_STREAMS; k++) {
+      if (k >= r->nstreams) break;
       int rc = cudasp_scanner_create(device, scan, spend, labels, nlabels, cap_rows, &r->scanners[k]);
       if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(r->scanners[k], &b.opt);
+      if (rc == CUDASP_OK && k == 0 && g.streaming) {
+        rc = cudasp_stream_create(r->scanners[0], blocks, &r->stream);
+        if (rc == CUDASP_OK) {
+          r->stream_blocks = blocks;
+        } else if (rc == CUDASP_ERR_INVALID_ARG) {  // a width the streaming kernel lacks: per-slot launches
+          r->stream = nullptr;
+          r->nstreams = g.feed_streams;
+          rc = CUDASP_OK;
+        }
+      }
       if (rc != CUDASP_OK) {
         std::string msg = cudasp_last_error();
         release_res(r);
@@ -980,6 +1111,12 @@ void feeds_release(cudasp_tf_global& g) {
     bool ok = f.error == CUDASP_OK;
     {
       DeviceSet dg(r->device);
+      // a streaming feed's kernel runs until its stream is closed: close it
+      // (an aborted query's published batches finish first)
+      if (r->stream) {
+        ok = cudasp_stream_finish(r->stream) == CUDASP_OK && ok;
+        free_stale(*r);
+      }
       for (int k = 0; k < r->nstreams; k++) ok = cudasp_scanner_sync(r->scanners[k]) == CUDASP_OK && ok;
       // a launch that failed after queueing its uploads left them on the
       // null stream, still reading the slot's pinned buffers
@@ -1134,6 +1271,16 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
     feeds_per_device = std::max(feeds_per_device, m);
   }
   g->feed_streams = feed_streams_for(b->batch_size, g->hw_queues, feeds_per_device);
+  {
+    const char* mode = getenv("CUDASP_TF_MODE");
+    // one feed per device: a persistent kernel holds its hardware queue for
+    // the whole query, so two feeds' kernels on one device could land on one
+    // queue (HIP shares queues among streams) and the second would wait for
+    // the first to end -- logical GPUs sharing a device (CUDASP_TF_DEVICE_MAP)
+    // take the per-slot launches
+    g->streaming = !(mode && !strcmp(mode, "launch")) && b->opt.output_count == 1 && feeds_per_device == 1;
+    if (g->streaming) g->feed_streams = 1;
+  }
   g->feeds.resize(g->num_gpus);
   g->feed_ptr.reset(new std::atomic<Feed*>[g->num_gpus]);
   for (int lg = 0; lg < g->num_gpus; lg++) g->feed_ptr[lg].store(nullptr);
@@ -1176,6 +1323,7 @@ int cudasp_tf_get_stats(cudasp_tf_global* g, cudasp_tf_stats* out) {
     if (!fp) continue;
     std::lock_guard<std::mutex> lock(fp->mu);
     out->feeds++;
+    out->streaming_feeds += fp->res->stream ? 1u : 0u;
     out->launches += fp->launches;
     out->rows += fp->rows;
     out->harvest_wait_s += fp->harvest_wait_s;

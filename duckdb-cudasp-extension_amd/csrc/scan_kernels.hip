@@ -15,18 +15,23 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <memory>
 #include <string>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/cudasp_abi.h"
 #include "scan_prepare.hpp"
 #include "scan_multi.hpp"
+#include "scan_stream.hpp"
 
 using namespace cudasp;
 
@@ -620,6 +625,378 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
     g_multi_trace[wave * 4 + 3] = trace_rows;
   }
 #endif
+}
+
+// ------------------------------------------------------------ streaming scan
+// k_scan_stream: k_scan_multi's pipelined body over batches the host publishes
+// while the kernel runs (scan_stream.hpp: zero-copy inputs from pinned host
+// memory, ticket claims and batch lookups in a device mirror of the host's
+// descriptor ring, per-batch completion words).
+
+__device__ __forceinline__ uint32_t sys_load_u32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t sys_load_u64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t dev_load_u32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t dev_load_u64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+}
+
+// A wave-row's batch, wave-uniform.
+struct StreamRow {
+  const uint8_t* rows;
+  const int64_t* outputs;
+  const uint32_t* offs;
+  const uint32_t* lens;
+  uint8_t* flags;
+  int64_t* mirror;
+  uint64_t first_wr;
+  uint32_t n;
+  uint32_t nwr;
+  uint32_t b;
+};
+
+// The batch holding published wave-row w, searched forward from `hint` (the
+// batch of an earlier wave-row of this wave's tickets).  A ring entry holding
+// another sequence number was reused: that batch is complete, hence before
+// w's (w is this wave's and not done yet).  Bounded: the walk never passes
+// the ring twice.
+__device__ __forceinline__ uint32_t stream_batch_of(StreamDev* dev, uint32_t hint, uint64_t w) {
+  uint32_t b = hint;
+  for (uint32_t i = 0; i < 2 * STREAM_RING; i++, b++) {
+    const StreamBatch* d = &dev->desc[b % STREAM_RING];
+    if (dev_load_u64(&d->seq) != b) continue;
+    if (w < dev_load_u64(&d->first_wr) + dev_load_u32(&d->nwr)) break;
+  }
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+}
+
+__device__ __forceinline__ StreamRow stream_row(StreamDev* dev, uint32_t& hint, uint64_t w) {
+  const uint32_t b = stream_batch_of(dev, hint, w);
+  hint = b;
+  const StreamBatch* d = &dev->desc[b % STREAM_RING];
+  StreamRow r;
+  const auto ptr = [&](auto* const* f) {
+    using T = std::remove_reference_t<decltype(**f)>;
+    return reinterpret_cast<T*>(uniform_u64(dev_load_u64(reinterpret_cast<const uint64_t*>(f))));
+  };
+  r.rows = ptr(&d->rows);
+  r.outputs = ptr(&d->outputs);
+  r.offs = ptr(&d->offs);
+  r.lens = ptr(&d->lens);
+  r.flags = ptr(&d->flags);
+  r.mirror = ptr(&d->mirror);
+  r.first_wr = uniform_u64(dev_load_u64(&d->first_wr));
+  r.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)dev_load_u32(&d->n));
+  r.nwr = (uint32_t)__builtin_amdgcn_readfirstlane((int)dev_load_u32(&d->nwr));
+  r.b = b;
+  return r;
+}
+
+// Row of this lane in wave-row w (false: the padding of the batch's last
+// wave-row, which then reads batch row 0).
+__device__ __forceinline__ uint32_t stream_lane_row(const StreamRow& sr, uint64_t w, uint32_t lane, bool* active) {
+  const uint32_t r = (uint32_t)(w - sr.first_wr) * 64u + lane;
+  *active = r < sr.n;
+  return *active ? r : 0u;
+}
+
+// The poller (lane 0 of one wave per kernel): mirrors new batches of the
+// host's control block into the device state -- descriptors first, then the
+// counts behind an agent-scope release -- and `closed` after the last one.
+// Leaves once closed is mirrored, or after abandon_ticks without a change.
+__device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t abandon_ticks) {
+  uint32_t seen = dev_load_u32(&dev->pub);
+  uint64_t last = wall_clock64();
+  for (;;) {
+    // the control block is uncached host memory (MTYPE UC): relaxed
+    // system-scope loads read it fresh without invalidating any cache; the
+    // wait keeps `published` read after `closed`
+    const uint32_t cl = sys_load_u32(&ctrl->closed);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t pub = sys_load_u32(&ctrl->published);
+    const uint64_t now = wall_clock64();
+    if (pub != seen) {
+      uint64_t pub_wr = 0;
+      for (uint32_t b = seen; b != pub; b++) {
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(&ctrl->desc[b % STREAM_RING]);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(&dev->desc[b % STREAM_RING]);
+        StreamBatch d;
+        uint64_t* dw = reinterpret_cast<uint64_t*>(&d);
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(StreamBatch) / 8); i++) {
+          dw[i] = sys_load_u64(src + i);
+          __hip_atomic_store(dst + i, dw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // the rows mirrored so far (not the host's published_wr, which may
+        // already count a batch published after `pub` was read)
+        pub_wr = d.first_wr + d.nwr;
+      }
+      __hip_atomic_store(&dev->pub_wr, pub_wr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&dev->pub, pub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      seen = pub;
+      last = now;
+    }
+    if (cl) {  // `published` was read after `closed`: every batch is mirrored
+      __hip_atomic_store(&dev->closed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (now - last > abandon_ticks) return;
+    atomicAdd(&dev->stat[STREAM_STAT_POLLER_POLLS], 1ull);
+    __builtin_amdgcn_s_sleep(32);
+  }
+}
+
+// Flags of wave-rows base .. base + count - 1 into their pinned slots, then
+// each batch's completion: the wave's stores are complete before its
+// wave-rows count, and the wave whose count finishes a batch writes the
+// batch's done word.
+__device__ __forceinline__ void stream_emit(StreamCtrl* ctrl, StreamDev* dev, uint64_t base, int count,
+                                            uint32_t hint, uint32_t lane, uint32_t hits) {
+#pragma unroll 1
+  for (int j = 0; j < count; j++) {
+    const StreamRow sr = stream_row(dev, hint, base + (uint32_t)j);
+    bool active;
+    const uint32_t r = stream_lane_row(sr, base + (uint32_t)j, lane, &active);
+    // system-scope stores: written through to host memory whatever the
+    // caching type of the pinned pages
+    if (active)
+      __hip_atomic_store(sr.flags + r, (uint8_t)((hits >> j) & 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t e = sr.b % STREAM_RING;
+      const uint32_t before = atomicAdd(&dev->wr_done[e], 1u);
+      if (before + 1u == sr.nwr) {
+        __hip_atomic_store(&dev->wr_done[e], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->done[e], sr.b + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
+// Base compare of a row; with labels the row's outputs are first copied to
+// the device mirror (read once over PCIe; the label compares read the copy).
+__device__ __forceinline__ bool stream_base_match(const ScanConsts& k, const StreamRow& sr, uint32_t off,
+                                                  uint32_t len, bool active, bool mirror, const fe& x, int64_t v) {
+  if (!mirror) return outputs_match(k, sr.outputs, off, len, x, v);
+  if (!active) return false;
+  const uint32_t ow = k.full_x ? 4u : 1u;
+#pragma unroll 1
+  for (uint32_t q = off * ow; q < (off + len) * ow; q++) sr.mirror[q] = sr.outputs[q];
+  return outputs_match(k, sr.mirror, off, len, x, v);
+}
+
+template <int FBB>
+__global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtrl* ctrl, StreamDev* dev,
+                                                                    const int8_t* __restrict__ naf, ScanConsts k,
+                                                                    const uint32_t* __restrict__ fb,
+                                                                    const uint32_t* __restrict__ labels,
+                                                                    uint32_t* __restrict__ scr, uint32_t rmax,
+                                                                    uint64_t abandon_ticks) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const Scratch sc = SCAN_SCRATCH(scr, gridDim.x * blockDim.x, slot);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {  // one wave of the grid is the poller
+    if (lane == 0) stream_poll(ctrl, dev, abandon_ticks);
+    return;
+  }
+  const uint32_t workers = gridDim.x * (BLOCK / 64) - 1;
+  constexpr int PB = VB_SCRATCH_WORDS;
+  constexpr int LB = VB_SCRATCH_WORDS + PEND_WORDS * multi_pend_slots(true);
+  const int QF = LB + FW * (int)k.label_count * MULTI_RMAX;
+  const int QACC = QF + 2 * FW * MULTI_RMAX;
+  const bool mirror = k.label_count != 0;
+  // pieces of the pipelined schedule: P (F points pending), Q (labels pending)
+  uint64_t base_p = 0, base_q = 0;
+  int count_p = 0, count_q = 0;
+  uint32_t hint_p = 0, hint_q = 0, hint = 0, hits_q = 0;
+  // the wave's ticket (lane 0): wave-rows [tk, tk + tr), held since t_wait
+  bool have = false;
+  uint64_t tk = 0, t_wait = 0;
+  uint32_t tr = 0;
+  const uint64_t t_start = wall_clock64();
+  uint64_t busy = 0, pieces = 0, rows = 0;
+  uint32_t stop = 0;  // 2: closed and past the end, 3: abandoned; leave once drained
+  for (;;) {
+    const uint64_t t_it = wall_clock64();
+    // 0: the ticket waits for the host; 1: ready (count rows); 2: the stream
+    // is closed and the ticket is past its end; 3: abandoned
+    uint32_t status = 0, cnt = 0;
+    uint64_t tbase = 0;
+    if (lane == 0 && !stop) {
+      if (!have) {
+        const uint64_t cur = dev_load_u64(&dev->ticket), pw = dev_load_u64(&dev->pub_wr);
+        tr = stream_piece_rows(pw > cur ? pw - cur : 0, workers, rmax);
+        tk = atomicAdd(reinterpret_cast<unsigned long long*>(&dev->ticket), (unsigned long long)tr);
+        have = true;
+        t_wait = t_it;
+      }
+      const uint32_t cl = dev_load_u32(&dev->closed);
+      if (cl) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pub_wr is final
+      const uint64_t pw = dev_load_u64(&dev->pub_wr);
+      if (tk < pw) {
+        // the published part of the ticket now; an unpublished rest stays
+        // the wave's ticket (the host may wait for this part's batch before
+        // it publishes more)
+        status = 1;
+        cnt = tk + tr <= pw ? tr : (uint32_t)(pw - tk);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the mirrored descriptors
+        tbase = tk;
+        tk += cnt;
+        tr -= cnt;
+        have = tr != 0;
+        t_wait = t_it;
+      } else if (cl) {
+        status = 2;  // closed, and the ticket lies past the last row
+        have = false;
+      } else if (t_it - t_wait > abandon_ticks) {
+        status = 3;
+        have = false;
+      }
+    }
+    status = (uint32_t)__builtin_amdgcn_readfirstlane((int)status);
+    const int count = __builtin_amdgcn_readfirstlane((int)cnt);
+    const uint64_t base = uniform_u64(tbase);
+    if (status >= 2) stop = status;
+    if (count == 0 && count_p == 0 && count_q == 0) {
+      if (stop) {  // closed (or abandoned) and nothing left
+        if (stop == 3 && lane == 0)
+          __hip_atomic_store(&ctrl->abandoned, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      if (lane == 0) atomicAdd(&dev->stat[STREAM_STAT_WAIT_POLLS], 1ull);
+      __builtin_amdgcn_s_sleep(64);
+      continue;
+    }
+    if (count == 0 && lane == 0) atomicAdd(&dev->stat[STREAM_STAT_DRAINS], 1ull);
+    uint32_t hint_c = hint;
+    if (count) {
+      hint_c = stream_batch_of(dev, hint, base);
+      hint = hint_c;
+      pieces++;
+      rows += (uint32_t)count;
+    }
+    // stage A: S = d T of the new piece's rows (read from the pinned slot)
+    {
+      uint32_t h = hint_c;
+#pragma unroll 1
+      for (int j = 0; j < count; j++) {
+        const StreamRow sr = stream_row(dev, h, base + (uint32_t)j);
+        bool active;
+        const uint32_t r = stream_lane_row(sr, base + (uint32_t)j, lane, &active);
+        const uint4* src = reinterpret_cast<const uint4*>(sr.rows + (size_t)r * 64);
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint4 v = src[q];
+          w[4 * q] = v.x;
+          w[4 * q + 1] = v.y;
+          w[4 * q + 2] = v.z;
+          w[4 * q + 3] = v.w;
+        }
+        gej P;
+        row_shared_secret_point(P, w, w + 8, naf, k.naf_len, sc);
+        pend_store(sc, PB, count_p + j, P);
+      }
+    }
+    // one inversion: the new S points, piece P's F points, piece Q's label product
+    int ninv = count_p + count;
+    if (count_q) {
+      fe acc;
+      scr_load(acc, sc, QACC);
+      scr_store(sc, PEND_Z(PB, ninv), acc);
+      ninv++;
+    }
+    pend_invert<2 * MULTI_RMAX + 1>(sc, PB, ninv);
+    const auto qf_at = [&](int j, ge& F) {
+      scr_load(F.x, sc, QF + 2 * FW * j);
+      scr_load(F.y, sc, QF + 2 * FW * j + FW);
+    };
+    if (count_q) {  // piece Q: its labels against the mirrored outputs, then its flags
+      const auto q_out = [&](int j, const int64_t*& o, uint32_t& off, uint32_t& len, int64_t*& vrow,
+                             uint32_t& vstride) {
+        uint32_t h = hint_q;
+        const StreamRow sr = stream_row(dev, h, base_q + (uint32_t)j);
+        bool active;
+        const uint32_t r = stream_lane_row(sr, base_q + (uint32_t)j, lane, &active);
+        o = sr.mirror;
+        off = sr.offs[r];
+        len = active ? sr.lens[r] : 0u;
+        vrow = nullptr;
+        vstride = 0;
+      };
+      fe inv;
+      scr_load(inv, sc, PEND_ZI(PB, ninv - 1));
+      hits_q |= labels_backward(inv, k, labels, count_q, sc, LB, qf_at, q_out);
+      stream_emit(ctrl, dev, base_q, count_q, hint_q, lane, hits_q);
+      count_q = 0;
+    }
+    if (count_p) {  // piece P: affine F, base compare; its labels wait one iteration
+      uint32_t hits = 0, h = hint_p;
+#pragma unroll 1
+      for (int j = 0; j < count_p; j++) {
+        const StreamRow sr = stream_row(dev, h, base_p + (uint32_t)j);
+        bool active;
+        const uint32_t r = stream_lane_row(sr, base_p + (uint32_t)j, lane, &active);
+        gej P;
+        fe zi;
+        pend_load(P, sc, PB, j);
+        scr_load(zi, sc, PEND_ZI(PB, j));
+        ge F;
+        gej_to_ge_zinv(F, P, zi);
+        if (mirror) {
+          scr_store(sc, QF + 2 * FW * j, F.x);
+          scr_store(sc, QF + 2 * FW * j + FW, F.y);
+        }
+        if (stream_base_match(k, sr, sr.offs[r], active ? sr.lens[r] : 0u, active, mirror, F.x, fe_upper64(F.x)))
+          hits |= 1u << j;
+      }
+      if (mirror) {
+        fe acc;
+        labels_forward(acc, k, labels, count_p, sc, LB, qf_at);
+        scr_store(sc, QACC, acc);
+        base_q = base_p;
+        hint_q = hint_p;
+        count_q = count_p;
+        hits_q = hits;
+      } else {
+        stream_emit(ctrl, dev, base_p, count_p, hint_p, lane, hits);
+      }
+    }
+    // t of each new row, then stage B's F = t G + B into slot j
+#pragma unroll 1
+    for (int j = 0; j < count; j++) {
+      gej P;
+      fe zi;
+      pend_load(P, sc, PB, count_p + j);
+      scr_load(zi, sc, PEND_ZI(PB, count_p + j));
+      uint32_t sx[8], t[8];
+      const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
+      bip352_shared_secret_hash(t, k.mid, sx, y_odd);
+      gej F;
+      row_match_point<FBB>(F, t, fb, k);
+      pend_store(sc, PB, j, F);
+    }
+    base_p = base;
+    hint_p = hint_c;
+    count_p = count;
+    busy += wall_clock64() - t_it;
+  }
+  if (lane == 0) {
+    atomicAdd(&dev->stat[stop == 3 ? STREAM_STAT_EXIT_ABANDONED : STREAM_STAT_EXIT_CLOSED], 1ull);
+    atomicAdd(&dev->stat[STREAM_STAT_PIECES], pieces);
+    atomicAdd(&dev->stat[STREAM_STAT_WAVE_ROWS], rows);
+    atomicAdd(&dev->stat[STREAM_STAT_BUSY_TICKS], busy);
+    atomicAdd(&dev->stat[STREAM_STAT_LIFE_TICKS], wall_clock64() - t_start);
+  }
 }
 
 // One entry per thread of a table with `windows` windows of `entries` odd
@@ -1251,6 +1628,46 @@ static MultiBatch multi_desc(const uint32_t* tx, const uint32_t* ty, const int64
   return m;
 }
 
+// Blocks of a persistent k_scan_multi / k_scan_stream grid: at most
+// CUDASP_WAVES_A waves per SIMD (one 256-thread block = one wave per SIMD of a
+// CU), blocks_req if smaller (0 = the whole device), within 4 GiB of scratch.
+static uint64_t multi_grid_blocks(cudasp_scanner* s, uint64_t blocks_req, bool pipe) {
+  if (!s->cus) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus <= 0)
+      cus = 256;
+    s->cus = cus;
+  }
+  const uint64_t words = multi_scratch_words(s->consts.label_count, pipe);
+  const uint64_t full_blocks = (uint64_t)s->cus * CUDASP_WAVES_A;
+  const uint64_t cap_blocks = ((1ull << 32) - 1) / 4 / (words * BLOCK);
+  uint64_t blocks = blocks_req ? blocks_req : full_blocks;
+  if (blocks > full_blocks) blocks = full_blocks;
+  if (blocks > cap_blocks) blocks = cap_blocks;
+  return blocks;
+}
+
+// k_scan_multi / k_scan_stream scratch for `blocks` blocks.  Sized for the
+// blocks a launch runs (a 300k-row fused batch: ~293 of the 768 persistent
+// blocks), grown when a later launch runs more.  An allocation failure is
+// reported as CUDASP_ERR_CAPACITY before anything is queued, so
+// launch_pipeline can fall back to the stage kernels.
+static int ensure_multi_scratch(cudasp_scanner* s, uint64_t blocks, bool pipe, hipStream_t st) {
+  const uint64_t need_words = blocks * BLOCK * multi_scratch_words(s->consts.label_count, pipe);
+  if (need_words <= s->mscratch_words) return CUDASP_OK;
+  HIP_TRY(hipStreamSynchronize(st));  // no kernel of this scanner still uses the old scratch
+  if (s->d_mscratch) HIP_TRY(hipFree(s->d_mscratch));
+  s->d_mscratch = nullptr;
+  s->mscratch_words = 0;
+  if (hipMalloc(&s->d_mscratch, (size_t)need_words * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    s->d_mscratch = nullptr;
+    return set_error(CUDASP_ERR_CAPACITY, "cannot allocate %.1f MB of k_scan_multi scratch", need_words * 4 / 1e6);
+  }
+  s->mscratch_words = need_words;
+  return CUDASP_OK;
+}
+
 // One k_scan_multi launch over the described batches (total_wr wave-rows):
 // uploads the descriptors, resets the work counter, launches on `st`.  rmax:
 // rows per thread of the bulk; g1/g2: guided-scheduling parameters (hundredths of the
@@ -1287,39 +1704,13 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
   }
   if (!s->multi_copied[area]) HIP_TRY(hipEventCreateWithFlags(&s->multi_copied[area], hipEventDisableTiming));
   if (!s->d_counter) HIP_TRY(hipMalloc(&s->d_counter, sizeof(uint32_t)));
-  if (!s->cus) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus <= 0)
-      cus = 256;
-    s->cus = cus;
-  }
-  // grid: at most CUDASP_WAVES_A waves per SIMD (one 256-thread block = one
-  // wave per SIMD of a CU), no more waves than wave-rows, within 4 GiB of scratch
-  const uint64_t words = multi_scratch_words(s->consts.label_count, s->multi_pipe);
-  const uint64_t full_blocks = (uint64_t)s->cus * CUDASP_WAVES_A;
-  const uint64_t cap_blocks = ((1ull << 32) - 1) / 4 / (words * BLOCK);
-  uint64_t blocks = blocks_req ? blocks_req : full_blocks;
-  if (blocks > full_blocks) blocks = full_blocks;
+  uint64_t blocks = multi_grid_blocks(s, blocks_req, s->multi_pipe);
   const uint64_t need_blocks = (total_wr + 3) / 4;
   if (blocks > need_blocks) blocks = need_blocks;
-  if (blocks > cap_blocks) blocks = cap_blocks;
   if (blocks == 0) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the multi-batch path");
-  const uint64_t need_words = blocks * BLOCK * words;
-  if (need_words > s->mscratch_words) {
-    // Sized for the blocks this launch runs (a 300k-row fused batch: ~293 of
-    // the 768 persistent blocks), grown when a later launch runs more.  An
-    // allocation failure is reported as CUDASP_ERR_CAPACITY before anything
-    // is queued, so launch_pipeline can fall back to the stage kernels.
-    HIP_TRY(hipStreamSynchronize(st));  // no kernel of this scanner still uses the old scratch
-    if (s->d_mscratch) HIP_TRY(hipFree(s->d_mscratch));
-    s->d_mscratch = nullptr;
-    s->mscratch_words = 0;
-    if (hipMalloc(&s->d_mscratch, (size_t)need_words * 4) != hipSuccess) {
-      (void)hipGetLastError();
-      s->d_mscratch = nullptr;
-      return set_error(CUDASP_ERR_CAPACITY, "cannot allocate %.1f MB of k_scan_multi scratch", need_words * 4 / 1e6);
-    }
-    s->mscratch_words = need_words;
+  {
+    const int rc = ensure_multi_scratch(s, blocks, s->multi_pipe, st);
+    if (rc != CUDASP_OK) return rc;
   }
   // d_multi itself is reused in stream order: launches of one scanner run on
   // one stream (include/cudasp_abi.h), so this upload lands after the
@@ -1873,6 +2264,250 @@ int cudasp_debug_field_ops(int op, const uint32_t* d_a, const uint32_t* d_b, uin
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipDeviceSynchronize());
   return CUDASP_OK;
+}
+
+// ----------------------------------------------------------- streaming scan
+// cudasp_stream_*: one persistent k_scan_stream kernel scans batches as the
+// host publishes them (scan_stream.hpp).
+struct cudasp_stream {
+  cudasp_scanner* s = nullptr;
+  StreamCtrl* ctrl = nullptr;  // coherent pinned host memory (same address on the device)
+  StreamDev* dev = nullptr;    // device memory
+  uint64_t blocks_req = 0;  // requested grid (0: the whole device)
+  uint64_t blocks = 0;      // the current query's grid
+  uint32_t rmax = MULTI_RMAX;
+  uint64_t abandon_ticks = 0;  // 100 MHz wall-clock ticks a wave waits for the host before it gives up
+  hipEvent_t exited = nullptr;
+  bool running = false;     // a kernel was launched and `exited` recorded after it
+  uint32_t next = 0;        // batches published
+  uint64_t published_wr = 0;
+  uint64_t launches = 0;
+  std::mutex mu;            // publish / launch / finish
+};
+
+// Caller holds st->mu.  Whether this query's kernel is still running; a
+// kernel that ended before the stream was closed gave up (abandoned) or failed.
+static bool stream_kernel_alive(cudasp_stream* st, int* err) {
+  *err = CUDASP_OK;
+  if (!st->running) return false;
+  const hipError_t e = hipEventQuery(st->exited);
+  if (e == hipErrorNotReady) return true;
+  st->running = false;
+  if (e != hipSuccess)
+    *err = set_error(CUDASP_ERR_HIP, "streaming scan kernel failed: %s", hipGetErrorString(e));
+  else if (__atomic_load_n(&st->ctrl->abandoned, __ATOMIC_ACQUIRE))
+    *err = set_error(CUDASP_ERR_HIP, "streaming scan kernel gave up waiting for the host (stream never closed)");
+  return false;
+}
+
+// Caller holds st->mu.  Launch the query's kernel at its first batch, with
+// the scanner's current keys and options (a host may rebind the scanner
+// between queries: the grid and its scratch follow the label count).
+static int stream_launch(cudasp_stream* st) {
+  cudasp_scanner* s = st->s;
+  DeviceGuard g(s->device);
+  if (!multi_ok(s) || !s->multi_pipe)
+    return set_error(CUDASP_ERR_INVALID_ARG, "the scanner's options do not allow the streaming scan");
+  st->blocks = multi_grid_blocks(s, st->blocks_req, true);
+  if (st->blocks < 2) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the streaming scan");
+  {
+    const int rc = ensure_multi_scratch(s, st->blocks, true, s->stream);
+    if (rc != CUDASP_OK) return rc;
+  }
+  auto kf = s->fb_bits == 26 ? k_scan_stream<26> : k_scan_stream<22>;
+  hipLaunchKernelGGL(kf, dim3((uint32_t)st->blocks), dim3(BLOCK), 0, s->stream, st->ctrl, st->dev, s->d_naf,
+                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, st->rmax, st->abandon_ticks);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(st->exited, s->stream));
+  st->running = true;
+  st->launches++;
+  return CUDASP_OK;
+}
+
+static bool stream_seq_done(const cudasp_stream* st, uint64_t seq) {
+  const uint32_t d = __atomic_load_n(&st->ctrl->done[seq % STREAM_RING], __ATOMIC_ACQUIRE);
+  return (int32_t)(d - (uint32_t)(seq + 1)) >= 0;
+}
+
+int cudasp_host_alloc(void** p, size_t bytes) {
+  if (!p) return set_error(CUDASP_ERR_INVALID_ARG, "null pointer");
+  *p = nullptr;
+  if (bytes == 0) return CUDASP_OK;
+  void* q = nullptr;
+  HIP_TRY(hipHostMalloc(&q, bytes, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
+  void* dq = nullptr;
+  if (hipHostGetDevicePointer(&dq, q, 0) != hipSuccess || dq != q) {
+    (void)hipHostFree(q);
+    return set_error(CUDASP_ERR_HIP, "pinned host memory is not device-addressable at its host address");
+  }
+  *p = q;
+  return CUDASP_OK;
+}
+
+void cudasp_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out) {
+  if (!s || !out) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  if (!multi_ok(s) || !s->multi_pipe)
+    return set_error(CUDASP_ERR_INVALID_ARG,
+                     "the streaming scan needs the default options (output_count 1), an HBM fixed-base width "
+                     "(22 or 26 bits) and the pipelined schedule");
+  DeviceGuard g(s->device);
+  std::unique_ptr<cudasp_stream> st(new cudasp_stream());
+  st->s = s;
+  st->blocks_req = blocks;
+  st->blocks = multi_grid_blocks(s, blocks, true);
+  if (st->blocks < 2) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the streaming scan");
+  uint32_t abandon_s = 120;
+  if (const char* e = getenv("CUDASP_STREAM_ABANDON_S")) {
+    const long v = atol(e);
+    if (v >= 1 && v <= 86400) abandon_s = (uint32_t)v;
+  }
+  st->abandon_ticks = (uint64_t)abandon_s * 100000000ull;
+  if (const char* e = getenv("CUDASP_MULTI_ROWS")) {
+    const int v = atoi(e);
+    if (v >= 1 && v <= MULTI_RMAX) st->rmax = (uint32_t)v;
+  }
+  int rc = ensure_multi_scratch(s, st->blocks, true, s->stream);
+  if (rc != CUDASP_OK) return rc;
+  void* c = nullptr;
+  rc = cudasp_host_alloc(&c, sizeof(StreamCtrl));
+  if (rc != CUDASP_OK) return rc;
+  st->ctrl = static_cast<StreamCtrl*>(c);
+  memset(st->ctrl, 0, sizeof(StreamCtrl));
+  if (hipMalloc(&st->dev, sizeof(StreamDev)) != hipSuccess || hipEventCreateWithFlags(&st->exited, hipEventDisableTiming) != hipSuccess ||
+      hipMemsetAsync(st->dev, 0, sizeof(StreamDev), s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
+    cudasp_stream_destroy(st.release());
+    return set_error(CUDASP_ERR_HIP, "streaming scan: device state allocation failed");
+  }
+  *out = st.release();
+  return CUDASP_OK;
+}
+
+int cudasp_stream_publish(cudasp_stream* st, const uint8_t* rows, const int64_t* outputs, const uint32_t* offs,
+                          const uint32_t* lens, uint32_t n, uint8_t* flags, int64_t* d_mirror, uint64_t* seq) {
+  if (!st) return set_error(CUDASP_ERR_INVALID_ARG, "null stream");
+  if (n == 0 || !rows || !offs || !lens || !flags) return set_error(CUDASP_ERR_INVALID_ARG, "empty batch or null buffer");
+  if (st->s->consts.label_count && !d_mirror)
+    return set_error(CUDASP_ERR_INVALID_ARG, "a streaming scan with labels needs an outputs mirror in device memory");
+  std::lock_guard<std::mutex> lk(st->mu);
+  if (st->ctrl->closed) return set_error(CUDASP_ERR_INVALID_ARG, "stream already finished");
+  const uint32_t b = st->next;
+  const uint32_t e = b % STREAM_RING;
+  if (b >= STREAM_RING && !stream_seq_done(st, (uint64_t)b - STREAM_RING))
+    return set_error(CUDASP_ERR_CAPACITY, "more than %u streamed batches in flight", STREAM_RING);
+  if (b == 0) {  // one kernel per query, launched before its first batch and ended by finish
+    const int rc = stream_launch(st);
+    if (rc != CUDASP_OK) return rc;
+  } else {
+    int err;
+    if (!stream_kernel_alive(st, &err))
+      return err != CUDASP_OK ? err : set_error(CUDASP_ERR_HIP, "streaming scan kernel is gone");
+  }
+  StreamBatch& d = st->ctrl->desc[e];
+  d.rows = rows;
+  d.outputs = outputs;
+  d.offs = offs;
+  d.lens = lens;
+  d.flags = flags;
+  d.mirror = d_mirror;
+  d.n = n;
+  d.nwr = (n + 63u) / 64u;
+  d.first_wr = st->published_wr;
+  d.seq = b;
+  st->published_wr += d.nwr;
+  __atomic_store_n(&st->ctrl->published_wr, st->published_wr, __ATOMIC_RELEASE);
+  __atomic_store_n(&st->ctrl->published, b + 1, __ATOMIC_RELEASE);
+  st->next = b + 1;
+  if (seq) *seq = b;
+  return CUDASP_OK;
+}
+
+int cudasp_stream_query(cudasp_stream* st, uint64_t seq) {
+  if (!st) return set_error(CUDASP_ERR_INVALID_ARG, "null stream");
+  if (stream_seq_done(st, seq)) return 1;
+  std::lock_guard<std::mutex> lk(st->mu);
+  if (seq >= st->next) return set_error(CUDASP_ERR_INVALID_ARG, "batch %llu was not published", (unsigned long long)seq);
+  if (stream_seq_done(st, seq)) return 1;
+  int err;
+  if (!stream_kernel_alive(st, &err) && !stream_seq_done(st, seq))
+    return err != CUDASP_OK ? err : set_error(CUDASP_ERR_HIP, "streaming scan kernel ended before batch %llu was done",
+                                              (unsigned long long)seq);
+  return 0;
+}
+
+int cudasp_stream_wait(cudasp_stream* st, uint64_t seq) {
+  for (uint32_t i = 0;; i++) {
+    const int q = cudasp_stream_query(st, seq);
+    if (q != 0) return q < 0 ? q : CUDASP_OK;
+    if (i < 64)
+      std::this_thread::yield();
+    else
+      std::this_thread::sleep_for(std::chrono::microseconds(i < 256 ? 5 : 20));
+  }
+}
+
+int cudasp_stream_finish(cudasp_stream* st) {
+  if (!st) return set_error(CUDASP_ERR_INVALID_ARG, "null stream");
+  int rc = CUDASP_OK;
+  {
+    std::lock_guard<std::mutex> lk(st->mu);
+    __atomic_store_n(&st->ctrl->closed, 1u, __ATOMIC_RELEASE);
+  }
+  if (st->next > 0) rc = cudasp_stream_wait(st, (uint64_t)st->next - 1);
+  for (uint64_t b = st->next > STREAM_RING ? st->next - STREAM_RING : 0; rc == CUDASP_OK && b < st->next; b++)
+    rc = cudasp_stream_wait(st, b);
+  std::lock_guard<std::mutex> lk(st->mu);
+  DeviceGuard g(st->s->device);
+  if (st->running) {  // its waves leave as soon as they see the closed stream drained
+    const hipError_t e = hipEventSynchronize(st->exited);
+    st->running = false;
+    if (e != hipSuccess && rc == CUDASP_OK)
+      rc = set_error(CUDASP_ERR_HIP, "streaming scan kernel failed: %s", hipGetErrorString(e));
+  }
+  if (rc == CUDASP_OK && __atomic_load_n(&st->ctrl->abandoned, __ATOMIC_ACQUIRE))
+    rc = set_error(CUDASP_ERR_HIP, "streaming scan kernel gave up waiting for the host (stream never closed)");
+  // ready for the next query
+  memset(st->ctrl, 0, sizeof(StreamCtrl));
+  st->next = 0;
+  st->published_wr = 0;
+  if (hipMemsetAsync(st->dev, 0, sizeof(StreamDev), st->s->stream) != hipSuccess ||
+      hipStreamSynchronize(st->s->stream) != hipSuccess) {
+    if (rc == CUDASP_OK) rc = set_error(CUDASP_ERR_HIP, "streaming scan: state reset failed");
+  }
+  return rc;
+}
+
+int cudasp_stream_stats(const cudasp_stream* st, uint64_t* launches, uint32_t* blocks) {
+  if (!st) return set_error(CUDASP_ERR_INVALID_ARG, "null stream");
+  if (launches) *launches = st->launches;
+  if (blocks) *blocks = (uint32_t)st->blocks;
+  return CUDASP_OK;
+}
+
+int cudasp_stream_counters(cudasp_stream* st, uint64_t* out, uint32_t count) {
+  if (!st || !out) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(st->mu);
+  DeviceGuard g(st->s->device);
+  unsigned long long v[16] = {};
+  HIP_TRY(hipMemcpy(v, st->dev->stat, sizeof(v), hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < count && i < 16; i++) out[i] = v[i];
+  return CUDASP_OK;
+}
+
+void cudasp_stream_destroy(cudasp_stream* st) {
+  if (!st) return;
+  if (st->ctrl) {
+    (void)cudasp_stream_finish(st);
+    cudasp_host_free(st->ctrl);
+  }
+  DeviceGuard g(st->s->device);
+  if (st->dev) (void)hipFree(st->dev);
+  if (st->exited) (void)hipEventDestroy(st->exited);
+  delete st;
 }
 
 // ------------------------------------------------ reference three-phase ABI

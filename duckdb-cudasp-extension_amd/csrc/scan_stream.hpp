@@ -1,0 +1,116 @@
+// Streaming scan: ONE persistent kernel per device feed scans batches while
+// the host is still reading the table (cudasp_stream_*, include/cudasp_abi.h).
+//
+// The per-batch host path (cudasp_tf_* before this) copied each closed slot
+// to the device, transposed it, and launched one k_scan_multi per slot on
+// 3 streams: every 300k-row launch ends in its own drain, the GPU holds at
+// most 3 launches, and a table smaller than a few batches never fills it
+// (end to end 0.92 / 0.88 / 0.62 of the device-resident rate at 32.7M /
+// 9.4M / 1M rows).  Here the host publishes each closed slot into a
+// descriptor ring in coherent pinned host memory and the kernel's waves take
+// 64-row wave-rows from it as they are published:
+//   * inputs are read straight from the pinned slot (zero copy over PCIe:
+//     the 64-byte row blob, offset, length and outputs, each once per row --
+//     ~90 B per row at k = 2, 16 GB/s at 177 M rows/s against PCIe Gen5 x16);
+//     a row's outputs are copied to a device mirror at the base compare so the
+//     label compares read HBM, not PCIe;
+//   * flags go straight back into the pinned slot; the wave that completes a
+//     batch (one device counter per ring entry) writes the batch's sequence
+//     number into the ring's done word, which the host polls;
+//   * one poller wave per kernel reads the host's control block over PCIe
+//     (published count, descriptors, closed) and mirrors it into device
+//     memory; the worker waves take tickets of R wave-rows from one device
+//     counter (atomicAdd: a claim never fails or retries -- a compare-and-swap
+//     claim measured 160 retries per claim with 3071 waves, the kernel at a
+//     third of k_scan_multi's rate) and look each wave-row's batch up in the
+//     mirror.  A ticket beyond the published rows waits until the host
+//     publishes them or closes the stream (then the rows past the end are
+//     empty); every wave leaves once the stream is closed and its tickets are
+//     done, so the kernel lives for one query and the host's finish ends it.
+//     A wave that waits abandon_ticks (100 MHz wall clock) without either
+//     flags the stream abandoned and leaves (a host that never closes).
+// Pieces and the pipelined schedule are k_scan_multi's (one inversion per
+// piece); a piece never spans two batches.  This header holds the data
+// structures and the pure scheduling rules (host + device: the CPU tests
+// replay them); the kernel is in scan_kernels.hip.
+#pragma once
+#include <stdint.h>
+
+#include "secp256k1_fe.hpp"  // CUDASP_HD
+
+namespace cudasp {
+
+// Batches published and not yet harvested, at most (the host's slot ring is
+// far smaller: a feed has 8 slots).
+constexpr uint32_t STREAM_RING = 64;
+
+// One published batch, written by the host before it bumps `published`.
+// Pointers into coherent pinned host memory except `mirror` (device memory,
+// outputs-sized; only read with labels).
+struct StreamBatch {
+  const uint8_t* rows;      // n x 64-byte tweak blobs (x then y, little-endian u32 words)
+  const int64_t* outputs;   // outputs CSR values (words: 1 per output, 4 with full_x)
+  const uint32_t* offs;     // n, in outputs
+  const uint32_t* lens;     // n
+  uint8_t* flags;           // n, written by the kernel
+  int64_t* mirror;          // device copy of the outputs the label compares read
+  uint32_t n;
+  uint32_t nwr;             // wave-rows: ceil(n / 64)
+  uint64_t first_wr;        // wave-rows published before this batch
+  uint64_t seq;             // the batch's sequence number (tells a reused ring entry)
+};
+
+// Host <-> kernel control block (coherent pinned host memory).
+struct StreamCtrl {
+  uint32_t published;               // batches published (host; release)
+  uint32_t closed;                  // 1: no batch follows (host)
+  uint64_t published_wr;            // wave-rows published (host)
+  uint32_t abandoned;               // 1: a wave gave up waiting (kernel)
+  uint32_t done[STREAM_RING];       // ring entry e: 1 + sequence number of the last batch completed there (kernel)
+  StreamBatch desc[STREAM_RING];    // batch b at entry b % STREAM_RING
+};
+
+// Device-side state (device memory), zeroed between queries.  The kernel's
+// poller wave (one per kernel) mirrors the host's control block here --
+// published batches, their descriptors, closed -- so the worker waves'
+// claims and polls touch device memory only, never PCIe.
+struct StreamDev {
+  uint64_t ticket;                  // wave-rows handed out to the workers
+  uint64_t pub_wr;                  // mirror of StreamCtrl::published_wr
+  uint32_t pub;                     // mirror of StreamCtrl::published
+  uint32_t closed;                  // mirror of StreamCtrl::closed (set after the last pub)
+  uint32_t wr_done[STREAM_RING];    // wave-rows finished of the batch at each entry
+  StreamBatch desc[STREAM_RING];    // mirror of StreamCtrl::desc
+  // counters (cudasp_stream_counters): STREAM_STAT_* below
+  unsigned long long stat[16];
+};
+
+// StreamDev::stat indices: pieces and wave-rows claimed, polls of a wave
+// waiting for its ticket, pipeline drains, batch lookups past a reused ring
+// entry, worker exits (abandoned / closed), poller polls, and the workers'
+// summed busy and lifetime in wall-clock ticks.
+enum {
+  STREAM_STAT_PIECES = 0,
+  STREAM_STAT_WAVE_ROWS,
+  STREAM_STAT_WAIT_POLLS,
+  STREAM_STAT_DRAINS,
+  STREAM_STAT_LOOKUP_STEPS,
+  STREAM_STAT_EXIT_ABANDONED,
+  STREAM_STAT_EXIT_CLOSED,
+  STREAM_STAT_POLLER_POLLS,
+  STREAM_STAT_BUSY_TICKS,
+  STREAM_STAT_LIFE_TICKS,
+  STREAM_STAT_COUNT
+};
+
+// Wave-rows of the next ticket.  rem: published wave-rows not yet handed
+// out; waves: the workers.  The wave's share of what is available now,
+// rem / waves (1 .. rmax), as k_scan_multi's guided rule: a full backlog gives
+// rmax rows per thread (one inversion for rmax rows), the first small slots
+// of a query and the end of the table single wave-rows to many waves.
+CUDASP_HD uint32_t stream_piece_rows(uint64_t rem, uint32_t waves, uint32_t rmax) {
+  const uint64_t r = waves ? rem / waves : rmax;
+  return r < 1 ? 1u : (r > rmax ? rmax : (uint32_t)r);
+}
+
+}  // namespace cudasp

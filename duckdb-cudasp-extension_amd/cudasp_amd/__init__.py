@@ -5,6 +5,6 @@ the C ABI in ``include/cudasp_abi.h``, table-function host behind
 ``include/cudasp_host.h``); this package is its Python face.
 """
 from ._native import CudaspError, load as load_native  # noqa: F401
-from .scanner import Scanner  # noqa: F401
+from .scanner import HostBuffer, Scanner, ScanStream, StreamBatch  # noqa: F401
 from .table_function import (BoundScan, assign_gpu, InvalidInputException, cudasp_scan, cudasp_scan_arrow, pool_size,  # noqa: F401
                              release_pool)

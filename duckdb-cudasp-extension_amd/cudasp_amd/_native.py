@@ -47,6 +47,16 @@ SIGNATURES = {
     "cudasp_synth_outputs": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _U32, _P, _P, _P, _P]),
     "cudasp_synth_output_lengths": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _U32, _P, _P]),
     "cudasp_synth_output_values": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _P, _P, _P, _P]),
+    "cudasp_host_alloc": (_I32, [ctypes.POINTER(_P), ctypes.c_size_t]),
+    "cudasp_host_free": (None, [_P]),
+    "cudasp_stream_create": (_I32, [_P, _U32, ctypes.POINTER(_P)]),
+    "cudasp_stream_publish": (_I32, [_P, _P, _P, _P, _P, _U32, _P, _P, ctypes.POINTER(ctypes.c_uint64)]),
+    "cudasp_stream_query": (_I32, [_P, ctypes.c_uint64]),
+    "cudasp_stream_wait": (_I32, [_P, ctypes.c_uint64]),
+    "cudasp_stream_finish": (_I32, [_P]),
+    "cudasp_stream_stats": (_I32, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_U32)]),
+    "cudasp_stream_counters": (_I32, [_P, ctypes.POINTER(ctypes.c_uint64), _U32]),
+    "cudasp_stream_destroy": (None, [_P]),
     "cudasp_debug_field_ops": (_I32, [ctypes.c_int, _P, _P, _P, _U32]),
     "cudasp_field_layout": (_I32, [_P, _P, _P, _P, _P]),
     "LaunchBatchScan": (_P, [_P, _P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _U32, ctypes.c_size_t]),

@@ -202,3 +202,134 @@ class Scanner:
             self._h, _ptr(tk), _ptr(outs) if outs.size else None, outs.shape[0], _ptr(offs), _ptr(lens), n,
             _ptr(flags)))
         return flags
+
+
+# ------------------------------------------------------------- streaming scan
+class HostBuffer:
+    """Coherent pinned host memory (cudasp_host_alloc), device-addressable at
+    the same address: what a streamed batch's host buffers must live in.
+    ``array`` is a uint8 numpy view; ``view(dtype)`` reinterprets it."""
+
+    def __init__(self, nbytes):
+        self._lib = _native.load()
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        _native.check(self._lib.cudasp_host_alloc(ctypes.byref(p), max(1, self.nbytes)))
+        self.ptr = p.value
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, self.nbytes)).from_address(self.ptr))
+
+    def view(self, dtype):
+        return self.array.view(dtype)
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            self._lib.cudasp_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ScanStream:
+    """cudasp_stream_*: ONE persistent kernel scans the batches published
+    into it, reading them from pinned host memory (HostBuffer) and writing
+    their flags back there (include/cudasp_abi.h).  The scanner must not run
+    other launches while the stream is open."""
+
+    def __init__(self, scanner, blocks=0):
+        self._lib = _native.load()
+        self.scanner = scanner
+        h = ctypes.c_void_p()
+        _native.check(self._lib.cudasp_stream_create(scanner._h, int(blocks), ctypes.byref(h)))
+        self._h = h
+
+    def publish(self, rows, outputs, offsets, lengths, n, flags, mirror=None):
+        """rows / outputs / offsets / lengths / flags: HostBuffers (or their
+        addresses); mirror: a device tensor of the batch's outputs size (with
+        labels).  Returns the batch's sequence number."""
+        seq = ctypes.c_uint64()
+        addr = lambda b: None if b is None else (b.ptr if isinstance(b, HostBuffer) else int(b))  # noqa: E731
+        _native.check(self._lib.cudasp_stream_publish(
+            self._h, addr(rows), addr(outputs), addr(offsets), addr(lengths), int(n), addr(flags),
+            None if mirror is None else mirror.data_ptr(), ctypes.byref(seq)))
+        return seq.value
+
+    def query(self, seq):
+        rc = self._lib.cudasp_stream_query(self._h, int(seq))
+        if rc < 0:
+            _native.check(rc)
+        return rc == 1
+
+    def wait(self, seq):
+        _native.check(self._lib.cudasp_stream_wait(self._h, int(seq)))
+
+    def finish(self):
+        _native.check(self._lib.cudasp_stream_finish(self._h))
+
+    def stats(self):
+        launches, blocks = ctypes.c_uint64(), ctypes.c_uint32()
+        _native.check(self._lib.cudasp_stream_stats(self._h, ctypes.byref(launches), ctypes.byref(blocks)))
+        return {"launches": launches.value, "blocks": blocks.value}
+
+    COUNTERS = ("pieces", "wave_rows", "wait_polls", "drains", "lookup_steps", "exit_abandoned", "exit_closed",
+                "poller_polls", "busy_ticks", "life_ticks")
+
+    def counters(self):
+        """The kernel's counters for the current query (cudasp_stream_counters)."""
+        v = (ctypes.c_uint64 * 16)()
+        _native.check(self._lib.cudasp_stream_counters(self._h, v, 16))
+        return dict(zip(self.COUNTERS, list(v)))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.cudasp_stream_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class StreamBatch:
+    """One batch staged in pinned host memory for a ScanStream: the tweak
+    blobs, the outputs CSR (int64 values, or 32-byte keys with full_x) and
+    the flags the kernel writes; plus the device mirror for label scans."""
+
+    def __init__(self, tweak_keys, outputs, offsets, lengths, label_count=0, device=0, full_x=False):
+        tk = np.ascontiguousarray(tweak_keys, dtype=np.uint8).reshape(-1, 64)
+        self.n = tk.shape[0]
+        outs = (np.ascontiguousarray(outputs, dtype=np.uint8).reshape(-1) if full_x
+                else np.ascontiguousarray(outputs, dtype=np.int64).view(np.uint8).reshape(-1))
+        self.rows = HostBuffer(tk.nbytes)
+        self.rows.array[:] = tk.reshape(-1)
+        self.outputs = HostBuffer(max(8, outs.nbytes))
+        self.outputs.array[:outs.nbytes] = outs
+        self.offsets = HostBuffer(4 * self.n)
+        self.offsets.view(np.uint32)[:] = np.asarray(offsets, dtype=np.uint32)
+        self.lengths = HostBuffer(4 * self.n)
+        self.lengths.view(np.uint32)[:] = np.asarray(lengths, dtype=np.uint32)
+        self.flags = HostBuffer(self.n)
+        self.flags.array[:] = 0xEE  # every row must be written
+        self.mirror = None
+        if label_count:
+            import torch
+            self.mirror = torch.empty((max(1, outs.nbytes // 8),), dtype=torch.int64,
+                                      device=torch.device("cuda", device))
+
+    def publish(self, stream):
+        return stream.publish(self.rows, self.outputs, self.offsets, self.lengths, self.n, self.flags, self.mirror)
+
+    def result(self):
+        return self.flags.array.copy()

@@ -100,6 +100,7 @@ class _Stats(ctypes.Structure):
         ("reserve_s", ctypes.c_double),
         ("copy_s", ctypes.c_double),
         ("launch_s", ctypes.c_double),
+        ("streaming_feeds", ctypes.c_uint32),
     ]
 
 

@@ -186,6 +186,54 @@ typedef struct {
 } cudasp_device_batch;
 int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* batches, uint32_t count, void* stream);
 
+/* Streaming scan (the table-function host's device feeds; no reference
+ * counterpart: it replaces the per-batch H2D copy + launch + D2H of
+ * ProcessBatch, src/cudasp_extension.cu:226-410, for batches that arrive
+ * while the query runs).  ONE persistent kernel per stream scans every batch
+ * published into it, reading the batch straight from pinned host memory (the
+ * 64-byte tweak blobs as the table holds them, the outputs CSR) and writing
+ * its flags back there; the host polls for each batch's completion.  Needs a
+ * scanner with the default options (output_count 1) and an HBM fixed-base
+ * width (22 or 26 bits); the scanner must not run other launches while a
+ * stream on it is open.
+ *   cudasp_host_alloc   coherent pinned host memory, device-addressable at
+ *                       the same address: every host buffer of a published
+ *                       batch must come from it.
+ *   cudasp_stream_create  blocks = 0: the whole device (3 waves per SIMD).
+ *   cudasp_stream_publish  a batch of n >= 1 rows; with labels, d_mirror is a
+ *                       device buffer as large as the batch's outputs (the
+ *                       kernel copies each row's outputs there once).  The
+ *                       buffers must stay untouched until the batch is done.
+ *                       *seq receives the batch's sequence number.  At most
+ *                       64 batches may be published and not yet done
+ *                       (CUDASP_ERR_CAPACITY otherwise).  Launches the kernel
+ *                       if none is running (a kernel whose waves find no work
+ *                       for CUDASP_STREAM_IDLE_US, default 2000 us, ends).
+ *   cudasp_stream_query  1: batch seq done (flags written), 0: not yet, < 0: error.
+ *   cudasp_stream_wait   blocks until batch seq is done.
+ *   cudasp_stream_finish  end of input: waits for every batch and for the
+ *                       kernel, then resets the stream for reuse (sequence
+ *                       numbers start again at 0).
+ *   cudasp_stream_stats  kernel launches so far and grid blocks.
+ *   cudasp_stream_counters  the kernel's counters of the current query
+ *                       (reset by finish): pieces, wave-rows, idle polls,
+ *                       pipeline drains, claim retries, worker exits on the
+ *                       idle timeout and on close, poller polls, workers'
+ *                       busy and lifetime ticks (100 MHz). */
+typedef struct cudasp_stream cudasp_stream;
+int cudasp_host_alloc(void** p, size_t bytes);
+void cudasp_host_free(void* p);
+int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out);
+int cudasp_stream_publish(cudasp_stream* st, const uint8_t* h_tweak_keys, const int64_t* h_outputs,
+                          const uint32_t* h_output_offsets, const uint32_t* h_output_lengths, uint32_t n,
+                          uint8_t* h_match_flags, int64_t* d_mirror, uint64_t* seq);
+int cudasp_stream_query(cudasp_stream* st, uint64_t seq);
+int cudasp_stream_wait(cudasp_stream* st, uint64_t seq);
+int cudasp_stream_finish(cudasp_stream* st);
+int cudasp_stream_stats(const cudasp_stream* st, uint64_t* launches, uint32_t* blocks);
+int cudasp_stream_counters(cudasp_stream* st, uint64_t* out, uint32_t count);
+void cudasp_stream_destroy(cudasp_stream* st);
+
 /* Host batch, synchronous: tweak keys as n 64-byte blobs back to back, the
  * outputs CSR in host memory; writes h_match_flags[n]. */
 int cudasp_scan_host(cudasp_scanner* s, const uint8_t* h_tweak_keys, const int64_t* h_outputs,

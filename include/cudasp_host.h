@@ -110,6 +110,8 @@ typedef struct {
   double reserve_s;                /* executor-thread time getting room in a slot (harvests and waits included) */
   double copy_s;                   /* executor-thread time copying rows into the slots */
   double launch_s;                 /* executor-thread time issuing the batches' copies and kernels */
+  uint32_t streaming_feeds;        /* feeds that ran the streaming scan (cudasp_stream_*: one
+                                      persistent kernel reading the slots in place) */
 } cudasp_tf_stats;
 int cudasp_tf_get_stats(cudasp_tf_global* g, cudasp_tf_stats* out);
 

@@ -1,0 +1,211 @@
+"""GPU: the streaming scan (cudasp_stream_*: ONE persistent k_scan_stream
+kernel scans batches as they are published, reading them from coherent pinned
+host memory and writing their flags back there) gives the per-batch path's
+flags -- ragged batch sizes, 0 / 2 / 16 labels (the label compares read the
+device mirror of each row's outputs), 1..15 outputs per row, a ring that
+wraps, reuse after finish, a slow publisher, a host that never closes (the
+waves give up), exceptional label sums in one thread's piece, and the C
+oracle."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import test_multi_batch_gpu as tm
+from test_multi_batch_gpu import torch  # noqa: F401  (fixture)
+
+pytestmark = pytest.mark.gpu
+
+# a stream that never completes a batch ends its kernel after this many
+# seconds (the test then fails instead of hanging)
+os.environ.setdefault("CUDASP_STREAM_ABANDON_S", "20")
+
+SCAN, SPEND, LABEL = tm.SCAN, tm.SPEND, tm.LABEL
+
+
+def host_rows(b):
+    """A device batch's tweak columns as the table's 64-byte row blobs."""
+    xs = b["tweak_x"].cpu().numpy().view(np.uint32)
+    ys = b["tweak_y"].cpu().numpy().view(np.uint32)
+    n = b["n"]
+    return np.ascontiguousarray(np.concatenate([xs.T, ys.T], axis=1).astype("<u4")).view(np.uint8).reshape(n, 64)
+
+
+def staged(b, label_count):
+    from cudasp_amd import StreamBatch
+    n = b["n"]
+    return StreamBatch(host_rows(b), b["outputs"].cpu().numpy(), b["offsets"][:n].cpu().numpy().view(np.uint32),
+                       b["lengths"][:n].cpu().numpy().view(np.uint32), label_count=label_count)
+
+
+def run_stream(batches, labels, rounds=1, max_in_flight=None):
+    """Publish every batch into one stream (`rounds` queries on the same
+    stream), waiting for the oldest when max_in_flight are out; returns the
+    last round's flags per batch and the stream's stats."""
+    from cudasp_amd import Scanner, ScanStream
+    stage = [staged(b, len(labels)) for b in batches]
+    with Scanner(SCAN, SPEND, labels, max_rows=1000) as s, ScanStream(s) as st:
+        for _ in range(rounds):
+            for sb in stage:
+                sb.flags.array[:] = 0xEE
+            seqs = []
+            for sb in stage:
+                if max_in_flight and len(seqs) >= max_in_flight:
+                    st.wait(seqs[-max_in_flight])
+                seqs.append(sb.publish(st))
+            for q in seqs:
+                st.wait(q)
+            assert all(st.query(q) for q in seqs)
+            st.finish()
+        stats = st.stats()
+    return [sb.result() for sb in stage], stats
+
+
+def flags_equal(got, want):
+    assert len(got) == len(want)
+    for i, (g, (w, _, _)) in enumerate(zip(got, want)):
+        assert (g == w).all(), "batch %d: %d rows differ" % (i, int((g != w).sum()))
+
+
+SIZES = [3001, 64, 1, 129, 70000, 65, 2047, 300000]
+
+
+@pytest.mark.parametrize("nlabels", [0, 2])
+def test_stream_equals_per_batch(torch, nlabels):
+    labels = [LABEL, SPEND][:nlabels]
+    batches = [tm.make_batch(torch, 1000 + 300000 * i, n) for i, n in enumerate(SIZES)]
+    tm.plant(torch, batches, labels)
+    want = tm.run_per_batch(torch, batches, labels)
+    assert sum(c for _, _, c in want) > 0
+    got, stats = run_stream(batches, labels, rounds=2)
+    flags_equal(got, want)
+    assert stats["launches"] >= 2  # one kernel per query at least
+
+
+def test_stream_16_labels_variable_outputs(torch):
+    """Config-5 shape: 16 labels, 1..15 outputs per row, planted values over
+    every label index; matches the per-batch path and the C oracle."""
+    from oracle import oracle
+    labels = tm.labels16()
+    batches = [tm.make_batch(torch, 3 + 40000 * i, n, kmax=15) for i, n in enumerate([5000, 333, 4096, 1])]
+    tm.plant(torch, batches, labels, every=7)
+    want = tm.run_per_batch(torch, batches, labels)
+    assert sum(c for _, _, c in want) > 1000
+    got, _ = run_stream(batches, labels)
+    flags_equal(got, want)
+    b = batches[1]
+    n = b["n"]
+    ref, _ = oracle.scan(SCAN, SPEND, labels, host_rows(b), b["outputs"].cpu().numpy(),
+                         b["offsets"][:n].cpu().numpy().view(np.uint32),
+                         b["lengths"][:n].cpu().numpy().view(np.uint32), threads=16)
+    assert (got[1] == ref).all()
+
+
+def test_stream_ring_wraps(torch):
+    """150 batches of 1..700 rows through the 64-entry descriptor ring with
+    at most 40 in flight, and then all of a second query: flags equal the
+    per-batch path's over the whole table."""
+    rng = np.random.default_rng(150)
+    sizes = [int(x) for x in rng.integers(1, 701, 150)]
+    labels = [LABEL]
+    batches = [tm.make_batch(torch, 77 + 1000 * i, n) for i, n in enumerate(sizes)]
+    tm.plant(torch, batches, labels, every=5)
+    want = tm.run_per_batch(torch, batches, labels)
+    got, _ = run_stream(batches, labels, rounds=2, max_in_flight=40)
+    flags_equal(got, want)
+
+
+def test_stream_slow_publisher(torch):
+    """Batches published 50 ms apart: the query's one kernel waits for each
+    (its waves hold tickets past the published rows) and the results are
+    the per-batch path's."""
+    from cudasp_amd import Scanner, ScanStream
+    labels = [LABEL]
+    batches = [tm.make_batch(torch, 5000 + 9000 * i, n) for i, n in enumerate([4000, 700, 8000])]
+    tm.plant(torch, batches, labels, every=9)
+    want = tm.run_per_batch(torch, batches, labels)
+    stage = [staged(b, 1) for b in batches]
+    with Scanner(SCAN, SPEND, labels, max_rows=1000) as s, ScanStream(s) as st:
+        for sb in stage:
+            q = sb.publish(st)
+            st.wait(q)
+            time.sleep(0.05)
+        c = st.counters()
+        st.finish()
+        assert st.stats()["launches"] == 1
+    assert c["wait_polls"] > 0
+    flags_equal([sb.result() for sb in stage], want)
+
+
+def test_stream_abandoned_by_host(torch, monkeypatch):
+    """A host that neither publishes nor closes for CUDASP_STREAM_ABANDON_S:
+    the kernel's waves give up and leave (no wave spins forever), the next
+    publish reports it, and after finish the stream serves a new query."""
+    from cudasp_amd import CudaspError, Scanner, ScanStream
+    monkeypatch.setenv("CUDASP_STREAM_ABANDON_S", "1")
+    b = tm.make_batch(torch, 99, 3000)
+    tm.plant(torch, [b], [], every=50)
+    want = tm.run_per_batch(torch, [b], [])
+    sb = staged(b, 0)
+    with Scanner(SCAN, SPEND, [], max_rows=1000) as s, ScanStream(s) as st:
+        st.wait(sb.publish(st))
+        time.sleep(2.5)
+        with pytest.raises(CudaspError):
+            st.wait(sb.publish(st))
+        with pytest.raises(CudaspError):
+            st.finish()
+        sb.flags.array[:] = 0xEE
+        st.wait(sb.publish(st))
+        st.finish()
+    flags_equal([sb.result()], want)
+
+
+def test_stream_exceptional_label_sums(torch):
+    """Label keys that make label sums exceptional inside one thread's piece
+    (test_multi_exceptional_label_sums' construction): F + L = 2F matches, a
+    sum at infinity never does; flags equal the oracle's."""
+    import variants as V
+    from oracle import oracle
+    n = 64 * 6 * 2 + 17
+    b = tm.make_batch(torch, 31337, n)
+    tw = host_rows(b)
+    ra, rb, rc = 5, 5 + 64, 5 + 128
+    F = [V.row(SCAN, SPEND, [], bytes(tw[i]))[0][0][0] for i in (ra, rb, rc)]
+    labels = [V.point_blob(F[0]), LABEL, V.point_blob(V.neg(F[1])), V.point_blob(F[2])]
+    _, vals = oracle.scan(SCAN, SPEND, labels, tw, want_values=True)
+    outs = b["outputs"].cpu().numpy()
+    offs = b["offsets"][:n].cpu().numpy().view(np.uint32)
+    lens = b["lengths"][:n].cpu().numpy().view(np.uint32)
+    for i in range(n):
+        if i in (ra, rb, rc):
+            continue
+        if i % 11 == 0:
+            outs[offs[i]] = vals[i, 0]
+        elif i % 9 == 0:
+            outs[offs[i] + 1] = vals[i, 2]
+    outs[offs[ra]] = vals[ra, 1]
+    outs[offs[rb]] = oracle.LABEL_INFINITY
+    outs[offs[rb] + 1] = 0
+    outs[offs[rc] + 1] = vals[rc, 4]
+    b["outputs"] = torch.from_numpy(outs).cuda()
+    want, _ = oracle.scan(SCAN, SPEND, labels, tw, outs, offs, lens, threads=16)
+    assert want[ra] == 1 and want[rb] == 0 and want[rc] == 1
+    got, _ = run_stream([b], labels)
+    assert (got[0] == want).all()
+
+
+def test_stream_rejects_bad_use(torch):
+    from cudasp_amd import CudaspError, Scanner, ScanStream, StreamBatch
+    b = tm.make_batch(torch, 1, 100)
+    with Scanner(SCAN, SPEND, [LABEL], max_rows=100) as s:
+        with ScanStream(s) as st:
+            sb = staged(b, 0)  # no mirror with a label scanner
+            with pytest.raises(CudaspError):
+                st.publish(sb.rows, sb.outputs, sb.offsets, sb.lengths, sb.n, sb.flags, None)
+            with pytest.raises(CudaspError):
+                st.publish(sb.rows, sb.outputs, sb.offsets, sb.lengths, 0, sb.flags, None)
+        s.set_options(output_count=2)
+        with pytest.raises(CudaspError):
+            ScanStream(s)
+    assert StreamBatch is not None

@@ -434,7 +434,7 @@ int main(int argc, char** argv) {
          "\"gpu_max_hw_queues_env\": \"%s\", \"launches\": %llu, \"rows_per_launch\": %.0f, "
          "\"harvest_wait_s\": %.4f, \"reserve_s\": %.4f, \"copy_s\": %.4f, \"launch_s\": %.4f, "
          "\"thread_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
-         "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f}\n",
+         "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f, \"streaming_feeds\": %u}\n",
          a.columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)t.rows, a.threads, (long long)a.batch,
          a.labels,
          a.kmax ? ("\"1.." + std::to_string(a.kmax) + "\"").c_str() : std::to_string(a.k).c_str(),
@@ -443,6 +443,7 @@ int main(int argc, char** argv) {
          all_exact ? "true" : "false", warm.secs, gen_s, cudasp_device_count(), q.stats.feeds,
          q.stats.streams_per_feed, q.stats.max_streams_per_device, q.stats.hw_queues, hq ? hq : "",
          (unsigned long long)q.stats.launches, q.stats.launches ? (double)q.stats.rows / q.stats.launches : 0.0,
-         q.stats.harvest_wait_s, q.stats.reserve_s, q.stats.copy_s, q.stats.launch_s, q.call_s_mean, q.final_s_mean, q.done_min, q.done_max);
+         q.stats.harvest_wait_s, q.stats.reserve_s, q.stats.copy_s, q.stats.launch_s, q.call_s_mean, q.final_s_mean, q.done_min, q.done_max,
+         q.stats.streaming_feeds);
   return all_exact ? 0 : 2;
 }
