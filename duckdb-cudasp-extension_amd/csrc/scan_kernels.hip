@@ -667,14 +667,28 @@ struct StreamRow {
 // The batch holding published wave-row w, searched forward from `hint` (the
 // batch of an earlier wave-row of this wave's tickets).  A ring entry holding
 // another sequence number was reused: that batch is complete, hence before
-// w's (w is this wave's and not done yet).  Bounded: the walk never passes
-// the ring twice.
+// w's (w is this wave's and not done yet).  The walk starts no earlier than
+// pub - STREAM_RING: the host publishes batch X only once X - STREAM_RING is
+// done, so every batch below that is done and w's lies at or above it (a
+// wave's first hint is 0, which once the ring has wrapped twice would leave
+// a walk from the hint short of w's batch).  A stale `pub` lowers the start
+// by at most one poller pass (STREAM_RING batches), so three passes of the
+// ring bound the walk.
 __device__ __forceinline__ uint32_t stream_batch_of(StreamDev* dev, uint32_t hint, uint64_t w) {
   uint32_t b = hint;
-  for (uint32_t i = 0; i < 2 * STREAM_RING; i++, b++) {
+  const uint32_t pub = dev_load_u32(&dev->pub);
+  if (pub > STREAM_RING && b < pub - STREAM_RING) b = pub - STREAM_RING;
+  for (uint32_t i = 0; i < 3 * STREAM_RING; i++, b++) {
+    // seqlock read: the poller rewrites an entry (batch b + STREAM_RING,
+    // once b is done) with its seq invalidated first and set last, so a
+    // range read between two equal seq loads belongs to batch b; an entry
+    // rewritten meanwhile held a done batch, not w's
     const StreamBatch* d = &dev->desc[b % STREAM_RING];
+    if (__hip_atomic_load(&d->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != b) continue;
+    const uint64_t end = dev_load_u64(&d->first_wr) + dev_load_u32(&d->nwr);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (dev_load_u64(&d->seq) != b) continue;
-    if (w < dev_load_u64(&d->first_wr) + dev_load_u32(&d->nwr)) break;
+    if (w < end) break;
   }
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
 }
@@ -723,19 +737,26 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t abandon_t
     const uint32_t cl = sys_load_u32(&ctrl->closed);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t pub = sys_load_u32(&ctrl->published);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the descriptors are read after `published`
     const uint64_t now = wall_clock64();
     if (pub != seen) {
       uint64_t pub_wr = 0;
       for (uint32_t b = seen; b != pub; b++) {
         const uint64_t* src = reinterpret_cast<const uint64_t*>(&ctrl->desc[b % STREAM_RING]);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(&dev->desc[b % STREAM_RING]);
+        StreamBatch* de = &dev->desc[b % STREAM_RING];
+        uint64_t* dst = reinterpret_cast<uint64_t*>(de);
         StreamBatch d;
         uint64_t* dw = reinterpret_cast<uint64_t*>(&d);
+        // seqlock write (stream_batch_of): seq invalid, the fields, then seq
+        static_assert(offsetof(StreamBatch, seq) + 8 == sizeof(StreamBatch), "seq is the descriptor's last word");
+        __hip_atomic_store(&de->seq, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 #pragma unroll
-        for (int i = 0; i < (int)(sizeof(StreamBatch) / 8); i++) {
-          dw[i] = sys_load_u64(src + i);
+        for (int i = 0; i < (int)(sizeof(StreamBatch) / 8); i++) dw[i] = sys_load_u64(src + i);
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(StreamBatch) / 8) - 1; i++)
           __hip_atomic_store(dst + i, dw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        __hip_atomic_store(&de->seq, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         // the rows mirrored so far (not the host's published_wr, which may
         // already count a batch published after `pub` was read)
         pub_wr = d.first_wr + d.nwr;
@@ -775,7 +796,10 @@ __device__ __forceinline__ void stream_emit(StreamCtrl* ctrl, StreamDev* dev, ui
       const uint32_t e = sr.b % STREAM_RING;
       const uint32_t before = atomicAdd(&dev->wr_done[e], 1u);
       if (before + 1u == sr.nwr) {
-        __hip_atomic_store(&dev->wr_done[e], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the entry's count back to 0 for batch b + STREAM_RING; a subtraction,
+        // so it commutes with that batch's counts however late it lands
+        atomicSub(&dev->wr_done[e], sr.nwr);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // complete before the host can reuse the entry
         __hip_atomic_store(&ctrl->done[e], sr.b + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
@@ -2282,6 +2306,7 @@ struct cudasp_stream {
   uint32_t next = 0;        // batches published
   uint64_t published_wr = 0;
   uint64_t launches = 0;
+  unsigned long long last_stat[16] = {};  // the kernel's counters of the last finished query
   std::mutex mu;            // publish / launch / finish
 };
 
@@ -2470,11 +2495,16 @@ int cudasp_stream_finish(cudasp_stream* st) {
   }
   if (rc == CUDASP_OK && __atomic_load_n(&st->ctrl->abandoned, __ATOMIC_ACQUIRE))
     rc = set_error(CUDASP_ERR_HIP, "streaming scan kernel gave up waiting for the host (stream never closed)");
-  // ready for the next query
+  // the query's counters (read here: while the kernel runs it holds every
+  // wave slot, and a device-to-host copy could wait for it), then ready for
+  // the next query
+  const bool ran = st->next > 0;
   memset(st->ctrl, 0, sizeof(StreamCtrl));
   st->next = 0;
   st->published_wr = 0;
-  if (hipMemsetAsync(st->dev, 0, sizeof(StreamDev), st->s->stream) != hipSuccess ||
+  if ((ran && hipMemcpyAsync(st->last_stat, st->dev->stat, sizeof(st->last_stat), hipMemcpyDeviceToHost,
+                             st->s->stream) != hipSuccess) ||
+      hipMemsetAsync(st->dev, 0, sizeof(StreamDev), st->s->stream) != hipSuccess ||
       hipStreamSynchronize(st->s->stream) != hipSuccess) {
     if (rc == CUDASP_OK) rc = set_error(CUDASP_ERR_HIP, "streaming scan: state reset failed");
   }
@@ -2491,10 +2521,7 @@ int cudasp_stream_stats(const cudasp_stream* st, uint64_t* launches, uint32_t* b
 int cudasp_stream_counters(cudasp_stream* st, uint64_t* out, uint32_t count) {
   if (!st || !out) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
   std::lock_guard<std::mutex> lk(st->mu);
-  DeviceGuard g(st->s->device);
-  unsigned long long v[16] = {};
-  HIP_TRY(hipMemcpy(v, st->dev->stat, sizeof(v), hipMemcpyDeviceToHost));
-  for (uint32_t i = 0; i < count && i < 16; i++) out[i] = v[i];
+  for (uint32_t i = 0; i < count && i < 16; i++) out[i] = st->last_stat[i];
   return CUDASP_OK;
 }
 

@@ -31,8 +31,9 @@
 //     flags the stream abandoned and leaves (a host that never closes).
 // Pieces and the pipelined schedule are k_scan_multi's (one inversion per
 // piece); a piece never spans two batches.  This header holds the data
-// structures and the pure scheduling rules (host + device: the CPU tests
-// replay them); the kernel is in scan_kernels.hip.
+// structures and the pure scheduling rules (host + device;
+// tests/test_stream_rules_cpu.py replays them and the ring lookup); the
+// kernel is in scan_kernels.hip.
 #pragma once
 #include <stdint.h>
 

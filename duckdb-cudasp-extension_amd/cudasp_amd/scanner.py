@@ -279,7 +279,7 @@ class ScanStream:
                 "poller_polls", "busy_ticks", "life_ticks")
 
     def counters(self):
-        """The kernel's counters for the current query (cudasp_stream_counters)."""
+        """The kernel's counters of the last finished query (cudasp_stream_counters)."""
         v = (ctypes.c_uint64 * 16)()
         _native.check(self._lib.cudasp_stream_counters(self._h, v, 16))
         return dict(zip(self.COUNTERS, list(v)))

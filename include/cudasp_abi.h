@@ -215,8 +215,9 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
  *                       kernel, then resets the stream for reuse (sequence
  *                       numbers start again at 0).
  *   cudasp_stream_stats  kernel launches so far and grid blocks.
- *   cudasp_stream_counters  the kernel's counters of the current query
- *                       (reset by finish): pieces, wave-rows, idle polls,
+ *   cudasp_stream_counters  the kernel's counters of the last finished
+ *                       query (taken by finish; reading them while the
+ *                       kernel runs could wait for it): pieces, wave-rows, idle polls,
  *                       pipeline drains, claim retries, worker exits on the
  *                       idle timeout and on close, poller polls, workers'
  *                       busy and lifetime ticks (100 MHz). */

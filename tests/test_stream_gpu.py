@@ -131,8 +131,8 @@ def test_stream_slow_publisher(torch):
             q = sb.publish(st)
             st.wait(q)
             time.sleep(0.05)
-        c = st.counters()
         st.finish()
+        c = st.counters()  # the finished query's
         assert st.stats()["launches"] == 1
     assert c["wait_polls"] > 0
     flags_equal([sb.result() for sb in stage], want)

@@ -1,0 +1,93 @@
+"""CPU replay of the streaming scan's scheduling rules
+(duckdb-cudasp-extension_amd/csrc/scan_stream.hpp, k_scan_stream in
+scan_kernels.hip): the ticket size rule, and the descriptor-ring lookup a wave
+makes for each of its wave-rows -- a walk forward from its hint, started no
+earlier than pub - STREAM_RING, skipping entries that hold another batch.
+
+The replay drives the host's publish rule (batch X only once X - STREAM_RING
+is done) with batches completing out of order, and checks that every lookup
+of a not-yet-done wave-row finds its batch within three passes of the ring,
+including a wave whose first hint is 0 after the ring has wrapped many times
+(the case a walk from the hint alone missed) and a stale `pub` one poller
+pass behind."""
+import random
+
+STREAM_RING = 64
+
+
+def stream_piece_rows(rem, waves, rmax):
+    r = rem // waves if waves else rmax
+    return max(1, min(rmax, r))
+
+
+def batch_of(ring, pub, hint, w):
+    """stream_batch_of: ring[e] = (seq, first_wr, nwr) of the batch last
+    mirrored at entry e; returns (batch, steps)."""
+    b = hint
+    if pub > STREAM_RING and b < pub - STREAM_RING:
+        b = pub - STREAM_RING
+    for i in range(3 * STREAM_RING):
+        seq, first, nwr = ring[b % STREAM_RING]
+        if seq == b and w < first + nwr:
+            return b, i
+        b += 1
+    raise AssertionError("walk exceeded three passes of the ring")
+
+
+def test_piece_rows_rule():
+    assert stream_piece_rows(0, 3071, 6) == 1
+    assert stream_piece_rows(10 ** 6, 3071, 6) == 6
+    assert stream_piece_rows(3071 * 3, 3071, 6) == 3
+    assert stream_piece_rows(5, 0, 4) == 4
+
+
+def test_ring_lookup_out_of_order_completion():
+    rng = random.Random(7)
+    ring = [(None, 0, 0)] * STREAM_RING
+    first = []          # first wave-row of each batch
+    nwr = []
+    done = set()
+    pub = 0
+    wr = 0
+    max_steps = 0
+    for step in range(20000):
+        # publish while the rule allows (X - RING done), up to a random depth
+        while rng.random() < 0.6 and (pub < STREAM_RING or (pub - STREAM_RING) in done):
+            n = rng.randint(1, 12)
+            first.append(wr)
+            nwr.append(n)
+            ring[pub % STREAM_RING] = (pub, wr, n)
+            wr += n
+            pub += 1
+        live = [b for b in range(max(0, pub - STREAM_RING), pub) if b not in done]
+        if not live:
+            continue
+        # a wave looks up a wave-row of a live batch, from a stale hint and a
+        # pub up to one poller pass behind
+        b = rng.choice(live)
+        w = first[b] + rng.randrange(nwr[b])
+        hint = rng.choice([0, max(0, b - rng.randint(0, 3 * STREAM_RING)), b])
+        seen_pub = max(b + 1, pub - rng.randint(0, STREAM_RING))
+        got, steps = batch_of(ring, seen_pub, hint, w)
+        assert got == b
+        max_steps = max(max_steps, steps)
+        # complete a random live batch (out of order)
+        done.add(rng.choice(live))
+    assert pub > 10 * STREAM_RING  # the ring wrapped many times
+    assert max_steps <= 3 * STREAM_RING
+
+
+def test_walk_from_hint_alone_misses_after_wraps():
+    """The bound the lookup had before the pub lower bound: a first hint of
+    0 and two passes of the ring do not reach a batch >= 2 * STREAM_RING."""
+    ring = [(None, 0, 0)] * STREAM_RING
+    for b in range(150):
+        ring[b % STREAM_RING] = (b, b, 1)
+    b, w = 0, 140
+    for _ in range(2 * STREAM_RING):
+        seq, first, n = ring[b % STREAM_RING]
+        if seq == b and w < first + n:
+            break
+        b += 1
+    assert b != 140
+    assert batch_of(ring, 150, 0, w) == (140, 140 - (150 - STREAM_RING))

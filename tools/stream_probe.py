@@ -95,8 +95,8 @@ def main():
                     for q in seqs:
                         st.wait(q)
                     times.append(time.perf_counter() - t)
-                    out["counters_%s" % mode] = st.counters()
                     st.finish()
+                    out["counters_%s" % mode] = st.counters()
                     for i, (sb, w, d) in enumerate(zip(stage, want, dev_in)):
                         res = d["dflags"].cpu().numpy() if mode == "dev_all" else sb.result()
                         if not (res == w).all():
