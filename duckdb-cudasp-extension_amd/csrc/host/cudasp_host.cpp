@@ -417,9 +417,10 @@ struct cudasp_tf_global {
   std::unique_ptr<std::mutex[]> feed_create_mu;
   int hw_queues = 0;  // GPU_MAX_HW_QUEUES at init (HIP's default 4 when unset)
   int max_streams_per_device = 0;
-  // Streaming feeds (one persistent kernel per feed, cudasp_stream_*): with
-  // the default options and one feed per device; CUDASP_TF_MODE=launch
-  // selects the per-slot launches.
+  // Streaming feeds (one persistent kernel per feed, cudasp_stream_*):
+  // opt-in with CUDASP_TF_MODE=stream (the default options and one feed per
+  // device only); the per-slot launches are the default (measured faster end
+  // to end).
   bool streaming = false;
 };
 
@@ -1278,7 +1279,7 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
     // queue (HIP shares queues among streams) and the second would wait for
     // the first to end -- logical GPUs sharing a device (CUDASP_TF_DEVICE_MAP)
     // take the per-slot launches
-    g->streaming = !(mode && !strcmp(mode, "launch")) && b->opt.output_count == 1 && feeds_per_device == 1;
+    g->streaming = mode && !strcmp(mode, "stream") && b->opt.output_count == 1 && feeds_per_device == 1;
     if (g->streaming) g->feed_streams = 1;
   }
   g->feeds.resize(g->num_gpus);

@@ -683,10 +683,13 @@ __device__ __forceinline__ uint32_t stream_batch_of(StreamDev* dev, uint32_t hin
     // once b is done) with its seq invalidated first and set last, so a
     // range read between two equal seq loads belongs to batch b; an entry
     // rewritten meanwhile held a done batch, not w's
+    // (agent-scope loads are served by the L2, so ordering them with vmcnt
+    // waits is the acquire; no cache of the CU is invalidated)
     const StreamBatch* d = &dev->desc[b % STREAM_RING];
-    if (__hip_atomic_load(&d->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != b) continue;
+    if (dev_load_u64(&d->seq) != b) continue;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t end = dev_load_u64(&d->first_wr) + dev_load_u32(&d->nwr);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (dev_load_u64(&d->seq) != b) continue;
     if (w < end) break;
   }
@@ -832,7 +835,6 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
     if (lane == 0) stream_poll(ctrl, dev, abandon_ticks);
     return;
   }
-  const uint32_t workers = gridDim.x * (BLOCK / 64) - 1;
   constexpr int PB = VB_SCRATCH_WORDS;
   constexpr int LB = VB_SCRATCH_WORDS + PEND_WORDS * multi_pend_slots(true);
   const int QF = LB + FW * (int)k.label_count * MULTI_RMAX;
@@ -842,12 +844,15 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
   uint64_t base_p = 0, base_q = 0;
   int count_p = 0, count_q = 0;
   uint32_t hint_p = 0, hint_q = 0, hint = 0, hits_q = 0;
-  // the wave's ticket (lane 0): wave-rows [tk, tk + tr), held since t_wait
-  bool have = false;
-  uint64_t tk = 0, t_wait = 0;
-  uint32_t tr = 0;
-  const uint64_t t_start = wall_clock64();
-  uint64_t busy = 0, pieces = 0, rows = 0;
+  // lane 0's ticket and counters live in LDS, so none of them is held in
+  // registers through a piece's ladders
+  __shared__ StreamWave waves[BLOCK / 64];
+  volatile StreamWave& me = waves[threadIdx.x >> 6];
+  if (lane == 0) {
+    me.tk = me.tr = me.have = me.mine = 0;
+    me.t_start = me.t_wait = wall_clock64();
+    me.busy = me.pieces = me.rows = me.polls = me.drains = 0;
+  }
   uint32_t stop = 0;  // 2: closed and past the end, 3: abandoned; leave once drained
   for (;;) {
     const uint64_t t_it = wall_clock64();
@@ -856,34 +861,45 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
     uint32_t status = 0, cnt = 0;
     uint64_t tbase = 0;
     if (lane == 0 && !stop) {
-      if (!have) {
-        const uint64_t cur = dev_load_u64(&dev->ticket), pw = dev_load_u64(&dev->pub_wr);
-        tr = stream_piece_rows(pw > cur ? pw - cur : 0, workers, rmax);
-        tk = atomicAdd(reinterpret_cast<unsigned long long*>(&dev->ticket), (unsigned long long)tr);
-        have = true;
-        t_wait = t_it;
-      }
+      // the device state is read with agent-scope loads, which the L2 serves
+      // (no L1 copy): ordering the loads (vmcnt) is all an acquire needs here,
+      // and no cache of the CU is invalidated
       const uint32_t cl = dev_load_u32(&dev->closed);
-      if (cl) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pub_wr is final
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pub_wr is final once closed is seen
       const uint64_t pw = dev_load_u64(&dev->pub_wr);
-      if (tk < pw) {
+      if (!me.have) {
+        // claim only published rows: the wave's share of what is published
+        // and unclaimed (k_scan_multi's adaptive rule: rem x mine / claimed)
+        const uint64_t cur = dev_load_u64(&dev->ticket);
+        if (pw > cur) {
+          const uint32_t tr = stream_piece_rows(pw - cur, cur, me.mine, rmax);
+          me.tk = atomicAdd(reinterpret_cast<unsigned long long*>(&dev->ticket), (unsigned long long)tr);
+          me.tr = tr;
+          me.mine = me.mine + tr;
+          me.have = 1;
+          me.t_wait = t_it;
+        }
+      }
+      const uint64_t tk = me.tk;
+      if (me.have && tk < pw) {
         // the published part of the ticket now; an unpublished rest stays
         // the wave's ticket (the host may wait for this part's batch before
         // it publishes more)
         status = 1;
+        const uint32_t tr = me.tr;
         cnt = tk + tr <= pw ? tr : (uint32_t)(pw - tk);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the mirrored descriptors
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the mirrored descriptors after pub_wr
         tbase = tk;
-        tk += cnt;
-        tr -= cnt;
-        have = tr != 0;
-        t_wait = t_it;
+        me.tk = tk + cnt;
+        me.tr = tr - cnt;
+        me.have = tr != cnt;
+        me.t_wait = t_it;
       } else if (cl) {
-        status = 2;  // closed, and the ticket lies past the last row
-        have = false;
-      } else if (t_it - t_wait > abandon_ticks) {
+        status = 2;  // closed, and the ticket (if any) lies past the last row
+        me.have = 0;
+      } else if (t_it - me.t_wait > abandon_ticks) {
         status = 3;
-        have = false;
+        me.have = 0;
       }
     }
     status = (uint32_t)__builtin_amdgcn_readfirstlane((int)status);
@@ -896,17 +912,21 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
           __hip_atomic_store(&ctrl->abandoned, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
-      if (lane == 0) atomicAdd(&dev->stat[STREAM_STAT_WAIT_POLLS], 1ull);
-      __builtin_amdgcn_s_sleep(64);
+      if (lane == 0) me.polls = me.polls + 1;
+      __builtin_amdgcn_s_sleep(32);
       continue;
     }
-    if (count == 0 && lane == 0) atomicAdd(&dev->stat[STREAM_STAT_DRAINS], 1ull);
+    if (lane == 0) {
+      if (count == 0) me.drains = me.drains + 1;
+      if (count) {
+        me.pieces = me.pieces + 1;
+        me.rows = me.rows + (uint32_t)count;
+      }
+    }
     uint32_t hint_c = hint;
     if (count) {
       hint_c = stream_batch_of(dev, hint, base);
       hint = hint_c;
-      pieces++;
-      rows += (uint32_t)count;
     }
     // stage A: S = d T of the new piece's rows (read from the pinned slot)
     {
@@ -1012,14 +1032,16 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
     base_p = base;
     hint_p = hint_c;
     count_p = count;
-    busy += wall_clock64() - t_it;
+    if (lane == 0) me.busy = me.busy + (wall_clock64() - t_it);
   }
   if (lane == 0) {
     atomicAdd(&dev->stat[stop == 3 ? STREAM_STAT_EXIT_ABANDONED : STREAM_STAT_EXIT_CLOSED], 1ull);
-    atomicAdd(&dev->stat[STREAM_STAT_PIECES], pieces);
-    atomicAdd(&dev->stat[STREAM_STAT_WAVE_ROWS], rows);
-    atomicAdd(&dev->stat[STREAM_STAT_BUSY_TICKS], busy);
-    atomicAdd(&dev->stat[STREAM_STAT_LIFE_TICKS], wall_clock64() - t_start);
+    atomicAdd(&dev->stat[STREAM_STAT_PIECES], (unsigned long long)me.pieces);
+    atomicAdd(&dev->stat[STREAM_STAT_WAVE_ROWS], (unsigned long long)me.rows);
+    atomicAdd(&dev->stat[STREAM_STAT_WAIT_POLLS], (unsigned long long)me.polls);
+    atomicAdd(&dev->stat[STREAM_STAT_DRAINS], (unsigned long long)me.drains);
+    atomicAdd(&dev->stat[STREAM_STAT_BUSY_TICKS], (unsigned long long)me.busy);
+    atomicAdd(&dev->stat[STREAM_STAT_LIFE_TICKS], (unsigned long long)(wall_clock64() - me.t_start));
   }
 }
 

@@ -104,14 +104,26 @@ enum {
   STREAM_STAT_COUNT
 };
 
-// Wave-rows of the next ticket.  rem: published wave-rows not yet handed
-// out; waves: the workers.  The wave's share of what is available now,
-// rem / waves (1 .. rmax), as k_scan_multi's guided rule: a full backlog gives
-// rmax rows per thread (one inversion for rmax rows), the first small slots
-// of a query and the end of the table single wave-rows to many waves.
-CUDASP_HD uint32_t stream_piece_rows(uint64_t rem, uint32_t waves, uint32_t rmax) {
-  const uint64_t r = waves ? rem / waves : rmax;
+// Wave-rows of the next ticket, claimed only while published rows are
+// unclaimed (rem > 0): k_scan_multi's adaptive rule, rem x mine / claimed
+// (the wave's share of the work done so far: the three waves of a SIMD
+// progress at ~1 : 0.3 : 0.05, so equal pieces would leave the slowest
+// wave's piece as the tail), at least 1 and at most rmax; a wave's first
+// claim is one wave-row.  A backlog of published batches gives rmax rows per
+// thread (one inversion for rmax rows); a host slower than the GPU leaves
+// small pieces, which cost only the GPU's slack.
+CUDASP_HD uint32_t stream_piece_rows(uint64_t rem, uint64_t claimed, uint32_t mine, uint32_t rmax) {
+  if (mine == 0 || claimed == 0) return 1u;
+  const uint64_t r = rem * mine / claimed;
   return r < 1 ? 1u : (r > rmax ? rmax : (uint32_t)r);
 }
+
+// A worker wave's bookkeeping, kept by its lane 0 in LDS (k_scan_stream):
+// the ticket (wave-rows [tk, tk + tr), held since t_wait), rows claimed in
+// the query, and the counters flushed to StreamDev::stat when it leaves.
+struct StreamWave {
+  uint64_t tk, t_wait, t_start, busy;
+  uint32_t tr, have, mine, pieces, rows, polls, drains;
+};
 
 }  // namespace cudasp

@@ -209,3 +209,4 @@ def test_stream_rejects_bad_use(torch):
         with pytest.raises(CudaspError):
             ScanStream(s)
     assert StreamBatch is not None
+

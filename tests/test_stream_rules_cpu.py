@@ -15,9 +15,10 @@ import random
 STREAM_RING = 64
 
 
-def stream_piece_rows(rem, waves, rmax):
-    r = rem // waves if waves else rmax
-    return max(1, min(rmax, r))
+def stream_piece_rows(rem, claimed, mine, rmax):
+    if mine == 0 or claimed == 0:
+        return 1
+    return max(1, min(rmax, rem * mine // claimed))
 
 
 def batch_of(ring, pub, hint, w):
@@ -35,10 +36,32 @@ def batch_of(ring, pub, hint, w):
 
 
 def test_piece_rows_rule():
-    assert stream_piece_rows(0, 3071, 6) == 1
-    assert stream_piece_rows(10 ** 6, 3071, 6) == 6
-    assert stream_piece_rows(3071 * 3, 3071, 6) == 3
-    assert stream_piece_rows(5, 0, 4) == 4
+    assert stream_piece_rows(1000, 0, 0, 6) == 1           # first claim: one wave-row
+    assert stream_piece_rows(10 ** 6, 3071, 1, 6) == 6      # a backlog: rmax
+    assert stream_piece_rows(3071 * 3, 3071 * 10, 10, 6) == 3  # a fair share of the rest
+    assert stream_piece_rows(100, 3071 * 10, 30, 6) == 1    # the tail: single wave-rows
+    # a wave that did 3x the average work gets 3x the piece
+    assert stream_piece_rows(3071 * 2, 3071 * 10, 30, 6) == 6
+
+
+def test_adaptive_claims_drain_together():
+    """Waves progressing at 1 : 0.3 : 0.05 (a SIMD's three waves) over a
+    fully published table: with the adaptive rule the last piece of the
+    slowest wave ends close to the others' (the tail is a small fraction of
+    the run), where equal pieces would leave the slow wave's rmax piece."""
+    speeds = [1.0, 0.3, 0.05] * 64
+    total, rmax = 20000, 6
+    claimed = 0
+    mine = [0] * len(speeds)
+    free_at = [0.0] * len(speeds)
+    while claimed < total:
+        w = min(range(len(speeds)), key=lambda i: free_at[i])
+        r = min(stream_piece_rows(total - claimed, claimed, mine[w], rmax), total - claimed)
+        claimed += r
+        mine[w] += r
+        free_at[w] += r / speeds[w]
+    ideal = total / sum(speeds)
+    assert max(free_at) < 1.15 * ideal
 
 
 def test_ring_lookup_out_of_order_completion():
