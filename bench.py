@@ -493,7 +493,7 @@ def host_cores():
     return visible, visible, "sched_getaffinity"
 
 
-def e2e_leg(args, labels, world, fb_bits):
+def e2e_leg(args, labels, world, fb_bits, mode=None):
     """PCIe-inclusive end-to-end rate through the table-function host
     (include/cudasp_host.h, the calls DuckDB's executor makes) over all
     `world` GPUs: tools/host_e2e as a fresh child process (this process only
@@ -505,7 +505,10 @@ def e2e_leg(args, labels, world, fb_bits):
     fixed-base tables), then `reps` queries are timed and the median is
     reported; every query must emit exactly the planted rows.  The child runs
     with the environment's GPU_MAX_HW_QUEUES (HIP's default 4 unless
-    --e2e-hw-queues sets one)."""
+    --e2e-hw-queues sets one).  The host's default is its streaming feeds
+    (one persistent kernel per device reading the slots in place, DESIGN.md
+    section 7c); mode="launch" selects its per-slot launches
+    (CUDASP_TF_MODE=launch)."""
     import subprocess
     import tempfile
     exe = os.path.join(ROOT, "tools", "host_e2e")
@@ -514,6 +517,9 @@ def e2e_leg(args, labels, world, fb_bits):
     threads = args.e2e_threads or 8 * world
     reps = args.e2e_reps or (5 if args.rows <= 2_000_000 else 3 if args.rows <= 10_000_000 else 1)
     env = dict(os.environ, CUDASP_FB_BITS=str(fb_bits))
+    env.pop("CUDASP_TF_MODE", None)
+    if mode:
+        env["CUDASP_TF_MODE"] = mode
     if args.e2e_hw_queues:
         env["GPU_MAX_HW_QUEUES"] = str(args.e2e_hw_queues)
     lf = None
@@ -855,6 +861,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layout-probe", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-e2e-launch", action="store_true",
+                    help="skip the second end-to-end leg with the host's per-slot launches (CUDASP_TF_MODE=launch)")
     ap.add_argument("--e2e-threads", type=int, default=0, help="executor threads of the e2e leg; 0 = 8 per GPU")
     ap.add_argument("--e2e-reps", type=int, default=0, help="timed e2e queries (median); 0 = by table size")
     ap.add_argument("--e2e-input", choices=["rows", "columns"], default="rows")
@@ -1076,6 +1084,12 @@ def main():
             e2e = e2e_leg(args, labels, world, args.fb_bits)
             result["e2e"] = e2e
             result["e2e_tx_s"] = e2e.get("tx_per_s")
+            if not args.no_e2e_launch:
+                # the same child with the host's per-slot launches (each slot
+                # copied to the device and scanned by its own k_scan_multi)
+                el = e2e_leg(args, labels, world, args.fb_bits, mode="launch")
+                result["e2e_launch"] = el
+                result["e2e_launch_tx_s"] = el.get("tx_per_s")
         if world > 1:
             dist.barrier(group=cpu_group)
     if rank == 0:

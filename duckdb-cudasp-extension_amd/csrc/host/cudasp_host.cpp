@@ -65,9 +65,11 @@ constexpr uint32_t XONLY_SIZE = 32;      // full_x outputs: x-only keys
 constexpr int FEED_MAX_STREAMS = 4;
 // A streaming feed (one persistent kernel, cudasp_stream_*) keeps more slots
 // in flight: the kernel's waves hold up to ~1.2M rows at once in 6-row
-// pieces, so 8 slots of 300k rows keep published work ahead of them while
-// the executor threads fill the next ones.
-constexpr int FEED_STREAM_SLOTS = 8;
+// pieces, and published work must stay ahead of them while the executor
+// threads fill the next slots (paced probe at 9.4M rows, 1 label: 148.7 M
+// tx/s with 8 slots in flight, 164.0 with 16, 166.6 with all published;
+// profiles/r03_stream_iter2.txt).
+constexpr int FEED_STREAM_SLOTS = 16;
 constexpr int FEED_MAX_SLOTS = FEED_STREAM_SLOTS > FEED_MAX_STREAMS + 2 ? FEED_STREAM_SLOTS : FEED_MAX_STREAMS + 2;
 // Rows resident on the GPU at once in k_scan_multi launches of 4 rows per
 // thread: 256 CUs x 4 SIMDs x 3 waves x 64 lanes x 4 rows.
@@ -417,10 +419,10 @@ struct cudasp_tf_global {
   std::unique_ptr<std::mutex[]> feed_create_mu;
   int hw_queues = 0;  // GPU_MAX_HW_QUEUES at init (HIP's default 4 when unset)
   int max_streams_per_device = 0;
-  // Streaming feeds (one persistent kernel per feed, cudasp_stream_*):
-  // opt-in with CUDASP_TF_MODE=stream (the default options and one feed per
-  // device only); the per-slot launches are the default (measured faster end
-  // to end).
+  // Streaming feeds (one persistent kernel per feed, cudasp_stream_*): the
+  // default with the default options and one feed per device (measured
+  // faster end to end); CUDASP_TF_MODE=launch selects the
+  // per-slot launches.
   bool streaming = false;
 };
 
@@ -1279,7 +1281,7 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
     // queue (HIP shares queues among streams) and the second would wait for
     // the first to end -- logical GPUs sharing a device (CUDASP_TF_DEVICE_MAP)
     // take the per-slot launches
-    g->streaming = mode && !strcmp(mode, "stream") && b->opt.output_count == 1 && feeds_per_device == 1;
+    g->streaming = !(mode && !strcmp(mode, "launch")) && b->opt.output_count == 1 && feeds_per_device == 1;
     if (g->streaming) g->feed_streams = 1;
   }
   g->feeds.resize(g->num_gpus);

@@ -2408,7 +2408,7 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
   st->blocks_req = blocks;
   st->blocks = multi_grid_blocks(s, blocks, true);
   if (st->blocks < 2) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the streaming scan");
-  uint32_t abandon_s = 120;
+  uint32_t abandon_s = 600;
   if (const char* e = getenv("CUDASP_STREAM_ABANDON_S")) {
     const long v = atol(e);
     if (v >= 1 && v <= 86400) abandon_s = (uint32_t)v;

@@ -42,7 +42,7 @@
 namespace cudasp {
 
 // Batches published and not yet harvested, at most (the host's slot ring is
-// far smaller: a feed has 8 slots).
+// far smaller: a streaming feed has 16 slots).
 constexpr uint32_t STREAM_RING = 64;
 
 // One published batch, written by the host before it bumps `published`.

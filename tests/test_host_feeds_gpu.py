@@ -191,12 +191,12 @@ def test_host_error_mid_query_then_pool_reuse(table16, keys):  # noqa: F811
 
 @pytest.mark.parametrize("threads,batch", [(3, 2500), (8, 300000)])
 def test_host_streaming_feed_16_labels(table16, keys, threads, batch, monkeypatch):  # noqa: F811
-    """Streaming feeds (CUDASP_TF_MODE=stream: each closed slot is published
-    to the feed's one persistent k_scan_stream kernel, which reads it from
-    pinned host memory in place): the emitted rows are the oracle's, through
-    more slots than the feed's ring holds (2500-row batches: ~10 slots over
-    8) and through the final partial slot alone; the pooled feed then serves
-    a per-slot-launch query with the same result."""
+    """Streaming feeds (the host's default, CUDASP_TF_MODE=stream: each
+    closed slot is published to the feed's one persistent k_scan_stream
+    kernel, which reads it from pinned host memory in place): the emitted
+    rows are the oracle's, through the final partial slot alone and through
+    many slots; the per-slot launches (CUDASP_TF_MODE=launch) give the same
+    result."""
     from cudasp_amd import cudasp_scan, release_pool
     rows, expected = table16
     scan, spend, labels = keys
@@ -207,7 +207,7 @@ def test_host_streaming_feed_16_labels(table16, keys, threads, batch, monkeypatc
     assert _heights(out) == expected
     _check_rows(out, rows)
     assert stats["rows"] == len(rows)
-    monkeypatch.delenv("CUDASP_TF_MODE")
+    monkeypatch.setenv("CUDASP_TF_MODE", "launch")
     stats = {}
     out = cudasp_scan(rows, scan, spend, labels, batch_size=batch, threads=threads, stats=stats)
     assert stats["streaming_feeds"] == 0
