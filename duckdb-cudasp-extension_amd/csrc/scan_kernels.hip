@@ -729,10 +729,14 @@ __device__ __forceinline__ uint32_t stream_lane_row(const StreamRow& sr, uint64_
 // The poller (lane 0 of one wave per kernel): mirrors new batches of the
 // host's control block into the device state -- descriptors first, then the
 // counts behind an agent-scope release -- and `closed` after the last one.
-// Leaves once closed is mirrored, or after abandon_ticks without a change.
-__device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t abandon_ticks) {
+// Leaves once closed is mirrored, or once the kernel has had nothing to do
+// for idle_ticks (no new batch, every published row claimed): it then sets
+// `idle`, the workers leave as they drain, and the GPU is free until the
+// host's next publish or wait relaunches the kernel (cudasp_stream_*).
+__device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_ticks) {
   uint32_t seen = dev_load_u32(&dev->pub);
   uint64_t last = wall_clock64();
+  uint64_t polls = 0;
   for (;;) {
     // the control block is uncached host memory (MTYPE UC): relaxed
     // system-scope loads read it fresh without invalidating any cache; the
@@ -771,12 +775,19 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t abandon_t
     }
     if (cl) {  // `published` was read after `closed`: every batch is mirrored
       __hip_atomic_store(&dev->closed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      return;
+      break;
     }
-    if (now - last > abandon_ticks) return;
-    atomicAdd(&dev->stat[STREAM_STAT_POLLER_POLLS], 1ull);
+    if (dev_load_u64(&dev->ticket) < dev_load_u64(&dev->pub_wr)) {
+      last = now;  // rows still unclaimed: not idle
+    } else if (now - last > idle_ticks) {
+      __hip_atomic_store(&dev->idle, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd(&dev->stat[STREAM_STAT_IDLE_EXITS], 1ull);
+      break;
+    }
+    polls++;
     __builtin_amdgcn_s_sleep(32);
   }
+  atomicAdd(&dev->stat[STREAM_STAT_POLLER_POLLS], (unsigned long long)polls);
 }
 
 // Flags of wave-rows base .. base + count - 1 into their pinned slots, then
@@ -827,12 +838,12 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
                                                                     const uint32_t* __restrict__ fb,
                                                                     const uint32_t* __restrict__ labels,
                                                                     uint32_t* __restrict__ scr, uint32_t rmax,
-                                                                    uint64_t abandon_ticks) {
+                                                                    uint64_t idle_ticks) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = SCAN_SCRATCH(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
   if (blockIdx.x == 0 && threadIdx.x < 64) {  // one wave of the grid is the poller
-    if (lane == 0) stream_poll(ctrl, dev, abandon_ticks);
+    if (lane == 0) stream_poll(ctrl, dev, idle_ticks);
     return;
   }
   constexpr int PB = VB_SCRATCH_WORDS;
@@ -850,26 +861,27 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
   volatile StreamWave& me = waves[threadIdx.x >> 6];
   if (lane == 0) {
     me.tk = me.tr = me.have = me.mine = 0;
-    me.t_start = me.t_wait = wall_clock64();
+    me.t_start = wall_clock64();
     me.busy = me.pieces = me.rows = me.polls = me.drains = 0;
   }
-  uint32_t stop = 0;  // 2: closed and past the end, 3: abandoned; leave once drained
+  bool stop = false;  // closed or idle, nothing published left in the ticket: leave once drained
   for (;;) {
     const uint64_t t_it = wall_clock64();
-    // 0: the ticket waits for the host; 1: ready (count rows); 2: the stream
-    // is closed and the ticket is past its end; 3: abandoned
-    uint32_t status = 0, cnt = 0;
+    uint32_t status = 0, cnt = 0;  // 0: nothing to do now; 1: cnt published rows of the ticket; 2: leave
     uint64_t tbase = 0;
     if (lane == 0 && !stop) {
       // the device state is read with agent-scope loads, which the L2 serves
       // (no L1 copy): ordering the loads (vmcnt) is all an acquire needs here,
       // and no cache of the CU is invalidated
-      const uint32_t cl = dev_load_u32(&dev->closed);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pub_wr is final once closed is seen
+      const uint32_t fin = dev_load_u32(&dev->closed) | dev_load_u32(&dev->idle);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pub_wr is final once closed / idle is seen
       const uint64_t pw = dev_load_u64(&dev->pub_wr);
       if (!me.have) {
-        // claim only published rows: the wave's share of what is published
-        // and unclaimed (k_scan_multi's adaptive rule: rem x mine / claimed)
+        // claim only while published rows are unclaimed: the wave's share of
+        // them (k_scan_multi's adaptive rule).  A single atomicAdd, never a
+        // retry (a compare-and-swap claim contends: 5M retries at 9.4M rows,
+        // profiles/r03_stream_cas_claims.txt), so concurrent claims may pass
+        // pub_wr; such a ticket waits for the host's next batch
         const uint64_t cur = dev_load_u64(&dev->ticket);
         if (pw > cur) {
           const uint32_t tr = stream_piece_rows(pw - cur, cur, me.mine, rmax);
@@ -877,7 +889,6 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
           me.tr = tr;
           me.mine = me.mine + tr;
           me.have = 1;
-          me.t_wait = t_it;
         }
       }
       const uint64_t tk = me.tk;
@@ -893,25 +904,20 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
         me.tk = tk + cnt;
         me.tr = tr - cnt;
         me.have = tr != cnt;
-        me.t_wait = t_it;
-      } else if (cl) {
-        status = 2;  // closed, and the ticket (if any) lies past the last row
-        me.have = 0;
-      } else if (t_it - me.t_wait > abandon_ticks) {
-        status = 3;
+      } else if (fin) {
+        // closed: the ticket lies past the last row; idle: its rows were
+        // never published to this kernel (pub_wr is final), so none of them
+        // is processed and the relaunch hands them out again from pub_wr
+        status = 2;
         me.have = 0;
       }
     }
     status = (uint32_t)__builtin_amdgcn_readfirstlane((int)status);
     const int count = __builtin_amdgcn_readfirstlane((int)cnt);
     const uint64_t base = uniform_u64(tbase);
-    if (status >= 2) stop = status;
+    if (status == 2) stop = true;
     if (count == 0 && count_p == 0 && count_q == 0) {
-      if (stop) {  // closed (or abandoned) and nothing left
-        if (stop == 3 && lane == 0)
-          __hip_atomic_store(&ctrl->abandoned, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
+      if (stop) break;  // closed (or idle) and nothing left
       if (lane == 0) me.polls = me.polls + 1;
       __builtin_amdgcn_s_sleep(32);
       continue;
@@ -1035,7 +1041,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
     if (lane == 0) me.busy = me.busy + (wall_clock64() - t_it);
   }
   if (lane == 0) {
-    atomicAdd(&dev->stat[stop == 3 ? STREAM_STAT_EXIT_ABANDONED : STREAM_STAT_EXIT_CLOSED], 1ull);
+    atomicAdd(&dev->stat[STREAM_STAT_WORKER_EXITS], 1ull);
     atomicAdd(&dev->stat[STREAM_STAT_PIECES], (unsigned long long)me.pieces);
     atomicAdd(&dev->stat[STREAM_STAT_WAVE_ROWS], (unsigned long long)me.rows);
     atomicAdd(&dev->stat[STREAM_STAT_WAIT_POLLS], (unsigned long long)me.polls);
@@ -2322,9 +2328,11 @@ struct cudasp_stream {
   uint64_t blocks_req = 0;  // requested grid (0: the whole device)
   uint64_t blocks = 0;      // the current query's grid
   uint32_t rmax = MULTI_RMAX;
-  uint64_t abandon_ticks = 0;  // 100 MHz wall-clock ticks a wave waits for the host before it gives up
+  uint64_t idle_ticks = 0;  // 100 MHz wall-clock ticks with nothing to do before the kernel leaves
   hipEvent_t exited = nullptr;
   bool running = false;     // a kernel was launched and `exited` recorded after it
+  bool failed = false;      // a kernel of this query failed (sticky until finish)
+  bool next_launch_resets = false;  // a kernel of this query ran: the next one follows k_stream_relaunch
   uint32_t next = 0;        // batches published
   uint64_t published_wr = 0;
   uint64_t launches = 0;
@@ -2332,24 +2340,37 @@ struct cudasp_stream {
   std::mutex mu;            // publish / launch / finish
 };
 
-// Caller holds st->mu.  Whether this query's kernel is still running; a
-// kernel that ended before the stream was closed gave up (abandoned) or failed.
+// Caller holds st->mu.  Whether the query's kernel is still running.  One
+// that ended before the stream was closed left idle (or failed: sticky).
 static bool stream_kernel_alive(cudasp_stream* st, int* err) {
   *err = CUDASP_OK;
   if (!st->running) return false;
   const hipError_t e = hipEventQuery(st->exited);
   if (e == hipErrorNotReady) return true;
   st->running = false;
-  if (e != hipSuccess)
+  if (e != hipSuccess) {
+    st->failed = true;
     *err = set_error(CUDASP_ERR_HIP, "streaming scan kernel failed: %s", hipGetErrorString(e));
-  else if (__atomic_load_n(&st->ctrl->abandoned, __ATOMIC_ACQUIRE))
-    *err = set_error(CUDASP_ERR_HIP, "streaming scan kernel gave up waiting for the host (stream never closed)");
+  }
   return false;
 }
 
-// Caller holds st->mu.  Launch the query's kernel at its first batch, with
-// the scanner's current keys and options (a host may rebind the scanner
-// between queries: the grid and its scratch follow the label count).
+// Before a relaunch (same stream, after the idle kernel ended): the claim
+// counter back to the rows mirrored so far -- claims past them were never
+// processed (the idle kernel's pub_wr was final) -- and `idle` cleared.
+__global__ void k_stream_relaunch(StreamDev* dev) {
+  if (threadIdx.x == 0) {
+    dev->ticket = dev->pub_wr;
+    dev->idle = 0;
+  }
+}
+
+// Caller holds st->mu.  Launch a kernel for the query: at its first batch,
+// or again after the previous one left idle (the device state -- claim
+// counter, mirrored descriptors, per-batch counts -- carries over; only
+// `idle` is cleared).  Uses the scanner's current keys and options (a host
+// may rebind the scanner between queries: the grid and its scratch follow
+// the label count).
 static int stream_launch(cudasp_stream* st) {
   cudasp_scanner* s = st->s;
   DeviceGuard g(s->device);
@@ -2361,14 +2382,26 @@ static int stream_launch(cudasp_stream* st) {
     const int rc = ensure_multi_scratch(s, st->blocks, true, s->stream);
     if (rc != CUDASP_OK) return rc;
   }
+  if (st->next_launch_resets) hipLaunchKernelGGL(k_stream_relaunch, dim3(1), dim3(64), 0, s->stream, st->dev);
   auto kf = s->fb_bits == 26 ? k_scan_stream<26> : k_scan_stream<22>;
   hipLaunchKernelGGL(kf, dim3((uint32_t)st->blocks), dim3(BLOCK), 0, s->stream, st->ctrl, st->dev, s->d_naf,
-                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, st->rmax, st->abandon_ticks);
+                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, st->rmax, st->idle_ticks);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(st->exited, s->stream));
   st->running = true;
+  st->next_launch_resets = true;
   st->launches++;
   return CUDASP_OK;
+}
+
+// Caller holds st->mu.  A kernel runs for the published batches: relaunched
+// if the last one left idle.
+static int stream_ensure_running(cudasp_stream* st) {
+  int err;
+  if (stream_kernel_alive(st, &err)) return CUDASP_OK;
+  if (err != CUDASP_OK) return err;
+  if (st->failed) return set_error(CUDASP_ERR_HIP, "streaming scan kernel failed earlier in this query");
+  return stream_launch(st);
 }
 
 static bool stream_seq_done(const cudasp_stream* st, uint64_t seq) {
@@ -2408,12 +2441,12 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
   st->blocks_req = blocks;
   st->blocks = multi_grid_blocks(s, blocks, true);
   if (st->blocks < 2) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the streaming scan");
-  uint32_t abandon_s = 600;
-  if (const char* e = getenv("CUDASP_STREAM_ABANDON_S")) {
+  uint32_t idle_ms = 20;
+  if (const char* e = getenv("CUDASP_STREAM_IDLE_MS")) {
     const long v = atol(e);
-    if (v >= 1 && v <= 86400) abandon_s = (uint32_t)v;
+    if (v >= 1 && v <= 600000) idle_ms = (uint32_t)v;
   }
-  st->abandon_ticks = (uint64_t)abandon_s * 100000000ull;
+  st->idle_ticks = (uint64_t)idle_ms * 100000ull;
   if (const char* e = getenv("CUDASP_MULTI_ROWS")) {
     const int v = atoi(e);
     if (v >= 1 && v <= MULTI_RMAX) st->rmax = (uint32_t)v;
@@ -2442,18 +2475,11 @@ int cudasp_stream_publish(cudasp_stream* st, const uint8_t* rows, const int64_t*
     return set_error(CUDASP_ERR_INVALID_ARG, "a streaming scan with labels needs an outputs mirror in device memory");
   std::lock_guard<std::mutex> lk(st->mu);
   if (st->ctrl->closed) return set_error(CUDASP_ERR_INVALID_ARG, "stream already finished");
+  if (st->failed) return set_error(CUDASP_ERR_HIP, "streaming scan kernel failed earlier in this query");
   const uint32_t b = st->next;
   const uint32_t e = b % STREAM_RING;
   if (b >= STREAM_RING && !stream_seq_done(st, (uint64_t)b - STREAM_RING))
     return set_error(CUDASP_ERR_CAPACITY, "more than %u streamed batches in flight", STREAM_RING);
-  if (b == 0) {  // one kernel per query, launched before its first batch and ended by finish
-    const int rc = stream_launch(st);
-    if (rc != CUDASP_OK) return rc;
-  } else {
-    int err;
-    if (!stream_kernel_alive(st, &err))
-      return err != CUDASP_OK ? err : set_error(CUDASP_ERR_HIP, "streaming scan kernel is gone");
-  }
   StreamBatch& d = st->ctrl->desc[e];
   d.rows = rows;
   d.outputs = outputs;
@@ -2470,7 +2496,9 @@ int cudasp_stream_publish(cudasp_stream* st, const uint8_t* rows, const int64_t*
   __atomic_store_n(&st->ctrl->published, b + 1, __ATOMIC_RELEASE);
   st->next = b + 1;
   if (seq) *seq = b;
-  return CUDASP_OK;
+  // the query's kernel: launched at its first batch, relaunched if it left
+  // idle (its poller picks the batch up from the control block either way)
+  return stream_ensure_running(st);
 }
 
 int cudasp_stream_query(cudasp_stream* st, uint64_t seq) {
@@ -2479,11 +2507,11 @@ int cudasp_stream_query(cudasp_stream* st, uint64_t seq) {
   std::lock_guard<std::mutex> lk(st->mu);
   if (seq >= st->next) return set_error(CUDASP_ERR_INVALID_ARG, "batch %llu was not published", (unsigned long long)seq);
   if (stream_seq_done(st, seq)) return 1;
-  int err;
-  if (!stream_kernel_alive(st, &err) && !stream_seq_done(st, seq))
-    return err != CUDASP_OK ? err : set_error(CUDASP_ERR_HIP, "streaming scan kernel ended before batch %llu was done",
-                                              (unsigned long long)seq);
-  return 0;
+  // not done: a kernel must be running for it (one that left idle while
+  // the batch was being published is relaunched here)
+  const int rc = stream_ensure_running(st);
+  if (rc != CUDASP_OK) return rc;
+  return stream_seq_done(st, seq) ? 1 : 0;
 }
 
 int cudasp_stream_wait(cudasp_stream* st, uint64_t seq) {
@@ -2509,14 +2537,14 @@ int cudasp_stream_finish(cudasp_stream* st) {
     rc = cudasp_stream_wait(st, b);
   std::lock_guard<std::mutex> lk(st->mu);
   DeviceGuard g(st->s->device);
-  if (st->running) {  // its waves leave as soon as they see the closed stream drained
+  if (st->running) {  // its waves leave as soon as they see the closed stream drained (or idle)
     const hipError_t e = hipEventSynchronize(st->exited);
     st->running = false;
     if (e != hipSuccess && rc == CUDASP_OK)
       rc = set_error(CUDASP_ERR_HIP, "streaming scan kernel failed: %s", hipGetErrorString(e));
   }
-  if (rc == CUDASP_OK && __atomic_load_n(&st->ctrl->abandoned, __ATOMIC_ACQUIRE))
-    rc = set_error(CUDASP_ERR_HIP, "streaming scan kernel gave up waiting for the host (stream never closed)");
+  st->failed = false;
+  st->next_launch_resets = false;
   // the query's counters (read here: while the kernel runs it holds every
   // wave slot, and a device-to-host copy could wait for it), then ready for
   // the next query

@@ -20,15 +20,17 @@
 //   * one poller wave per kernel reads the host's control block over PCIe
 //     (published count, descriptors, closed) and mirrors it into device
 //     memory; the worker waves take tickets of R wave-rows from one device
-//     counter (atomicAdd: a claim never fails or retries -- a compare-and-swap
-//     claim measured 160 retries per claim with 3071 waves, the kernel at a
-//     third of k_scan_multi's rate) and look each wave-row's batch up in the
-//     mirror.  A ticket beyond the published rows waits until the host
-//     publishes them or closes the stream (then the rows past the end are
-//     empty); every wave leaves once the stream is closed and its tickets are
-//     done, so the kernel lives for one query and the host's finish ends it.
-//     A wave that waits abandon_ticks (100 MHz wall clock) without either
-//     flags the stream abandoned and leaves (a host that never closes).
+//     counter (one atomicAdd while published rows are unclaimed: concurrent
+//     claims may pass the published rows, and such a ticket waits for the
+//     next batch) and look each wave-row's batch up in the mirror;
+//   * the kernel is elastic: every wave leaves once the stream is closed and
+//     drained, or once the poller has seen nothing to do for idle_ticks
+//     (CUDASP_STREAM_IDLE_MS, 100 MHz wall clock; every published row
+//     claimed, no new batch).  Rows past the mirrored pub_wr were never
+//     processed, so the host's next publish or wait relaunches the kernel
+//     with the claim counter reset to pub_wr (k_stream_relaunch).  A host
+//     that stalls (a slow source, or executor threads busy elsewhere) never
+//     holds the GPU, and a host that never closes leaves no kernel spinning.
 // Pieces and the pipelined schedule are k_scan_multi's (one inversion per
 // piece); a piece never spans two batches.  This header holds the data
 // structures and the pure scheduling rules (host + device;
@@ -66,7 +68,7 @@ struct StreamCtrl {
   uint32_t published;               // batches published (host; release)
   uint32_t closed;                  // 1: no batch follows (host)
   uint64_t published_wr;            // wave-rows published (host)
-  uint32_t abandoned;               // 1: a wave gave up waiting (kernel)
+  uint32_t reserved;
   uint32_t done[STREAM_RING];       // ring entry e: 1 + sequence number of the last batch completed there (kernel)
   StreamBatch desc[STREAM_RING];    // batch b at entry b % STREAM_RING
 };
@@ -80,32 +82,35 @@ struct StreamDev {
   uint64_t pub_wr;                  // mirror of StreamCtrl::published_wr
   uint32_t pub;                     // mirror of StreamCtrl::published
   uint32_t closed;                  // mirror of StreamCtrl::closed (set after the last pub)
+  uint32_t idle;                    // the poller left idle: the workers leave as they drain
+                                    // (reset by the host before it relaunches the kernel)
   uint32_t wr_done[STREAM_RING];    // wave-rows finished of the batch at each entry
   StreamBatch desc[STREAM_RING];    // mirror of StreamCtrl::desc
   // counters (cudasp_stream_counters): STREAM_STAT_* below
   unsigned long long stat[16];
 };
 
-// StreamDev::stat indices: pieces and wave-rows claimed, polls of a wave
-// waiting for its ticket, pipeline drains, batch lookups past a reused ring
-// entry, worker exits (abandoned / closed), poller polls, and the workers'
-// summed busy and lifetime in wall-clock ticks.
+// StreamDev::stat indices (summed over the query's kernel launches): pieces
+// and wave-rows claimed, polls of a wave with nothing to claim, pipeline
+// drains, (unused), worker exits, idle exits of the
+// poller (each one a kernel that left before the stream was closed), poller
+// polls, and the workers' summed busy and lifetime in wall-clock ticks.
 enum {
   STREAM_STAT_PIECES = 0,
   STREAM_STAT_WAVE_ROWS,
   STREAM_STAT_WAIT_POLLS,
   STREAM_STAT_DRAINS,
-  STREAM_STAT_LOOKUP_STEPS,
-  STREAM_STAT_EXIT_ABANDONED,
-  STREAM_STAT_EXIT_CLOSED,
+  STREAM_STAT_RESERVED,
+  STREAM_STAT_WORKER_EXITS,
+  STREAM_STAT_IDLE_EXITS,
   STREAM_STAT_POLLER_POLLS,
   STREAM_STAT_BUSY_TICKS,
   STREAM_STAT_LIFE_TICKS,
   STREAM_STAT_COUNT
 };
 
-// Wave-rows of the next ticket, claimed only while published rows are
-// unclaimed (rem > 0): k_scan_multi's adaptive rule, rem x mine / claimed
+// Wave-rows of the next claim (never past the published rows, rem > 0):
+// k_scan_multi's adaptive rule, rem x mine / claimed
 // (the wave's share of the work done so far: the three waves of a SIMD
 // progress at ~1 : 0.3 : 0.05, so equal pieces would leave the slowest
 // wave's piece as the tail), at least 1 and at most rmax; a wave's first
@@ -119,10 +124,10 @@ CUDASP_HD uint32_t stream_piece_rows(uint64_t rem, uint64_t claimed, uint32_t mi
 }
 
 // A worker wave's bookkeeping, kept by its lane 0 in LDS (k_scan_stream):
-// the ticket (wave-rows [tk, tk + tr), held since t_wait), rows claimed in
-// the query, and the counters flushed to StreamDev::stat when it leaves.
+// its ticket, wave-rows claimed in this launch and the counters flushed to
+// StreamDev::stat when it leaves.
 struct StreamWave {
-  uint64_t tk, t_wait, t_start, busy;
+  uint64_t tk, t_start, busy;  // tk: the ticket, wave-rows [tk, tk + tr)
   uint32_t tr, have, mine, pieces, rows, polls, drains;
 };
 

@@ -275,7 +275,7 @@ class ScanStream:
         _native.check(self._lib.cudasp_stream_stats(self._h, ctypes.byref(launches), ctypes.byref(blocks)))
         return {"launches": launches.value, "blocks": blocks.value}
 
-    COUNTERS = ("pieces", "wave_rows", "wait_polls", "drains", "lookup_steps", "exit_abandoned", "exit_closed",
+    COUNTERS = ("pieces", "wave_rows", "wait_polls", "drains", "reserved", "worker_exits", "idle_exits",
                 "poller_polls", "busy_ticks", "life_ticks")
 
     def counters(self):

@@ -207,8 +207,10 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
  *                       *seq receives the batch's sequence number.  At most
  *                       64 batches may be published and not yet done
  *                       (CUDASP_ERR_CAPACITY otherwise).  Launches the kernel
- *                       if none is running (a kernel whose waves find no work
- *                       for CUDASP_STREAM_IDLE_US, default 2000 us, ends).
+ *                       if none is running: a kernel that finds nothing to do
+ *                       for CUDASP_STREAM_IDLE_MS (default 20 ms) ends, so a
+ *                       stalled host never holds the GPU; publish and wait
+ *                       relaunch it.
  *   cudasp_stream_query  1: batch seq done (flags written), 0: not yet, < 0: error.
  *   cudasp_stream_wait   blocks until batch seq is done.
  *   cudasp_stream_finish  end of input: waits for every batch and for the
@@ -217,10 +219,11 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
  *   cudasp_stream_stats  kernel launches so far and grid blocks.
  *   cudasp_stream_counters  the kernel's counters of the last finished
  *                       query (taken by finish; reading them while the
- *                       kernel runs could wait for it): pieces, wave-rows, idle polls,
- *                       pipeline drains, claim retries, worker exits on the
- *                       idle timeout and on close, poller polls, workers'
- *                       busy and lifetime ticks (100 MHz). */
+ *                       kernel runs could wait for it), summed over its
+ *                       launches: pieces, wave-rows, polls with nothing to
+ *                       claim, pipeline drains, (unused), worker exits,
+ *                       idle exits, poller polls, workers' busy and lifetime
+ *                       ticks (100 MHz). */
 typedef struct cudasp_stream cudasp_stream;
 int cudasp_host_alloc(void** p, size_t bytes);
 void cudasp_host_free(void* p);

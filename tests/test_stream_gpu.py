@@ -3,8 +3,8 @@ kernel scans batches as they are published, reading them from coherent pinned
 host memory and writing their flags back there) gives the per-batch path's
 flags -- ragged batch sizes, 0 / 2 / 16 labels (the label compares read the
 device mirror of each row's outputs), 1..15 outputs per row, a ring that
-wraps, reuse after finish, a slow publisher, a host that never closes (the
-waves give up), exceptional label sums in one thread's piece, and the C
+wraps, reuse after finish, a slow publisher and an idle host (the kernel
+leaves and is relaunched), exceptional label sums in one thread's piece, and the C
 oracle."""
 import os
 import time
@@ -17,9 +17,9 @@ from test_multi_batch_gpu import torch  # noqa: F401  (fixture)
 
 pytestmark = pytest.mark.gpu
 
-# a stream that never completes a batch ends its kernel after this many
-# seconds (the test then fails instead of hanging)
-os.environ.setdefault("CUDASP_STREAM_ABANDON_S", "20")
+# a kernel with nothing to do leaves after this many milliseconds (the
+# default; the host's next publish or wait relaunches it)
+os.environ.setdefault("CUDASP_STREAM_IDLE_MS", "20")
 
 SCAN, SPEND, LABEL = tm.SCAN, tm.SPEND, tm.LABEL
 
@@ -117,9 +117,10 @@ def test_stream_ring_wraps(torch):
 
 
 def test_stream_slow_publisher(torch):
-    """Batches published 50 ms apart: the query's one kernel waits for each
-    (its waves hold tickets past the published rows) and the results are
-    the per-batch path's."""
+    """Batches published 50 ms apart, longer than the 20 ms idle time: the
+    kernel leaves after each batch (the GPU is not held while the host is
+    slow) and the next publish relaunches it; the results are the per-batch
+    path's."""
     from cudasp_amd import Scanner, ScanStream
     labels = [LABEL]
     batches = [tm.make_batch(torch, 5000 + 9000 * i, n) for i, n in enumerate([4000, 700, 8000])]
@@ -132,29 +133,38 @@ def test_stream_slow_publisher(torch):
             st.wait(q)
             time.sleep(0.05)
         st.finish()
-        c = st.counters()  # the finished query's
-        assert st.stats()["launches"] == 1
-    assert c["wait_polls"] > 0
+        c = st.counters()  # the finished query's, summed over its launches
+        launches = st.stats()["launches"]
+    assert launches == 3
+    assert c["idle_exits"] >= 2
+    assert c["wave_rows"] == sum((b["n"] + 63) // 64 for b in batches)
     flags_equal([sb.result() for sb in stage], want)
 
 
-def test_stream_abandoned_by_host(torch, monkeypatch):
-    """A host that neither publishes nor closes for CUDASP_STREAM_ABANDON_S:
-    the kernel's waves give up and leave (no wave spins forever), the next
-    publish reports it, and after finish the stream serves a new query."""
-    from cudasp_amd import CudaspError, Scanner, ScanStream
-    monkeypatch.setenv("CUDASP_STREAM_ABANDON_S", "1")
+def test_stream_idle_kernel_releases_gpu(torch):
+    """While a stream is open but the host publishes nothing, the kernel
+    leaves after the idle time, so other work on the GPU runs (a kernel that
+    held every wave slot until the stream closed would stall it); the next
+    publish relaunches it and a later query on the stream is unaffected."""
+    from cudasp_amd import Scanner, ScanStream
     b = tm.make_batch(torch, 99, 3000)
     tm.plant(torch, [b], [], every=50)
     want = tm.run_per_batch(torch, [b], [])
     sb = staged(b, 0)
     with Scanner(SCAN, SPEND, [], max_rows=1000) as s, ScanStream(s) as st:
         st.wait(sb.publish(st))
-        time.sleep(2.5)
-        with pytest.raises(CudaspError):
-            st.wait(sb.publish(st))
-        with pytest.raises(CudaspError):
-            st.finish()
+        time.sleep(0.1)
+        x = torch.ones(1 << 20, device="cuda")
+        t = time.perf_counter()
+        y = (x * 3).sum()
+        torch.cuda.synchronize()
+        assert float(y) == 3 * (1 << 20)
+        assert time.perf_counter() - t < 5
+        sb.flags.array[:] = 0xEE
+        st.wait(sb.publish(st))
+        st.finish()
+        assert st.stats()["launches"] == 2
+        flags_equal([sb.result()], want)
         sb.flags.array[:] = 0xEE
         st.wait(sb.publish(st))
         st.finish()

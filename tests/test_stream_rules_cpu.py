@@ -114,3 +114,64 @@ def test_walk_from_hint_alone_misses_after_wraps():
         b += 1
     assert b != 140
     assert batch_of(ring, 150, 0, w) == (140, 140 - (150 - STREAM_RING))
+
+
+def test_idle_exit_and_relaunch_process_every_row_once():
+    """The elastic protocol replayed with random interleavings: waves claim
+    with a single fetch-and-add while published rows are unclaimed (so
+    concurrent claims pass pub_wr), process only the published part of a
+    ticket, and drop the rest when the poller declares the kernel idle; the
+    relaunch resets the claim counter to the mirrored pub_wr.  Over many
+    publish / stall / relaunch cycles every published wave-row is processed
+    exactly once and nothing past the published rows ever is."""
+    rng = random.Random(11)
+    for trial in range(40):
+        nwaves = rng.randint(1, 12)
+        processed = {}
+        pub_wr = 0        # the kernel's mirror (final while idle)
+        host_wr = 0       # rows the host has published
+        ticket = 0
+        launches = 0
+        for cycle in range(rng.randint(1, 8)):
+            host_wr += rng.randint(1, 60)
+            # relaunch: k_stream_relaunch resets the claim counter
+            ticket = pub_wr
+            launches += 1
+            waves = [None] * nwaves      # (tk, tr) tickets
+            mine = [0] * nwaves
+            idle = False
+            steps = 0
+            while True:
+                steps += 1
+                # the poller mirrors what the host published (sometimes late)
+                if not idle and rng.random() < 0.3:
+                    pub_wr = host_wr
+                active = False
+                for w in rng.sample(range(nwaves), nwaves):
+                    if waves[w] is None and not idle and pub_wr > ticket:
+                        tr = max(1, min(rng.randint(1, 6), pub_wr - ticket))
+                        # fetch-and-add: other waves may have read the same `ticket`
+                        waves[w] = (ticket, tr + rng.choice([0, 0, 0, 3]))
+                        ticket += waves[w][1]
+                        mine[w] += waves[w][1]
+                    if waves[w] is not None:
+                        tk, tr = waves[w]
+                        if tk < pub_wr:
+                            cnt = min(tr, pub_wr - tk)
+                            for r in range(tk, tk + cnt):
+                                processed[r] = processed.get(r, 0) + 1
+                            waves[w] = (tk + cnt, tr - cnt) if tr > cnt else None
+                            active = True
+                        elif idle:
+                            waves[w] = None  # unpublished rest dropped
+                # the poller: idle once everything published is claimed and mirrored
+                if not idle and ticket >= pub_wr and pub_wr == host_wr and rng.random() < 0.5:
+                    idle = True
+                if idle and all(x is None for x in waves):
+                    break
+                assert steps < 10000
+            assert all(r < pub_wr for r in processed)
+        # each cycle ends idle only with everything published mirrored and
+        # claimed, and the claimed published parts processed
+        assert all(processed.get(r) == 1 for r in range(host_wr)), trial
+        assert launches >= 1
