@@ -3,7 +3,7 @@
 # bench lines at the configs' shapes and the 2-rank rehearsal.
 #   $1: "notests" skips pytest + smoke
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r03c_measure; mkdir -p $O; cd $R
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${MEASURE_TAG:-r03d}_measure; mkdir -p $O; cd $R
 if [ "$1" != "notests" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { grep -E "PASS|FAIL|Error|error" $O/gpu_tests.log | tail -30; tail -60 $O/gpu_tests.log; exit 1; }
   tail -1 $O/gpu_tests.log
