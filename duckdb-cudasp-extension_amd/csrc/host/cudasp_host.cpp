@@ -412,6 +412,7 @@ struct cudasp_tf_global {
   // device feeds, one per logical GPU, created on its first chunk
   const cudasp_tf_bind_data* bind = nullptr;
   int feed_streams = 0;
+  int launch_streams = 0;  // streams of a per-slot-launch feed (a streaming feed that falls back)
   // feeds[lg] is written once, under feed_create_mu[lg]; threads look a feed
   // up through feed_ptr[lg] (published after the feed is complete)
   std::vector<std::unique_ptr<Feed>> feeds;
@@ -799,7 +800,7 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
           r->stream_blocks = blocks;
         } else if (rc == CUDASP_ERR_INVALID_ARG) {  // a width the streaming kernel lacks: per-slot launches
           r->stream = nullptr;
-          r->nstreams = g.feed_streams;
+          r->nstreams = g.launch_streams;
           rc = CUDASP_OK;
         }
       }
@@ -1274,6 +1275,7 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
     feeds_per_device = std::max(feeds_per_device, m);
   }
   g->feed_streams = feed_streams_for(b->batch_size, g->hw_queues, feeds_per_device);
+  g->launch_streams = g->feed_streams;
   {
     const char* mode = getenv("CUDASP_TF_MODE");
     // one feed per device: a persistent kernel holds its hardware queue for
