@@ -213,3 +213,36 @@ def test_host_streaming_feed_16_labels(table16, keys, threads, batch, monkeypatc
     assert stats["streaming_feeds"] == 0
     assert _heights(out) == expected
     release_pool()
+
+
+def test_host_concurrent_queries_one_gpu(table16, keys):  # noqa: F811
+    """Two queries at once on one GPU, each with its own executor threads
+    (two DuckDB connections in one process): each query's streaming feed
+    runs its own kernel, and a kernel holds the GPU only while its query has
+    work (it leaves after CUDASP_STREAM_IDLE_MS idle) -- both queries finish
+    with the oracle's rows, with different batch sizes and label sets."""
+    import threading
+    from cudasp_amd import cudasp_scan, release_pool
+    rows, expected = table16
+    scan, spend, labels = keys
+    out, errs = {}, []
+
+    def run(name, batch, threads):
+        try:
+            st = {}
+            out[name] = (cudasp_scan(rows, scan, spend, labels, batch_size=batch, threads=threads, stats=st), st)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append((name, repr(e)))
+
+    ts = [threading.Thread(target=run, args=("a", 2500, 3)), threading.Thread(target=run, args=("b", 4000, 4))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "a concurrent query did not finish"
+    assert not errs, errs
+    for name in ("a", "b"):
+        got, st = out[name]
+        assert _heights(got) == expected, name
+        assert st["streaming_feeds"] == 1
+    release_pool()
