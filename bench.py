@@ -32,7 +32,10 @@ timed steps, rank 0 also reports the PCIe-inclusive end-to-end rate of the
 table-function host over all N GPUs (`e2e`: tools/host_e2e as a child
 process, the same table shape in host memory, fed by executor threads through
 the calls DuckDB makes; at N > 1 the other ranks wait at a CPU barrier) --
-never the `value`.
+never the `value`.  `e2e` runs the host's default streaming feeds (one
+persistent kernel per GPU reading the batch slots in place from pinned host
+memory); `e2e_launch` the same child with per-slot
+copies and launches (CUDASP_TF_MODE=launch).
 
 Synthetic data: T_i = (s0 + g) G with s0 = SHA256("cudasp-synth-v1")
 mod n and g the global row index; 2 splitmix64 outputs per row (seed
