@@ -1013,6 +1013,13 @@ def main():
                     streams=1 if multi else args.streams, batches_rank0=tab.nb, parallelism="dp%d" % world),
         roofline=dict(bound="hbm", achieved=achieved_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                       frac=achieved_gbs / HBM_PEAK_GBS, traffic=traffic,
+                      traffic_ratio=(traffic / algo_bytes) if traffic else None,
+                      traffic_counts=("2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 --pmc derived counters, the "
+                                      "MI355X_MICROARCH.md gfx950 correction) per launch: L2-to-fabric traffic, so "
+                                      "MALL (Infinity Cache) hits are included -- an upper bound on HBM bytes; the "
+                                      "excess over the algorithmic bytes is the per-thread scratch (odd-multiple "
+                                      "tables, pending rows) leaving L2, DESIGN.md section 5"
+                                      if traffic else None),
                       kernel=kernel, kernel_ms=kernel_ms, kernel_ms_how=kernel_ms_how,
                       algorithmic_bytes_per_launch=algo_bytes, rows_per_launch=rows_per_launch,
                       launches_per_step_rank0=launches,

@@ -91,6 +91,12 @@ double now_s() {
 
 extern "C" void cudasp_internal_set_error(const char* msg);
 extern "C" void* cudasp_internal_scanner_stream(cudasp_scanner* s);
+#if CUDASP_STREAM_TRACE
+extern "C" void cudasp_internal_trace_host(uint32_t kind, uint64_t a, uint32_t b);
+#define ST_HOST(...) cudasp_internal_trace_host(__VA_ARGS__)
+#else
+#define ST_HOST(...) ((void)0)
+#endif
 
 struct cudasp_tf_bind_data {
   uint64_t batch_size = CUDASP_TF_DEFAULT_BATCH;
@@ -168,6 +174,8 @@ struct FeedSlot {
   uint8_t* h_flags = nullptr;
   int64_t* h_outputs = nullptr;  // outputs_cap int64 words
   size_t outputs_cap = 0;
+  uint32_t* h_matches = nullptr;  // streaming feed: the kernel's matching row indices (cap_rows)
+  bool coherent = false;          // host buffers from cudasp_host_alloc (streaming feed)
   // emit data of the rows (pageable; only read for matches)
   std::vector<uint8_t> txid_bytes;  // size() is the capacity
   std::vector<uint64_t> txid_off;   // cap_rows
@@ -214,16 +222,21 @@ struct FeedRes {
 };
 
 void free_stale(FeedRes& r) {
-  for (void* p : r.stale_host) (void)hipHostFree(p);
+  for (void* p : r.stale_host) cudasp_host_free(p);
   for (void* p : r.stale_dev) (void)hipFree(p);
   r.stale_host.clear();
   r.stale_dev.clear();
 }
 
 void free_slot(FeedSlot& s) {
-  void* host[] = {s.h_tweaks, s.h_offs, s.h_lens, s.h_flags, s.h_outputs};
+  void* host[] = {s.h_tweaks, s.h_offs, s.h_lens, s.h_flags, s.h_outputs, s.h_matches};
   for (void* p : host)
-    if (p) (void)hipHostFree(p);
+    if (p) {
+      if (s.coherent)
+        cudasp_host_free(p);
+      else
+        (void)hipHostFree(p);
+    }
   void* dev[] = {s.d_rows, s.d_tx, s.d_ty, s.d_offs, s.d_lens, s.d_flags, s.d_outputs};
   for (void* p : dev)
     if (p) (void)hipFree(p);
@@ -235,7 +248,14 @@ void free_slot(FeedSlot& s) {
 void release_res(FeedRes* r) {
   if (!r) return;
   if (r->stream) {
-    cudasp_stream_destroy(r->stream);  // closes it and waits for its kernel
+    (void)cudasp_stream_finish(r->stream);  // closes it and waits for its kernel (bounded)
+    if (cudasp_stream_abandoned(r->stream)) {
+      // its kernel may still read the slots and use the scanner: leak them all
+      fprintf(stderr, "cudasp_scan: device %d feed leaked (its streaming kernel did not end)\n", r->device);
+      cudasp_stream_destroy(r->stream);
+      return;
+    }
+    cudasp_stream_destroy(r->stream);
     r->stream = nullptr;
   }
   {
@@ -344,10 +364,11 @@ int prepare_slot_streaming(FeedRes& r, FeedSlot& s, size_t words, size_t txid) {
     return rc == CUDASP_OK ? rc : host_fail(rc, "pinned slot allocation failed: %s", cudasp_last_error());
   };
   if (!s.allocated) {
+    s.coherent = true;
     int rc = host((void**)&s.h_tweaks, n * 64);
     if (rc == CUDASP_OK) rc = host((void**)&s.h_offs, n * 4);
     if (rc == CUDASP_OK) rc = host((void**)&s.h_lens, n * 4);
-    if (rc == CUDASP_OK) rc = host((void**)&s.h_flags, n);
+    if (rc == CUDASP_OK) rc = host((void**)&s.h_matches, n * 4);
     if (rc != CUDASP_OK) return rc;
     s.txid_off.resize(n);
     s.txid_size.resize(n);
@@ -363,6 +384,19 @@ int prepare_slot_streaming(FeedRes& r, FeedSlot& s, size_t words, size_t txid) {
     const int rc = host((void**)&s.h_outputs, cap * sizeof(int64_t));
     if (rc != CUDASP_OK) return rc;
     s.outputs_cap = cap;
+  }
+  // the device mirror of the outputs, which the kernel's compares read (at
+  // least one word: a batch whose rows have no outputs still needs one)
+  if (!s.d_outputs || s.d_outputs_cap < s.outputs_cap) {
+    if (s.d_outputs) r.stale_dev.push_back(s.d_outputs);
+    s.d_outputs = nullptr;
+    s.d_outputs_cap = 0;
+    const size_t cap = std::max<size_t>(s.outputs_cap, 1);
+    if (hipMalloc((void**)&s.d_outputs, cap * sizeof(int64_t)) != hipSuccess) {
+      (void)hipGetLastError();
+      return host_fail(CUDASP_ERR_HIP, "outputs mirror of %zu words on device %d: allocation failed", cap, r.device);
+    }
+    s.d_outputs_cap = cap;
   }
   if (txid > s.txid_bytes.size()) s.txid_bytes.resize(txid);
   return CUDASP_OK;
@@ -384,7 +418,7 @@ struct Feed {
   // txid space before batch_size rows: long output lists, long txids)
   double words_per_row = 2.0;
   double txid_per_row = 32.0;
-  bool ramp = true;      // close_at; CUDASP_TF_RAMP=0 turns it off
+  int ramp = 3;          // ramp slots (close_at); CUDASP_TF_RAMP=N sets them, 0 turns the ramp off
   bool upload_null = true;  // H2D on the null stream; CUDASP_TF_UPLOAD=stream: on the scan stream (A/B)
   uint32_t closed = 0;   // slots closed so far
   int error = CUDASP_OK;
@@ -425,6 +459,7 @@ struct cudasp_tf_global {
   // faster end to end); CUDASP_TF_MODE=launch selects the
   // per-slot launches.
   bool streaming = false;
+  std::atomic<bool> streaming_fallback{false};  // this query's keys/options rule the streaming scan out (feed_for)
 };
 
 struct cudasp_tf_local {
@@ -461,25 +496,24 @@ int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   int rc = CUDASP_OK;
   if (r.stream) {
     // Streaming feed: publish the slot to the feed's kernel, which reads it
-    // in place (no copies, no launch).  With labels the kernel copies each
-    // row's outputs to the slot's device mirror, grown here (the old one is
-    // freed after the kernel ends).
+    // in place (no copies, no launch), copies each row's outputs to the
+    // slot's device mirror (sized with the slot, prepare_slot_streaming) and
+    // writes the matching rows' indices back into the slot.
     DeviceSet dg(r.device);
-    if (f.g->bind->label_keys_data.size() && words > s.d_outputs_cap) {
-      if (s.d_outputs) r.stale_dev.push_back(s.d_outputs);
-      s.d_outputs = nullptr;
-      s.d_outputs_cap = 0;
-      if (hipMalloc((void**)&s.d_outputs, s.outputs_cap * sizeof(int64_t)) != hipSuccess) {
-        (void)hipGetLastError();
-        rc = host_fail(CUDASP_ERR_HIP, "outputs mirror of %zu words on device %d: allocation failed", s.outputs_cap,
-                       r.device);
-      } else {
-        s.d_outputs_cap = s.outputs_cap;
-      }
-    }
-    if (rc == CUDASP_OK) {
-      rc = cudasp_stream_publish(r.stream, s.h_tweaks, s.h_outputs, s.h_offs, s.h_lens, n, s.h_flags, s.d_outputs,
-                                 &s.seq);
+    if (words > s.d_outputs_cap) {
+      rc = host_fail(CUDASP_ERR_INVALID_ARG, "batch of %zu output words exceeds its mirror (%zu)", words,
+                     s.d_outputs_cap);
+    } else {
+      cudasp_stream_batch b{};
+      b.tweak_keys = s.h_tweaks;
+      b.outputs = s.h_outputs;
+      b.output_offsets = s.h_offs;
+      b.output_lengths = s.h_lens;
+      b.n = n;
+      b.match_flags = nullptr;
+      b.match_rows = s.h_matches;
+      b.d_mirror = s.d_outputs;
+      rc = cudasp_stream_publish_batch(r.stream, &b, &s.seq);
       if (rc != CUDASP_OK)
         rc = host_fail(rc, "cudasp_scan batch of %u rows on device %d failed: %s", n, r.device, cudasp_last_error());
     }
@@ -561,14 +595,39 @@ int harvest_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
     }
   }
   const double waited = now_s() - t0;
+  ST_HOST(112, (uint64_t)(waited * 1e9), (uint32_t)s.seq);
   if (e == hipSuccess) {
     cudasp_tf_global& g = *f.g;
-    std::lock_guard<std::mutex> lock(g.output_lock);
-    for (uint32_t i = 0; i < s.rows; i++) {
-      if (!s.h_flags[i]) continue;
+    const auto emit = [&](uint32_t i) {
       g.output_txids.emplace_back((const char*)s.txid_bytes.data() + s.txid_off[i], s.txid_size[i]);
       g.output_heights.push_back(s.heights[i]);
       g.output_tweak_keys.emplace_back((const char*)s.h_tweaks + (size_t)i * TWEAK_KEY_SIZE, TWEAK_KEY_SIZE);
+    };
+    if (f.res->stream) {
+      // the kernel's compacted matches (in no particular order: sorted, so a
+      // batch emits in row order like the flags scan)
+      uint32_t nm = 0;
+      if (cudasp_stream_matches(f.res->stream, s.seq, &nm) != CUDASP_OK || nm > s.rows) {
+        e = hipErrorUnknown;
+        stream_err = cudasp_last_error();
+      } else {
+        std::sort(s.h_matches, s.h_matches + nm);
+        std::lock_guard<std::mutex> lock(g.output_lock);
+        for (uint32_t k = 0; k < nm; k++) emit(s.h_matches[k]);
+      }
+    } else {
+      std::lock_guard<std::mutex> lock(g.output_lock);
+      // eight flags at a time: matches are rare
+      uint32_t i = 0;
+      for (; i + 8 <= s.rows; i += 8) {
+        uint64_t w;
+        memcpy(&w, s.h_flags + i, 8);
+        if (!w) continue;
+        for (uint32_t k = i; k < i + 8; k++)
+          if (s.h_flags[k]) emit(k);
+      }
+      for (; i < s.rows; i++)
+        if (s.h_flags[i]) emit(i);
     }
   }
   lk.lock();
@@ -593,14 +652,41 @@ int close_open_locked(Feed& f, std::unique_lock<std::mutex>& lk) {
 }
 
 // Rows at which the open slot closes: batch_size, except that a feed's first
-// three slots close at batch_size / 8, / 4 and / 2 (the ramp), so the GPU
-// starts before a whole batch has been read: +6% end to end at 1M rows, +2%
-// at 9.4M, within the spread at 32.7M (profiles/r03_e2e_ramp_ab.txt).
-// CUDASP_TF_RAMP=0 turns it off.
+// `ramp` slots close at batch_size / 2^ramp, ..., / 4, / 2, so the GPU starts
+// before a whole batch has been read.  Per-slot launches: 3 (/ 8, / 4, / 2:
+// +6% end to end at 1M rows, +2% at 9.4M, within the spread at 32.7M,
+// profiles/r03_e2e_ramp_ab.txt).  A streaming feed starts its kernel on the
+// first slot and takes 5 (from / 32: ~9k rows, read in well under 0.1 ms).
+// CUDASP_TF_RAMP=N sets N, 0 turns the ramp off.
 uint64_t close_at(const Feed& f) {
-  if (!f.ramp || f.closed >= 3) return f.batch_size;
-  const uint64_t r = f.batch_size >> (3 - f.closed);
+  if (f.closed >= (uint32_t)f.ramp) return f.batch_size;
+  const uint64_t r = f.batch_size >> (f.ramp - (int)f.closed);
   return r < CUDASP_TF_VECTOR_SIZE ? std::min<uint64_t>(f.batch_size, CUDASP_TF_VECTOR_SIZE) : r;
+}
+
+// Whether a launched slot's batch is done (no waiting).
+bool slot_done(Feed& f, FeedSlot& s) {
+  if (f.res->stream) return cudasp_stream_query(f.res->stream, s.seq) == 1;
+  DeviceSet dg(f.res->device);
+  return hipEventQuery(s.done) == hipSuccess;
+}
+
+// Another slot to open instead of the open one, whose batch is still in
+// flight: the next slot in ring order that is free or whose batch is done
+// (-1: none).  Slots are taken out of order, so a batch held up by a slow
+// wave-row occupies its slot alone instead of stalling the whole ring (a
+// streaming kernel's youngest waves get few issue slots: one batch of the
+// 9.4M-row table finished 27 ms after it was published).  A done slot is
+// reached within one pass of the ring, long before its match count could be
+// overwritten (STREAM_RING = 64 batches later).
+int ready_slot_locked(Feed& f) {
+  const int n = f.res->nslots();
+  for (int i = 1; i < n; i++) {
+    const int k = (f.open + i) % n;
+    FeedSlot& t = f.res->slots[k];
+    if (t.state == SLOT_FREE || (t.state == SLOT_LAUNCHED && slot_done(f, t))) return k;
+  }
+  return -1;
 }
 
 struct Reservation {
@@ -691,6 +777,24 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
         continue;
       }
       case SLOT_LAUNCHED: {
+        // the open slot's batch may still be in flight: take a ready slot
+        // if there is one; else poll for one for a while (any batch that
+        // completes frees a slot), then wait for this one
+        if (!slot_done(f, s)) {
+          const int open0 = f.open;
+          int k = ready_slot_locked(f);
+          for (int spin = 0; k < 0 && spin < 100; spin++) {
+            f.cv.wait_for(lk, std::chrono::microseconds(20));
+            if (f.error != CUDASP_OK) return feed_error(f);
+            if (f.open != open0 || s.state != SLOT_LAUNCHED || slot_done(f, s)) break;
+            k = ready_slot_locked(f);
+          }
+          if (f.open != open0 || s.state != SLOT_LAUNCHED) continue;  // another thread moved on
+          if (k >= 0) {
+            f.open = k;
+            continue;
+          }
+        }
         const int rc = harvest_locked(f, s, lk);
         if (rc != CUDASP_OK) return rc;
         continue;
@@ -715,6 +819,7 @@ int feed_commit(Feed& f, FeedSlot& s, double reserve_s, double copy_s) {
 // first, so the devices drain in parallel), then harvest everything.
 int feeds_flush(cudasp_tf_global& g) {
   int rc = CUDASP_OK;
+  ST_HOST(111, 0, 0);
   for (auto& fp : g.feeds) {
     if (!fp) continue;
     Feed& f = *fp;
@@ -727,6 +832,13 @@ int feeds_flush(cudasp_tf_global& g) {
       } else {
         s.state = SLOT_FREE;
       }
+    }
+    // a streaming feed's last batch is published: its kernel may end as
+    // soon as the batches are done (finish below only waits and resets)
+    if (f.res->stream) {
+      lk.unlock();
+      DeviceSet dg(f.res->device);
+      (void)cudasp_stream_close(f.res->stream);
     }
   }
   for (auto& fp : g.feeds) {
@@ -743,6 +855,7 @@ int feeds_flush(cudasp_tf_global& g) {
     }
     if (rc == CUDASP_OK && f.error != CUDASP_OK) rc = feed_error(f);
   }
+  ST_HOST(113, 0, 0);
   // streaming feeds: every batch is done; close the streams so their kernels
   // end (and the streams are ready for the next query)
   for (auto& fp : g.feeds) {
@@ -753,6 +866,17 @@ int feeds_flush(cudasp_tf_global& g) {
     free_stale(*fp->res);
   }
   return rc;
+}
+
+// The streaming feeds' wait timeout (cudasp_stream_set_timeout): a wait
+// that sees no batch complete for this long fails the query instead of
+// hanging it.  CUDASP_STREAM_TIMEOUT_MS, read per query; 60 s by default.
+uint32_t stream_timeout_ms() {
+  if (const char* e = getenv("CUDASP_STREAM_TIMEOUT_MS")) {
+    const long v = atol(e);
+    if (v >= 1 && v <= 86400000) return (uint32_t)v;
+  }
+  return 60000u;
 }
 
 // The feed of logical GPU `lg`, created on first use: pooled resources for
@@ -785,16 +909,39 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
         return host_fail(rc, "Failed to bind scanner on GPU %d: %s", lg, cudasp_last_error());
       }
     }
-  } else {
+    // a pooled streaming feed rebound to keys or options the streaming scan
+    // cannot run (too many label keys): back to the pool, and this query
+    // takes per-slot launches like a new feed would (cudasp_stream_create's
+    // CUDASP_ERR_INVALID_ARG below)
+    if (r->stream && !cudasp_stream_supported(r->scanners[0])) {
+      pool_put(r);
+      r = nullptr;
+      g.streaming_fallback = true;
+    }
+  }
+  if (!r && g.streaming_fallback) {
+    r = pool_take(device, cap_rows, g.launch_streams, 0);
+    if (r) {
+      for (int k = 0; k < r->nstreams; k++) {
+        int rc = cudasp_scanner_set_keys(r->scanners[k], scan, spend, labels, nlabels);
+        if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(r->scanners[k], &b.opt);
+        if (rc != CUDASP_OK) {
+          pool_put(r);
+          return host_fail(rc, "Failed to bind scanner on GPU %d: %s", lg, cudasp_last_error());
+        }
+      }
+    }
+  }
+  if (!r) {
     r = new FeedRes();
     r->device = device;
     r->cap_rows = cap_rows;
-    r->nstreams = g.streaming ? 1 : g.feed_streams;
+    r->nstreams = g.streaming && !g.streaming_fallback ? 1 : g.launch_streams;
     for (int k = 0; k < FEED_MAX_STREAMS; k++) {
       if (k >= r->nstreams) break;
       int rc = cudasp_scanner_create(device, scan, spend, labels, nlabels, cap_rows, &r->scanners[k]);
       if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(r->scanners[k], &b.opt);
-      if (rc == CUDASP_OK && k == 0 && g.streaming) {
+      if (rc == CUDASP_OK && k == 0 && g.streaming && !g.streaming_fallback) {
         rc = cudasp_stream_create(r->scanners[0], blocks, &r->stream);
         if (rc == CUDASP_OK) {
           r->stream_blocks = blocks;
@@ -811,13 +958,15 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
       }
     }
   }
+  if (r->stream) (void)cudasp_stream_set_timeout(r->stream, stream_timeout_ms());
   auto f = std::make_unique<Feed>();
   f->res = r;
   f->g = &g;
   f->batch_size = b.batch_size;
   f->ow = out_words(b);
   f->words_per_row = 2.0 * f->ow;
-  if (const char* e = getenv("CUDASP_TF_RAMP")) f->ramp = atoi(e) != 0;
+  f->ramp = r->stream ? 5 : 3;
+  if (const char* e = getenv("CUDASP_TF_RAMP")) f->ramp = std::max(0, std::min(atoi(e), 10));
   if (const char* e = getenv("CUDASP_TF_UPLOAD")) f->upload_null = strcmp(e, "stream") != 0;
   *out = f.get();
   g.feeds[lg] = std::move(f);
@@ -1112,19 +1261,26 @@ void feeds_release(cudasp_tf_global& g) {
         s.writers = 0;
       }
     }
-    bool ok = f.error == CUDASP_OK;
+    // The resources go back to the pool when the device is done with them
+    // cleanly, whether or not the query failed (a bad row, a wait that hit
+    // its timeout); anything else releases them.
+    bool ok = true;
     {
       DeviceSet dg(r->device);
       // a streaming feed's kernel runs until its stream is closed: close it
-      // (an aborted query's published batches finish first)
+      // (an aborted query's published batches finish first), allowing the
+      // drain at least the default timeout even when the query's own waits
+      // had a shorter one -- a slow kernel ends and the feed is pooled; one
+      // that never ends is abandoned and leaked (release_res)
       if (r->stream) {
-        ok = cudasp_stream_finish(r->stream) == CUDASP_OK && ok;
+        (void)cudasp_stream_set_timeout(r->stream, std::max<uint32_t>(stream_timeout_ms(), 60000u));
+        ok = cudasp_stream_finish(r->stream) == CUDASP_OK;
         free_stale(*r);
       }
       for (int k = 0; k < r->nstreams; k++) ok = cudasp_scanner_sync(r->scanners[k]) == CUDASP_OK && ok;
       // a launch that failed after queueing its uploads left them on the
       // null stream, still reading the slot's pinned buffers
-      if (!ok) (void)hipStreamSynchronize((hipStream_t)0);
+      if (!ok || f.error != CUDASP_OK) (void)hipStreamSynchronize((hipStream_t)0);
     }
     fp.reset();
     if (ok)
@@ -1240,6 +1396,7 @@ uint64_t cudasp_tf_bind_batch_size(const cudasp_tf_bind_data* b) { return b ? b-
 int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
   if (!b || !out) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
   auto* g = new cudasp_tf_global();
+  ST_HOST(110, 0, 0);
   // Reference: cudaGetDeviceCount, falling back to 1 (:129-132).
   g->num_gpus = cudasp_device_count();
   if (g->num_gpus <= 0) g->num_gpus = 1;
@@ -1283,7 +1440,8 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
     // queue (HIP shares queues among streams) and the second would wait for
     // the first to end -- logical GPUs sharing a device (CUDASP_TF_DEVICE_MAP)
     // take the per-slot launches
-    g->streaming = !(mode && !strcmp(mode, "launch")) && b->opt.output_count == 1 && feeds_per_device == 1;
+    g->streaming = !(mode && !strcmp(mode, "launch")) && b->opt.output_count <= CUDASP_STREAM_MAX_OUTPUT_COUNT &&
+                   feeds_per_device == 1;
     if (g->streaming) g->feed_streams = 1;
   }
   g->feeds.resize(g->num_gpus);
@@ -1420,6 +1578,7 @@ int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf
   if (!b || !g || !l || !out) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
   out->count = 0;
   if (!l->finalized) {
+    ST_HOST(114, 0, 0);
     // A thread's rows are already in the device feeds.  The last thread to
     // finish launches every feed's partial slot, waits for all of them and
     // becomes the output thread (:554-624: the last thread emits).

@@ -650,6 +650,58 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
 }
 
+// Measurement builds only (-DCUDASP_STREAM_TRACE=1, tools/stream_trace.py):
+// timestamped events of k_scan_stream (wave starts with their hardware
+// placement, claims, pieces, iteration ends, exits, batches mirrored and
+// completed), appended by cudasp_stream_finish to $CUDASP_STREAM_TRACE_FILE.
+#ifndef CUDASP_STREAM_TRACE
+#define CUDASP_STREAM_TRACE 0
+#endif
+#if CUDASP_STREAM_TRACE
+struct StreamTraceEv {
+  uint64_t t, a;
+  uint32_t wave, kind, b, c;
+};
+enum { ST_START = 1, ST_CLAIM, ST_PIECE, ST_ITER_END, ST_EXIT, ST_PUB, ST_DONE };
+constexpr uint32_t STREAM_TRACE_CAP = 1u << 21;
+__device__ uint32_t g_st_n;
+__device__ StreamTraceEv g_st_ev[STREAM_TRACE_CAP];
+__device__ __forceinline__ void st_ev(uint32_t kind, uint32_t wave, uint64_t a, uint32_t b, uint32_t c) {
+  const uint32_t i = atomicAdd(&g_st_n, 1u);
+  if (i < STREAM_TRACE_CAP) {
+    StreamTraceEv e;
+    e.t = wall_clock64();
+    e.a = a;
+    e.wave = wave;
+    e.kind = kind;
+    e.b = b;
+    e.c = c;
+    g_st_ev[i] = e;
+  }
+}
+#define ST_EV(...) st_ev(__VA_ARGS__)
+// host-side events of the same query (wave = ~0u, t = steady_clock ns)
+static std::mutex g_st_host_mu;
+static std::vector<StreamTraceEv> g_st_host;
+extern "C" void cudasp_internal_trace_host(uint32_t kind, uint64_t a, uint32_t b) {
+  StreamTraceEv e;
+  e.t = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+            std::chrono::steady_clock::now().time_since_epoch())
+            .count();
+  e.a = a;
+  e.wave = ~0u;
+  e.kind = kind;
+  e.b = b;
+  e.c = 0;
+  std::lock_guard<std::mutex> lk(g_st_host_mu);
+  g_st_host.push_back(e);
+}
+#define ST_HOST(...) cudasp_internal_trace_host(__VA_ARGS__)
+#else
+#define ST_EV(...) ((void)0)
+#define ST_HOST(...) ((void)0)
+#endif
+
 // A wave-row's batch, wave-uniform.
 struct StreamRow {
   const uint8_t* rows;
@@ -657,6 +709,7 @@ struct StreamRow {
   const uint32_t* offs;
   const uint32_t* lens;
   uint8_t* flags;
+  uint32_t* matches;
   int64_t* mirror;
   uint64_t first_wr;
   uint32_t n;
@@ -710,20 +763,13 @@ __device__ __forceinline__ StreamRow stream_row(StreamDev* dev, uint32_t& hint, 
   r.offs = ptr(&d->offs);
   r.lens = ptr(&d->lens);
   r.flags = ptr(&d->flags);
+  r.matches = ptr(&d->matches);
   r.mirror = ptr(&d->mirror);
   r.first_wr = uniform_u64(dev_load_u64(&d->first_wr));
   r.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)dev_load_u32(&d->n));
   r.nwr = (uint32_t)__builtin_amdgcn_readfirstlane((int)dev_load_u32(&d->nwr));
   r.b = b;
   return r;
-}
-
-// Row of this lane in wave-row w (false: the padding of the batch's last
-// wave-row, which then reads batch row 0).
-__device__ __forceinline__ uint32_t stream_lane_row(const StreamRow& sr, uint64_t w, uint32_t lane, bool* active) {
-  const uint32_t r = (uint32_t)(w - sr.first_wr) * 64u + lane;
-  *active = r < sr.n;
-  return *active ? r : 0u;
 }
 
 // The poller (lane 0 of one wave per kernel): mirrors new batches of the
@@ -770,6 +816,7 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_tick
       }
       __hip_atomic_store(&dev->pub_wr, pub_wr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&dev->pub, pub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      ST_EV(ST_PUB, 0u, pub_wr, pub, seen);
       seen = pub;
       last = now;
     }
@@ -790,46 +837,235 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_tick
   atomicAdd(&dev->stat[STREAM_STAT_POLLER_POLLS], (unsigned long long)polls);
 }
 
-// Flags of wave-rows base .. base + count - 1 into their pinned slots, then
-// each batch's completion: the wave's stores are complete before its
-// wave-rows count, and the wave whose count finishes a batch writes the
-// batch's done word.
-__device__ __forceinline__ void stream_emit(StreamCtrl* ctrl, StreamDev* dev, uint64_t base, int count,
-                                            uint32_t hint, uint32_t lane, uint32_t hits) {
+// Raw scratch words (column-major like scr_load / scr_store).
+__device__ __forceinline__ void scr_store_w(const Scratch& sc, int w, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_buffer_store_b32(v, sc.rsrc, sc.slot * 4u, (uint32_t)w * sc.stride * 4u, CUDASP_SCR_STORE_CPOL);
+#else
+  sc.s[(size_t)w * sc.stride + sc.slot] = v;
+#endif
+}
+__device__ __forceinline__ uint32_t scr_load_w(const Scratch& sc, int w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_raw_buffer_load_b32(sc.rsrc, sc.slot * 4u, (uint32_t)w * sc.stride * 4u,
+                                              CUDASP_SCR_LOAD_CPOL);
+#else
+  return sc.s[(size_t)w * sc.stride + sc.slot];
+#endif
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// Scratch of a k_scan_stream thread (u32 words from the slot's base):
+// k_scan_multi's pipelined layout, then the new piece's row blobs (16 words
+// per wave-row), the offsets and lengths of the three pieces in flight (new,
+// P, Q: 2 words per wave-row each) and, with output_count > 1, the new
+// piece's affine shared-secret x and y parity (9 words per row).
+constexpr int STREAM_STG_WORDS = 16 * MULTI_RMAX;
+constexpr int STREAM_META_WORDS = 3 * 2 * MULTI_RMAX;
+constexpr int STREAM_SXA_WORDS = 9 * MULTI_RMAX;
+constexpr uint32_t stream_scratch_words(uint32_t label_count) {
+  return multi_scratch_words(label_count, true) + STREAM_STG_WORDS + STREAM_META_WORDS + STREAM_SXA_WORDS;
+}
+
+// Host pointers of a piece's wave-rows, kept in LDS during its prefetch.
+struct StreamPf {
+  const uint8_t* rows;
+  const int64_t* outputs;
+  const uint32_t* offs;
+  const uint32_t* lens;
+};
+
+// Outputs words [q0, q1) of one batch into its device mirror, the whole wave
+// copying (lane-strided, 4 loads in flight per lane).
+__device__ __forceinline__ void stream_copy_range(int64_t* mirror, const int64_t* outputs, uint32_t q0, uint32_t q1,
+                                                  uint32_t lane) {
+#pragma unroll 1
+  for (uint32_t q = q0 + lane; q < q1; q += 4 * 64) {
+    int64_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (q + 64u * i < q1) v[i] = outputs[q + 64u * i];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (q + 64u * i < q1) mirror[q + 64u * i] = v[i];
+  }
+}
+
+// Prefetch of a new piece (count wave-rows from `base`): each wave-row's
+// batch looked up once (its StreamWr to LDS), then the row blobs into the
+// staging words `stg`, the offsets and lengths into `meta` (0 for padding
+// lanes) and the rows' outputs into the batch's device mirror -- all loads
+// of up to 3 wave-rows in flight together, and one cooperative copy per
+// group of wave-rows of one batch whose outputs lie close together (else
+// each lane copies its own row's) -- so the piece's PCIe latencies are paid
+// here, a few per piece, and nothing later reads host memory.
+__device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, uint64_t base, int count,
+                                                uint32_t lane, StreamWr* wr, StreamPf* pf, const Scratch& sc,
+                                                int stg, int meta, uint32_t ow) {
 #pragma unroll 1
   for (int j = 0; j < count; j++) {
     const StreamRow sr = stream_row(dev, hint, base + (uint32_t)j);
-    bool active;
-    const uint32_t r = stream_lane_row(sr, base + (uint32_t)j, lane, &active);
-    // system-scope stores: written through to host memory whatever the
-    // caching type of the pinned pages
-    if (active)
-      __hip_atomic_store(sr.flags + r, (uint8_t)((hits >> j) & 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (lane == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t e = sr.b % STREAM_RING;
-      const uint32_t before = atomicAdd(&dev->wr_done[e], 1u);
-      if (before + 1u == sr.nwr) {
-        // the entry's count back to 0 for batch b + STREAM_RING; a subtraction,
-        // so it commutes with that batch's counts however late it lands
-        atomicSub(&dev->wr_done[e], sr.nwr);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // complete before the host can reuse the entry
-        __hip_atomic_store(&ctrl->done[e], sr.b + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    StreamWr w;
+    w.mirror = sr.mirror;
+    w.flags = sr.flags;
+    w.matches = sr.matches;
+    w.r0 = (uint32_t)(base + (uint32_t)j - sr.first_wr) * 64u;
+    w.n = sr.n;
+    w.nwr = sr.nwr;
+    w.b = sr.b;
+    wr[j] = w;  // every lane stores the same (wave-uniform) values
+    StreamPf p;
+    p.rows = sr.rows;
+    p.outputs = sr.outputs;
+    p.offs = sr.offs;
+    p.lens = sr.lens;
+    pf[j] = p;
+  }
+#pragma unroll 1
+  for (int g = 0; g < count; g += 3) {
+    uint4 v[3][4];
+    uint32_t of[3], ln[3];
+    bool act[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      act[i] = false;
+      of[i] = ln[i] = 0;
+      if (g + i < count) {
+        const uint32_t r0 = wr[g + i].r0;
+        act[i] = r0 + lane < wr[g + i].n;
+        const uint32_t r = act[i] ? r0 + lane : 0u;
+        const uint4* src = reinterpret_cast<const uint4*>(pf[g + i].rows + (size_t)r * 64);
+#pragma unroll
+        for (int q = 0; q < 4; q++) v[i][q] = src[q];
+        of[i] = pf[g + i].offs[r];
+        ln[i] = pf[g + i].lens[r];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      if (g + i < count) {
+        const int s0 = stg + 16 * (g + i);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          scr_store_w(sc, s0 + 4 * q, v[i][q].x);
+          scr_store_w(sc, s0 + 4 * q + 1, v[i][q].y);
+          scr_store_w(sc, s0 + 4 * q + 2, v[i][q].z);
+          scr_store_w(sc, s0 + 4 * q + 3, v[i][q].w);
+        }
+        if (!act[i]) ln[i] = 0;
+        scr_store_w(sc, meta + 2 * (g + i), of[i]);
+        scr_store_w(sc, meta + 2 * (g + i) + 1, ln[i]);
+      }
+    }
+    // the outputs: runs of wave-rows of one batch whose lists span at most
+    // 48 words per lane are copied by the whole wave; anything else (a
+    // scattered CSR) lane by lane
+    uint32_t lo = ~0u, hi = 0;
+    int i0 = 0;
+#pragma unroll
+    for (int i = 0; i <= 3; i++) {
+      const bool in = g + i < count && i < 3;
+      const bool flush = !in || (i > i0 && wr[g + i].b != wr[g + i0].b);
+      if (flush && i > i0) {
+        int64_t* mir = wr[g + i0].mirror;
+        const int64_t* out = pf[g + i0].outputs;
+        if (hi > lo && (uint64_t)(hi - lo) * ow <= 48u * 64u) {
+          stream_copy_range(mir, out, lo * ow, hi * ow, lane);
+        } else if (hi > lo) {
+#pragma unroll
+          for (int t = 0; t < 3; t++)
+            if (t >= i0 && t < i) {
+#pragma unroll 1
+              for (uint32_t q = of[t] * ow; q < (of[t] + ln[t]) * ow; q++) mir[q] = out[q];
+            }
+        }
+        lo = ~0u;
+        hi = 0;
+        i0 = i;
+      }
+      if (in) {
+        lo = min(lo, wave_min_u32(ln[i] ? of[i] : ~0u));
+        hi = max(hi, wave_max_u32(ln[i] ? of[i] + ln[i] : 0u));
       }
     }
   }
 }
 
-// Base compare of a row; with labels the row's outputs are first copied to
-// the device mirror (read once over PCIe; the label compares read the copy).
-__device__ __forceinline__ bool stream_base_match(const ScanConsts& k, const StreamRow& sr, uint32_t off,
-                                                  uint32_t len, bool active, bool mirror, const fe& x, int64_t v) {
-  if (!mirror) return outputs_match(k, sr.outputs, off, len, x, v);
-  if (!active) return false;
-  const uint32_t ow = k.full_x ? 4u : 1u;
+// Results of the piece's wave-rows (wr: their StreamWr, hits: bit j = row j
+// of this lane matched) into the pinned slots -- one flag per row and/or the
+// matching rows' indices (ballot compaction: one atomic per wave-row with a
+// match) -- then each batch's completion: the wave's stores are complete
+// before its wave-rows count, and the wave whose count finishes a batch
+// writes the batch's match count and, behind a system-scope release, its
+// done word.
+__device__ __forceinline__ void stream_emit(StreamCtrl* ctrl, StreamDev* dev, const StreamWr* wr, int count,
+                                            uint32_t lane, uint32_t hits) {
 #pragma unroll 1
-  for (uint32_t q = off * ow; q < (off + len) * ow; q++) sr.mirror[q] = sr.outputs[q];
-  return outputs_match(k, sr.mirror, off, len, x, v);
+  for (int j = 0; j < count; j++) {
+    const uint32_t r = wr[j].r0 + lane;
+    const bool active = r < wr[j].n;
+    const bool hit = active && ((hits >> j) & 1u);
+    // system-scope stores: written through to host memory whatever the
+    // caching type of the pinned pages
+    uint8_t* flags = wr[j].flags;
+    if (flags != nullptr && active)
+      __hip_atomic_store(flags + r, (uint8_t)(hit ? 1 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* matches = wr[j].matches;
+    if (matches != nullptr) {
+      const uint64_t m = __ballot(hit);
+      if (m) {
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(&dev->nmatch[wr[j].b % STREAM_RING], (uint32_t)__popcll(m));
+        at = (uint32_t)__shfl((int)at, 0);
+        if (hit)
+          __hip_atomic_store(matches + at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), r, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's stores are written before its rows count
+  if (lane == 0) {
+#pragma unroll 1
+    for (int j = 0; j < count; j++) {
+      const uint32_t e = wr[j].b % STREAM_RING;
+      const uint32_t nwr = wr[j].nwr;
+      const uint32_t before = atomicAdd(&dev->wr_done[e], 1u);
+      if (before + 1u == nwr) {
+        // the entry's counts back to 0 for batch b + STREAM_RING (published
+        // only after the host has seen this batch done); the subtraction
+        // commutes with that batch's counts however late it lands
+        atomicSub(&dev->wr_done[e], nwr);
+        const uint32_t nm = atomicExch(&dev->nmatch[e], 0u);
+        __hip_atomic_store(&ctrl->nmatch[e], nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // system-scope release, then the done word: the host's acquire of
+        // `done` sees the match count and every result store before it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&ctrl->done[e], wr[j].b + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ST_EV(ST_DONE, 0u, (uint64_t)nm, wr[j].b, nwr);
+      }
+    }
+  }
+}
+
+// Row bits of a label pass's unit bits (unit u = row u / K, index u % K).
+__device__ __forceinline__ uint32_t stream_unit_rows(uint32_t uh, int K) {
+  if (K == 1) return uh;
+  uint32_t r = 0;
+#pragma unroll 1
+  for (int u = 0; u < MULTI_RMAX; u++)
+    if ((uh >> u) & 1u) r |= 1u << (u / K);
+  return r;
 }
 
 template <int FBB>
@@ -838,7 +1074,8 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
                                                                     const uint32_t* __restrict__ fb,
                                                                     const uint32_t* __restrict__ labels,
                                                                     uint32_t* __restrict__ scr, uint32_t rmax,
-                                                                    uint64_t idle_ticks) {
+                                                                    uint64_t idle_ticks,
+                                                                    unsigned long long* __restrict__ wstat) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = SCAN_SCRATCH(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
@@ -850,20 +1087,39 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
   constexpr int LB = VB_SCRATCH_WORDS + PEND_WORDS * multi_pend_slots(true);
   const int QF = LB + FW * (int)k.label_count * MULTI_RMAX;
   const int QACC = QF + 2 * FW * MULTI_RMAX;
-  const bool mirror = k.label_count != 0;
-  // pieces of the pipelined schedule: P (F points pending), Q (labels pending)
-  uint64_t base_p = 0, base_q = 0;
+  const int STG = (int)multi_scratch_words(k.label_count, true);
+  const int META = STG + STREAM_STG_WORDS;  // piece area a: META + 2 MULTI_RMAX a
+  const int SXA = META + STREAM_META_WORDS;
+  const int K = (int)k.output_count;  // 1 .. MULTI_RMAX (cudasp_stream_create); K x rmax <= MULTI_RMAX
+  const bool with_labels = k.label_count != 0;
+  const uint32_t ow = k.full_x ? 4u : 1u;
+  // pieces of the pipelined schedule: P (F points pending), Q (labels
+  // pending), each with its wave-rows' StreamWr and offsets/lengths in piece
+  // area pp / pq; the new piece's go to area pn
   int count_p = 0, count_q = 0;
-  uint32_t hint_p = 0, hint_q = 0, hint = 0, hits_q = 0;
+  int pn = 0, pp = 1, pq = 2;
+  uint32_t hint = 0, hits_q = 0;
   // lane 0's ticket and counters live in LDS, so none of them is held in
   // registers through a piece's ladders
   __shared__ StreamWave waves[BLOCK / 64];
-  volatile StreamWave& me = waves[threadIdx.x >> 6];
+  __shared__ StreamWr wrs[BLOCK / 64][3][MULTI_RMAX];
+  __shared__ StreamPf pfs[BLOCK / 64][MULTI_RMAX];
+  const uint32_t wid = threadIdx.x >> 6;
+  volatile StreamWave& me = waves[wid];
   if (lane == 0) {
     me.tk = me.tr = me.have = me.mine = 0;
     me.t_start = wall_clock64();
     me.busy = me.pieces = me.rows = me.polls = me.drains = 0;
   }
+#if CUDASP_STREAM_TRACE
+  const uint32_t st_wave = slot / 64u;
+  if (lane == 0) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    ST_EV(ST_START, st_wave, (uint64_t)hw | ((uint64_t)xcc << 32), 0u, 0u);
+  }
+#endif
   bool stop = false;  // closed or idle, nothing published left in the ticket: leave once drained
   for (;;) {
     const uint64_t t_it = wall_clock64();
@@ -889,6 +1145,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
           me.tr = tr;
           me.mine = me.mine + tr;
           me.have = 1;
+          ST_EV(ST_CLAIM, st_wave, me.tk, tr, (uint32_t)(pw - cur));
         }
       }
       const uint64_t tk = me.tk;
@@ -928,37 +1185,24 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
         me.pieces = me.pieces + 1;
         me.rows = me.rows + (uint32_t)count;
       }
+      ST_EV(ST_PIECE, st_wave, base, (uint32_t)count, (uint32_t)count_p | ((uint32_t)count_q << 8));
     }
-    uint32_t hint_c = hint;
-    if (count) {
-      hint_c = stream_batch_of(dev, hint, base);
-      hint = hint_c;
-    }
-    // stage A: S = d T of the new piece's rows (read from the pinned slot)
-    {
-      uint32_t h = hint_c;
+    StreamWr* const wn = wrs[wid][pn];
+    const int meta_n = META + 2 * MULTI_RMAX * pn;
+    if (count) stream_prefetch(dev, hint, base, count, lane, wn, pfs[wid], sc, STG, meta_n, ow);
+    const int np = count_p * K;  // F points of piece P in pending slots 0 .. np - 1
+    // stage A: S = d T of the new piece's rows (staged by the prefetch)
 #pragma unroll 1
-      for (int j = 0; j < count; j++) {
-        const StreamRow sr = stream_row(dev, h, base + (uint32_t)j);
-        bool active;
-        const uint32_t r = stream_lane_row(sr, base + (uint32_t)j, lane, &active);
-        const uint4* src = reinterpret_cast<const uint4*>(sr.rows + (size_t)r * 64);
-        uint32_t w[16];
+    for (int j = 0; j < count; j++) {
+      uint32_t w[16];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const uint4 v = src[q];
-          w[4 * q] = v.x;
-          w[4 * q + 1] = v.y;
-          w[4 * q + 2] = v.z;
-          w[4 * q + 3] = v.w;
-        }
-        gej P;
-        row_shared_secret_point(P, w, w + 8, naf, k.naf_len, sc);
-        pend_store(sc, PB, count_p + j, P);
-      }
+      for (int q = 0; q < 16; q++) w[q] = scr_load_w(sc, STG + 16 * j + q);
+      gej P;
+      row_shared_secret_point(P, w, w + 8, naf, k.naf_len, sc);
+      pend_store(sc, PB, np + j, P);
     }
     // one inversion: the new S points, piece P's F points, piece Q's label product
-    int ninv = count_p + count;
+    int ninv = np + count;
     if (count_q) {
       fe acc;
       scr_load(acc, sc, QACC);
@@ -966,88 +1210,125 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
       ninv++;
     }
     pend_invert<2 * MULTI_RMAX + 1>(sc, PB, ninv);
-    const auto qf_at = [&](int j, ge& F) {
-      scr_load(F.x, sc, QF + 2 * FW * j);
-      scr_load(F.y, sc, QF + 2 * FW * j + FW);
+    const auto qf_at = [&](int u, ge& F) {
+      scr_load(F.x, sc, QF + 2 * FW * u);
+      scr_load(F.y, sc, QF + 2 * FW * u + FW);
     };
-    if (count_q) {  // piece Q: its labels against the mirrored outputs, then its flags
-      const auto q_out = [&](int j, const int64_t*& o, uint32_t& off, uint32_t& len, int64_t*& vrow,
+    if (count_q) {  // piece Q: its labels against the mirrored outputs, then its results
+      const StreamWr* wq = wrs[wid][pq];
+      const int meta_q = META + 2 * MULTI_RMAX * pq;
+      const auto q_out = [&](int u, const int64_t*& o, uint32_t& off, uint32_t& len, int64_t*& vrow,
                              uint32_t& vstride) {
-        uint32_t h = hint_q;
-        const StreamRow sr = stream_row(dev, h, base_q + (uint32_t)j);
-        bool active;
-        const uint32_t r = stream_lane_row(sr, base_q + (uint32_t)j, lane, &active);
-        o = sr.mirror;
-        off = sr.offs[r];
-        len = active ? sr.lens[r] : 0u;
+        const int j = u / K;
+        o = wq[j].mirror;
+        off = scr_load_w(sc, meta_q + 2 * j);
+        len = scr_load_w(sc, meta_q + 2 * j + 1);  // 0 for padding lanes
         vrow = nullptr;
         vstride = 0;
       };
       fe inv;
       scr_load(inv, sc, PEND_ZI(PB, ninv - 1));
-      hits_q |= labels_backward(inv, k, labels, count_q, sc, LB, qf_at, q_out);
-      stream_emit(ctrl, dev, base_q, count_q, hint_q, lane, hits_q);
+      hits_q |= stream_unit_rows(labels_backward(inv, k, labels, count_q * K, sc, LB, qf_at, q_out), K);
+      stream_emit(ctrl, dev, wq, count_q, lane, hits_q);
       count_q = 0;
     }
     if (count_p) {  // piece P: affine F, base compare; its labels wait one iteration
-      uint32_t hits = 0, h = hint_p;
+      const StreamWr* wp = wrs[wid][pp];
+      const int meta_p = META + 2 * MULTI_RMAX * pp;
+      uint32_t hits = 0;
 #pragma unroll 1
-      for (int j = 0; j < count_p; j++) {
-        const StreamRow sr = stream_row(dev, h, base_p + (uint32_t)j);
-        bool active;
-        const uint32_t r = stream_lane_row(sr, base_p + (uint32_t)j, lane, &active);
+      for (int u = 0; u < np; u++) {
+        const int j = u / K;
         gej P;
         fe zi;
-        pend_load(P, sc, PB, j);
-        scr_load(zi, sc, PEND_ZI(PB, j));
+        pend_load(P, sc, PB, u);
+        scr_load(zi, sc, PEND_ZI(PB, u));
         ge F;
         gej_to_ge_zinv(F, P, zi);
-        if (mirror) {
-          scr_store(sc, QF + 2 * FW * j, F.x);
-          scr_store(sc, QF + 2 * FW * j + FW, F.y);
+        if (with_labels) {
+          scr_store(sc, QF + 2 * FW * u, F.x);
+          scr_store(sc, QF + 2 * FW * u + FW, F.y);
         }
-        if (stream_base_match(k, sr, sr.offs[r], active ? sr.lens[r] : 0u, active, mirror, F.x, fe_upper64(F.x)))
-          hits |= 1u << j;
+        const uint32_t off = scr_load_w(sc, meta_p + 2 * j);
+        const uint32_t len = scr_load_w(sc, meta_p + 2 * j + 1);  // 0 for padding lanes
+        if (outputs_match(k, wp[j].mirror, off, len, F.x, fe_upper64(F.x))) hits |= 1u << j;
       }
-      if (mirror) {
+      if (with_labels) {
         fe acc;
-        labels_forward(acc, k, labels, count_p, sc, LB, qf_at);
+        labels_forward(acc, k, labels, np, sc, LB, qf_at);
         scr_store(sc, QACC, acc);
-        base_q = base_p;
-        hint_q = hint_p;
+        const int t = pq;  // P's wave-rows and offsets become Q's
+        pq = pp;
+        pp = t;
         count_q = count_p;
         hits_q = hits;
       } else {
-        stream_emit(ctrl, dev, base_p, count_p, hint_p, lane, hits);
+        stream_emit(ctrl, dev, wp, count_p, lane, hits);
       }
     }
-    // t of each new row, then stage B's F = t G + B into slot j
+    // t of each new row (K output indices), then stage B's F = t G + B into
+    // slots u = j K + kk
+    if (K == 1) {
 #pragma unroll 1
-    for (int j = 0; j < count; j++) {
-      gej P;
-      fe zi;
-      pend_load(P, sc, PB, count_p + j);
-      scr_load(zi, sc, PEND_ZI(PB, count_p + j));
-      uint32_t sx[8], t[8];
-      const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
-      bip352_shared_secret_hash(t, k.mid, sx, y_odd);
-      gej F;
-      row_match_point<FBB>(F, t, fb, k);
-      pend_store(sc, PB, j, F);
+      for (int j = 0; j < count; j++) {
+        gej P;
+        fe zi;
+        pend_load(P, sc, PB, np + j);
+        scr_load(zi, sc, PEND_ZI(PB, np + j));
+        uint32_t sx[8], t[8];
+        const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
+        bip352_shared_secret_hash(t, k.mid, sx, y_odd);
+        gej F;
+        row_match_point<FBB>(F, t, fb, k);
+        pend_store(sc, PB, j, F);  // slot np + j' (j' < j) is consumed already
+      }
+    } else {
+      // every S first (the F slots of row j overlap later rows' S slots)
+#pragma unroll 1
+      for (int j = 0; j < count; j++) {
+        gej P;
+        fe zi;
+        pend_load(P, sc, PB, np + j);
+        scr_load(zi, sc, PEND_ZI(PB, np + j));
+        uint32_t sx[8];
+        const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
+#pragma unroll
+        for (int q = 0; q < 8; q++) scr_store_w(sc, SXA + 9 * j + q, sx[q]);
+        scr_store_w(sc, SXA + 9 * j + 8, y_odd);
+      }
+#pragma unroll 1
+      for (int u = 0; u < count * K; u++) {
+        const int j = u / K, kk = u - j * K;
+        uint32_t sx[8], t[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) sx[q] = scr_load_w(sc, SXA + 9 * j + q);
+        const uint32_t y_odd = scr_load_w(sc, SXA + 9 * j + 8);
+        bip352_shared_secret_hash(t, k.mid, sx, y_odd, (uint32_t)kk);
+        gej F;
+        row_match_point<FBB>(F, t, fb, k);
+        pend_store(sc, PB, u, F);
+      }
     }
-    base_p = base;
-    hint_p = hint_c;
+    {  // the new piece becomes P
+      const int t = pp;
+      pp = pn;
+      pn = t;
+    }
     count_p = count;
-    if (lane == 0) me.busy = me.busy + (wall_clock64() - t_it);
+    if (lane == 0) {
+      me.busy = me.busy + (wall_clock64() - t_it);
+      ST_EV(ST_ITER_END, st_wave, 0ull, 0u, 0u);
+    }
   }
   if (lane == 0) {
-    atomicAdd(&dev->stat[STREAM_STAT_WORKER_EXITS], 1ull);
-    atomicAdd(&dev->stat[STREAM_STAT_PIECES], (unsigned long long)me.pieces);
-    atomicAdd(&dev->stat[STREAM_STAT_WAVE_ROWS], (unsigned long long)me.rows);
-    atomicAdd(&dev->stat[STREAM_STAT_WAIT_POLLS], (unsigned long long)me.polls);
-    atomicAdd(&dev->stat[STREAM_STAT_DRAINS], (unsigned long long)me.drains);
-    atomicAdd(&dev->stat[STREAM_STAT_BUSY_TICKS], (unsigned long long)me.busy);
-    atomicAdd(&dev->stat[STREAM_STAT_LIFE_TICKS], (unsigned long long)(wall_clock64() - me.t_start));
+    ST_EV(ST_EXIT, st_wave, 0ull, me.polls, me.rows);
+    // this wave's counters, summed over the query's launches (a wave slot
+    // runs one wave per launch); the host adds them up (cudasp_stream_counters)
+    unsigned long long* o = wstat + (size_t)(slot / 64u) * STREAM_WSTAT;
+    const unsigned long long v[STREAM_WSTAT] = {me.pieces, me.rows, me.polls, me.drains, 0ull, 1ull, me.busy,
+                                                wall_clock64() - me.t_start};
+#pragma unroll
+    for (int i = 0; i < (int)STREAM_WSTAT; i++) o[i] += v[i];
   }
 }
 
@@ -1281,34 +1562,31 @@ std::map<std::pair<int, int>, DeviceTable> g_tables;
 // (LDS-staged, stage B only).
 bool fb_bits_supported(int bits) { return bits == 22 || bits == 26 || bits == LDS_FB_BITS; }
 
-int g_default_fb_bits = 0;  // 0: not read yet
-std::once_flag g_default_fb_once;
-
 // Devices with at least this much memory take the 26-bit table by default
 // (21.5 GB: 7.5% of an MI355X's 288 GB); smaller ones the 22-bit table.
 constexpr uint64_t FB26_MIN_DEVICE_BYTES = 128ull << 30;
 
-// The process default width: CUDASP_FB_BITS (22 or 26) from the environment;
-// else 26 bits when the current device has >= 128 GiB (every MI355X), else
-// the build's FB_BITS.  Read once per process (the synthetic generator uses
-// it too).
-int default_fb_bits() {
-  std::call_once(g_default_fb_once, [] {
-    g_default_fb_bits = FB_BITS;
-    if (const char* e = getenv("CUDASP_FB_BITS")) {
-      const int b = atoi(e);
-      if (b == 22 || b == 26) {
-        g_default_fb_bits = b;
-        return;
-      }
-    }
-    int dev = 0;
-    size_t total = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceTotalMem(&total, dev) == hipSuccess &&
-        (uint64_t)total >= FB26_MIN_DEVICE_BYTES)
-      g_default_fb_bits = 26;
-  });
-  return g_default_fb_bits;
+// The default width of a device (-1: the current one): CUDASP_FB_BITS (22 or
+// 26) from the environment; else 26 bits when that device has >= 128 GiB
+// (every MI355X), else the build's FB_BITS.  Decided once per device, so a
+// host with GPUs of different sizes gives each its own.
+int default_fb_bits(int device = -1) {
+  static const int env_bits = [] {
+    const char* e = getenv("CUDASP_FB_BITS");
+    const int b = e ? atoi(e) : 0;
+    return b == 22 || b == 26 ? b : 0;
+  }();
+  if (env_bits) return env_bits;
+  if (device < 0 && hipGetDevice(&device) != hipSuccess) return FB_BITS;
+  static std::mutex mu;
+  static std::map<int, int> bits_of;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = bits_of.find(device);
+  if (it != bits_of.end()) return it->second;
+  size_t total = 0;
+  const int b = hipDeviceTotalMem(&total, device) == hipSuccess && (uint64_t)total >= FB26_MIN_DEVICE_BYTES ? 26 : FB_BITS;
+  bits_of[device] = b;
+  return b;
 }
 
 size_t fb_table_bytes(int bits) {
@@ -1377,6 +1655,8 @@ struct cudasp_scanner {
   cudasp_scan_options opt{1, 0, 0};
   uint32_t t_cap_k = 1;            // output indices d_t / d_vflags are sized for
   std::vector<uint8_t> keys;       // scan key || spend key || label keys (set_options re-prepares)
+  bool prepared = false;           // consts / d_naf / d_labels hold `keys` under prepared_opt (set_keys)
+  cudasp_scan_options prepared_opt{1, 0, 0};
   uint32_t raw_label_count = 0;
   // Stage-kernel buffers (k_shared_secret / k_match: the stage entry points,
   // the values path, the protocol variants, the LDS width).  Allocated on
@@ -1682,30 +1962,48 @@ static MultiBatch multi_desc(const uint32_t* tx, const uint32_t* ty, const int64
 
 // Blocks of a persistent k_scan_multi / k_scan_stream grid: at most
 // CUDASP_WAVES_A waves per SIMD (one 256-thread block = one wave per SIMD of a
-// CU), blocks_req if smaller (0 = the whole device), within 4 GiB of scratch.
-static uint64_t multi_grid_blocks(cudasp_scanner* s, uint64_t blocks_req, bool pipe) {
+// CU), blocks_req if smaller (0 = the whole device), within 4 GiB of scratch
+// (`words` per thread).
+static uint64_t grid_blocks_for(cudasp_scanner* s, uint64_t blocks_req, uint64_t words) {
   if (!s->cus) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus <= 0)
       cus = 256;
     s->cus = cus;
   }
-  const uint64_t words = multi_scratch_words(s->consts.label_count, pipe);
   const uint64_t full_blocks = (uint64_t)s->cus * CUDASP_WAVES_A;
   const uint64_t cap_blocks = ((1ull << 32) - 1) / 4 / (words * BLOCK);
   uint64_t blocks = blocks_req ? blocks_req : full_blocks;
   if (blocks > full_blocks) blocks = full_blocks;
   if (blocks > cap_blocks) blocks = cap_blocks;
+  if (blocks > MAX_BLOCKS) blocks = MAX_BLOCKS;
   return blocks;
 }
 
-// k_scan_multi / k_scan_stream scratch for `blocks` blocks.  Sized for the
-// blocks a launch runs (a 300k-row fused batch: ~293 of the 768 persistent
-// blocks), grown when a later launch runs more.  An allocation failure is
-// reported as CUDASP_ERR_CAPACITY before anything is queued, so
-// launch_pipeline can fall back to the stage kernels.
-static int ensure_multi_scratch(cudasp_scanner* s, uint64_t blocks, bool pipe, hipStream_t st) {
-  const uint64_t need_words = blocks * BLOCK * multi_scratch_words(s->consts.label_count, pipe);
+static uint64_t multi_grid_blocks(cudasp_scanner* s, uint64_t blocks_req, bool pipe) {
+  return grid_blocks_for(s, blocks_req, multi_scratch_words(s->consts.label_count, pipe));
+}
+
+static uint64_t stream_grid_blocks(cudasp_scanner* s, uint64_t blocks_req) {
+  return grid_blocks_for(s, blocks_req, stream_scratch_words(s->consts.label_count));
+}
+
+// The streaming scan's options: output_count up to MULTI_RMAX (K x rows per
+// piece <= MULTI_RMAX), an HBM fixed-base width, the pipelined schedule.
+static_assert(CUDASP_STREAM_MAX_OUTPUT_COUNT <= MULTI_RMAX, "K x rows of a piece <= MULTI_RMAX");
+static bool stream_ok(const cudasp_scanner* s) {
+  return s->consts.output_count >= 1 && s->consts.output_count <= (uint32_t)CUDASP_STREAM_MAX_OUTPUT_COUNT &&
+         (s->fb_bits == 22 || s->fb_bits == 26) && s->multi_pipe &&
+         (uint64_t)stream_scratch_words(s->consts.label_count) * 4 * BLOCK <= (1ull << 32) - 1;
+}
+
+// k_scan_multi / k_scan_stream scratch for `blocks` blocks of `words` per
+// thread.  Sized for the blocks a launch runs (a 300k-row fused batch: ~293
+// of the 768 persistent blocks), grown when a later launch runs more.  An
+// allocation failure is reported as CUDASP_ERR_CAPACITY before anything is
+// queued, so launch_pipeline can fall back to the stage kernels.
+static int ensure_scratch_words(cudasp_scanner* s, uint64_t blocks, uint64_t words, hipStream_t st) {
+  const uint64_t need_words = blocks * BLOCK * words;
   if (need_words <= s->mscratch_words) return CUDASP_OK;
   HIP_TRY(hipStreamSynchronize(st));  // no kernel of this scanner still uses the old scratch
   if (s->d_mscratch) HIP_TRY(hipFree(s->d_mscratch));
@@ -1718,6 +2016,14 @@ static int ensure_multi_scratch(cudasp_scanner* s, uint64_t blocks, bool pipe, h
   }
   s->mscratch_words = need_words;
   return CUDASP_OK;
+}
+
+static int ensure_multi_scratch(cudasp_scanner* s, uint64_t blocks, bool pipe, hipStream_t st) {
+  return ensure_scratch_words(s, blocks, multi_scratch_words(s->consts.label_count, pipe), st);
+}
+
+static int ensure_stream_scratch(cudasp_scanner* s, uint64_t blocks, hipStream_t st) {
+  return ensure_scratch_words(s, blocks, stream_scratch_words(s->consts.label_count), st);
 }
 
 // One k_scan_multi launch over the described batches (total_wr wave-rows):
@@ -1864,7 +2170,7 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
 
   // --- device state --------------------------------------------------------
   DeviceGuard g(device);
-  s->fb_bits = default_fb_bits();
+  s->fb_bits = default_fb_bits(device);
   int rc = ensure_device_table(device, s->fb_bits, &s->d_fb);
   if (rc != CUDASP_OK) {
     delete s;
@@ -1927,6 +2233,7 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
     free_scanner(s);
     return set_error(CUDASP_ERR_HIP, "hipMemcpy failed: %s", hipGetErrorString(e));
   }
+  s->prepared = true;  // prepare_scan above used the default options (s->opt)
   *out = s;
   return CUDASP_OK;
 }
@@ -1938,6 +2245,13 @@ int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32
   g_last_error.clear();
   if (!s || !scan_private_key || !spend_public_key || (label_count > 0 && !label_keys))
     return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  // the keys and options the scanner's constants were prepared for: nothing
+  // to do (a pooled scanner rebound to the same wallet, query after query)
+  if (s->prepared && label_count == s->raw_label_count && s->keys.size() == 96 + 64 * (size_t)label_count &&
+      memcmp(s->keys.data(), scan_private_key, 32) == 0 && memcmp(s->keys.data() + 32, spend_public_key, 64) == 0 &&
+      (label_count == 0 || memcmp(s->keys.data() + 96, label_keys, 64 * (size_t)label_count) == 0) &&
+      memcmp(&s->prepared_opt, &s->opt, sizeof(s->opt)) == 0)
+    return CUDASP_OK;
   ScanConsts consts;
   std::vector<int8_t> naf;
   std::vector<uint32_t> labels;
@@ -1976,6 +2290,8 @@ int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32
   HIP_TRY(hipMemcpy(s->d_labels, labels.data(), labels.size() * 4, hipMemcpyHostToDevice));
   s->consts = consts;
   s->label_count = label_count;
+  s->prepared = true;
+  s->prepared_opt = s->opt;
   if (s->keys.data() != scan_private_key) {
     std::vector<uint8_t> keys(scan_private_key, scan_private_key + 32);
     keys.insert(keys.end(), spend_public_key, spend_public_key + 64);
@@ -1994,6 +2310,10 @@ int cudasp_scanner_set_options(cudasp_scanner* s, const cudasp_scan_options* opt
     return set_error(CUDASP_ERR_INVALID_ARG, "output_count must be between 1 and %d", CUDASP_MAX_OUTPUT_COUNT);
   if ((uint64_t)K * s->capacity > 0xFFFFFFFFull)
     return set_error(CUDASP_ERR_CAPACITY, "output_count %u x capacity %u exceeds 2^32 virtual rows", K, s->capacity);
+  if (K == s->opt.output_count && (options->label_negation != 0) == (s->opt.label_negation != 0) &&
+      (options->full_x != 0) == (s->opt.full_x != 0) && s->prepared &&
+      memcmp(&s->prepared_opt, &s->opt, sizeof(s->opt)) == 0)
+    return CUDASP_OK;  // unchanged
   DeviceGuard g(s->device);
   HIP_TRY(hipStreamSynchronize(s->stream));
   if (K > s->t_cap_k && !s->d_t) {
@@ -2030,7 +2350,7 @@ uint64_t cudasp_fixed_base_table_bytes(int bits) { return fb_bits_supported(bits
 int cudasp_scanner_set_fixed_base_bits(cudasp_scanner* s, int bits) {
   g_last_error.clear();
   if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
-  if (bits == 0) bits = default_fb_bits();
+  if (bits == 0) bits = default_fb_bits(s->device);
   if (bits == s->fb_bits) return CUDASP_OK;
   DeviceGuard g(s->device);
   HIP_TRY(hipStreamSynchronize(s->stream));
@@ -2321,18 +2641,46 @@ int cudasp_debug_field_ops(int op, const uint32_t* d_a, const uint32_t* d_b, uin
 // ----------------------------------------------------------- streaming scan
 // cudasp_stream_*: one persistent k_scan_stream kernel scans batches as the
 // host publishes them (scan_stream.hpp).
+
+// Coherent pinned allocations of cudasp_host_alloc, by start address: a
+// published batch's host buffers must lie inside them.  The protocol needs
+// it: the kernel reads the buffers with uncached (MTYPE UC) loads and writes
+// its results with system-scope stores that the host sees without any cache
+// maintenance, which holds for coherent host memory only (a non-coherent
+// pinned buffer would let results sit in a device cache).
+static std::mutex g_host_alloc_mu;
+static std::map<uintptr_t, size_t> g_host_allocs;
+
+static bool host_range_coherent(const void* p, size_t bytes) {
+  if (!p) return false;
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> lk(g_host_alloc_mu);
+  auto it = g_host_allocs.upper_bound(a);
+  if (it == g_host_allocs.begin()) return false;
+  --it;
+  return a >= it->first && a + bytes <= it->first + it->second;
+}
+
+constexpr uint32_t STREAM_MAX_WAVES = MAX_BLOCKS * (BLOCK / 64);
+
 struct cudasp_stream {
   cudasp_scanner* s = nullptr;
   StreamCtrl* ctrl = nullptr;  // coherent pinned host memory (same address on the device)
   StreamDev* dev = nullptr;    // device memory
+  unsigned long long* wstat = nullptr;    // device: STREAM_WSTAT counters per wave slot of the grid
+  unsigned long long* h_counts = nullptr;  // pinned: StreamDev::stat, then the per-wave counters (finish copies)
   uint64_t blocks_req = 0;  // requested grid (0: the whole device)
   uint64_t blocks = 0;      // the current query's grid
   uint32_t rmax = MULTI_RMAX;
   uint64_t idle_ticks = 0;  // 100 MHz wall-clock ticks with nothing to do before the kernel leaves
+  uint32_t timeout_ms = 0;  // waits fail after this long without progress (cudasp_stream_set_timeout)
   hipEvent_t exited = nullptr;
   bool running = false;     // a kernel was launched and `exited` recorded after it
-  bool failed = false;      // a kernel of this query failed (sticky until finish)
+  bool failed = false;      // a kernel of this query failed or a wait timed out (sticky until finish)
+  bool abandoned = false;   // finish timed out with the kernel alive: nothing may be freed
   bool next_launch_resets = false;  // a kernel of this query ran: the next one follows k_stream_relaunch
+  bool counts_pending = false;      // finish queued the counters' copy; counters() waits for it
+  uint64_t counts_waves = 0;        // wave slots of the last finished query's grid
   uint32_t next = 0;        // batches published
   uint64_t published_wr = 0;
   uint64_t launches = 0;
@@ -2374,20 +2722,23 @@ __global__ void k_stream_relaunch(StreamDev* dev) {
 static int stream_launch(cudasp_stream* st) {
   cudasp_scanner* s = st->s;
   DeviceGuard g(s->device);
-  if (!multi_ok(s) || !s->multi_pipe)
+  if (!stream_ok(s))
     return set_error(CUDASP_ERR_INVALID_ARG, "the scanner's options do not allow the streaming scan");
-  st->blocks = multi_grid_blocks(s, st->blocks_req, true);
+  st->blocks = stream_grid_blocks(s, st->blocks_req);
   if (st->blocks < 2) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the streaming scan");
   {
-    const int rc = ensure_multi_scratch(s, st->blocks, true, s->stream);
+    const int rc = ensure_stream_scratch(s, st->blocks, s->stream);
     if (rc != CUDASP_OK) return rc;
   }
+  const uint32_t K = s->consts.output_count;
+  const uint32_t rmax = std::max(1u, std::min(st->rmax, (uint32_t)MULTI_RMAX / K));
   if (st->next_launch_resets) hipLaunchKernelGGL(k_stream_relaunch, dim3(1), dim3(64), 0, s->stream, st->dev);
   auto kf = s->fb_bits == 26 ? k_scan_stream<26> : k_scan_stream<22>;
   hipLaunchKernelGGL(kf, dim3((uint32_t)st->blocks), dim3(BLOCK), 0, s->stream, st->ctrl, st->dev, s->d_naf,
-                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, st->rmax, st->idle_ticks);
+                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, rmax, st->idle_ticks, st->wstat);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(st->exited, s->stream));
+  ST_HOST(102, st->blocks, (uint32_t)st->launches);
   st->running = true;
   st->next_launch_resets = true;
   st->launches++;
@@ -2409,6 +2760,16 @@ static bool stream_seq_done(const cudasp_stream* st, uint64_t seq) {
   return (int32_t)(d - (uint32_t)(seq + 1)) >= 0;
 }
 
+// A fingerprint of the kernel's visible progress: the done words of the ring
+// (a completed batch changes one) -- what a wait's no-progress deadline
+// watches.
+static uint64_t stream_progress(const cudasp_stream* st) {
+  uint64_t h = 0;
+  for (uint32_t e = 0; e < STREAM_RING; e++)
+    h = h * 1000003ull + __atomic_load_n(&st->ctrl->done[e], __ATOMIC_ACQUIRE);
+  return h;
+}
+
 int cudasp_host_alloc(void** p, size_t bytes) {
   if (!p) return set_error(CUDASP_ERR_INVALID_ARG, "null pointer");
   *p = nullptr;
@@ -2420,26 +2781,41 @@ int cudasp_host_alloc(void** p, size_t bytes) {
     (void)hipHostFree(q);
     return set_error(CUDASP_ERR_HIP, "pinned host memory is not device-addressable at its host address");
   }
+  {
+    std::lock_guard<std::mutex> lk(g_host_alloc_mu);
+    g_host_allocs[(uintptr_t)q] = bytes;
+  }
   *p = q;
   return CUDASP_OK;
 }
 
 void cudasp_host_free(void* p) {
-  if (p) (void)hipHostFree(p);
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(g_host_alloc_mu);
+    g_host_allocs.erase((uintptr_t)p);
+  }
+  (void)hipHostFree(p);
+}
+
+int cudasp_stream_supported(const cudasp_scanner* s) {
+  if (!s || !stream_ok(s)) return 0;
+  return stream_grid_blocks(const_cast<cudasp_scanner*>(s), 0) >= 2 ? 1 : 0;
 }
 
 int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out) {
   if (!s || !out) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
   *out = nullptr;
-  if (!multi_ok(s) || !s->multi_pipe)
+  if (!stream_ok(s))
     return set_error(CUDASP_ERR_INVALID_ARG,
-                     "the streaming scan needs the default options (output_count 1), an HBM fixed-base width "
-                     "(22 or 26 bits) and the pipelined schedule");
+                     "the streaming scan needs output_count <= %d, an HBM fixed-base width (22 or 26 bits) and the "
+                     "pipelined schedule",
+                     CUDASP_STREAM_MAX_OUTPUT_COUNT);
   DeviceGuard g(s->device);
   std::unique_ptr<cudasp_stream> st(new cudasp_stream());
   st->s = s;
   st->blocks_req = blocks;
-  st->blocks = multi_grid_blocks(s, blocks, true);
+  st->blocks = stream_grid_blocks(s, blocks);
   if (st->blocks < 2) return set_error(CUDASP_ERR_INVALID_ARG, "too many label keys for the streaming scan");
   uint32_t idle_ms = 20;
   if (const char* e = getenv("CUDASP_STREAM_IDLE_MS")) {
@@ -2447,19 +2823,28 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
     if (v >= 1 && v <= 600000) idle_ms = (uint32_t)v;
   }
   st->idle_ticks = (uint64_t)idle_ms * 100000ull;
+  st->timeout_ms = 60000;
+  if (const char* e = getenv("CUDASP_STREAM_TIMEOUT_MS")) {
+    const long v = atol(e);
+    if (v >= 1 && v <= 86400000) st->timeout_ms = (uint32_t)v;
+  }
   if (const char* e = getenv("CUDASP_MULTI_ROWS")) {
     const int v = atoi(e);
     if (v >= 1 && v <= MULTI_RMAX) st->rmax = (uint32_t)v;
   }
-  int rc = ensure_multi_scratch(s, st->blocks, true, s->stream);
+  int rc = ensure_stream_scratch(s, st->blocks, s->stream);
   if (rc != CUDASP_OK) return rc;
   void* c = nullptr;
   rc = cudasp_host_alloc(&c, sizeof(StreamCtrl));
   if (rc != CUDASP_OK) return rc;
   st->ctrl = static_cast<StreamCtrl*>(c);
   memset(st->ctrl, 0, sizeof(StreamCtrl));
-  if (hipMalloc(&st->dev, sizeof(StreamDev)) != hipSuccess || hipEventCreateWithFlags(&st->exited, hipEventDisableTiming) != hipSuccess ||
-      hipMemsetAsync(st->dev, 0, sizeof(StreamDev), s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
+  const size_t wbytes = (size_t)STREAM_MAX_WAVES * STREAM_WSTAT * sizeof(unsigned long long);
+  if (hipMalloc(&st->dev, sizeof(StreamDev)) != hipSuccess || hipMalloc(&st->wstat, wbytes) != hipSuccess ||
+      hipHostMalloc(&st->h_counts, 16 * sizeof(unsigned long long) + wbytes, hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&st->exited, hipEventDisableTiming) != hipSuccess ||
+      hipMemsetAsync(st->dev, 0, sizeof(StreamDev), s->stream) != hipSuccess ||
+      hipMemsetAsync(st->wstat, 0, wbytes, s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
     cudasp_stream_destroy(st.release());
     return set_error(CUDASP_ERR_HIP, "streaming scan: device state allocation failed");
   }
@@ -2467,26 +2852,40 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
   return CUDASP_OK;
 }
 
-int cudasp_stream_publish(cudasp_stream* st, const uint8_t* rows, const int64_t* outputs, const uint32_t* offs,
-                          const uint32_t* lens, uint32_t n, uint8_t* flags, int64_t* d_mirror, uint64_t* seq) {
-  if (!st) return set_error(CUDASP_ERR_INVALID_ARG, "null stream");
-  if (n == 0 || !rows || !offs || !lens || !flags) return set_error(CUDASP_ERR_INVALID_ARG, "empty batch or null buffer");
-  if (st->s->consts.label_count && !d_mirror)
-    return set_error(CUDASP_ERR_INVALID_ARG, "a streaming scan with labels needs an outputs mirror in device memory");
+int cudasp_stream_publish_batch(cudasp_stream* st, const cudasp_stream_batch* bt, uint64_t* seq) {
+  if (!st || !bt) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  const uint32_t n = bt->n;
+  if (n == 0 || !bt->tweak_keys || !bt->output_offsets || !bt->output_lengths || !bt->d_mirror)
+    return set_error(CUDASP_ERR_INVALID_ARG, "empty batch or null buffer (the outputs mirror included)");
+  if (!bt->match_flags && !bt->match_rows)
+    return set_error(CUDASP_ERR_INVALID_ARG, "a streamed batch needs match_flags and/or match_rows");
+  // every host buffer the kernel touches must be coherent pinned memory
+  // (cudasp_host_alloc); the outputs are checked up to the last offset + length
+  uint64_t words = 0;
+  const uint64_t ow = st->s->consts.full_x ? 4 : 1;
+  if (!host_range_coherent(bt->output_offsets, (size_t)n * 4) || !host_range_coherent(bt->output_lengths, (size_t)n * 4))
+    return set_error(CUDASP_ERR_INVALID_ARG, "streamed batch buffers must come from cudasp_host_alloc");
+  for (uint32_t i = 0; i < n; i++) words = std::max<uint64_t>(words, ((uint64_t)bt->output_offsets[i] + bt->output_lengths[i]) * ow);
+  if (!host_range_coherent(bt->tweak_keys, (size_t)n * 64) ||
+      (words && !host_range_coherent(bt->outputs, (size_t)words * 8)) ||
+      (bt->match_flags && !host_range_coherent(bt->match_flags, n)) ||
+      (bt->match_rows && !host_range_coherent(bt->match_rows, (size_t)n * 4)))
+    return set_error(CUDASP_ERR_INVALID_ARG, "streamed batch buffers must come from cudasp_host_alloc");
   std::lock_guard<std::mutex> lk(st->mu);
-  if (st->ctrl->closed) return set_error(CUDASP_ERR_INVALID_ARG, "stream already finished");
+  if (st->ctrl->closed) return set_error(CUDASP_ERR_INVALID_ARG, "stream already closed");
   if (st->failed) return set_error(CUDASP_ERR_HIP, "streaming scan kernel failed earlier in this query");
   const uint32_t b = st->next;
   const uint32_t e = b % STREAM_RING;
   if (b >= STREAM_RING && !stream_seq_done(st, (uint64_t)b - STREAM_RING))
     return set_error(CUDASP_ERR_CAPACITY, "more than %u streamed batches in flight", STREAM_RING);
   StreamBatch& d = st->ctrl->desc[e];
-  d.rows = rows;
-  d.outputs = outputs;
-  d.offs = offs;
-  d.lens = lens;
-  d.flags = flags;
-  d.mirror = d_mirror;
+  d.rows = bt->tweak_keys;
+  d.outputs = bt->outputs;
+  d.offs = bt->output_offsets;
+  d.lens = bt->output_lengths;
+  d.flags = bt->match_flags;
+  d.matches = bt->match_rows;
+  d.mirror = bt->d_mirror;
   d.n = n;
   d.nwr = (n + 63u) / 64u;
   d.first_wr = st->published_wr;
@@ -2496,9 +2895,33 @@ int cudasp_stream_publish(cudasp_stream* st, const uint8_t* rows, const int64_t*
   __atomic_store_n(&st->ctrl->published, b + 1, __ATOMIC_RELEASE);
   st->next = b + 1;
   if (seq) *seq = b;
+  ST_HOST(101, n, b);
   // the query's kernel: launched at its first batch, relaunched if it left
   // idle (its poller picks the batch up from the control block either way)
   return stream_ensure_running(st);
+}
+
+int cudasp_stream_publish(cudasp_stream* st, const uint8_t* rows, const int64_t* outputs, const uint32_t* offs,
+                          const uint32_t* lens, uint32_t n, uint8_t* flags, int64_t* d_mirror, uint64_t* seq) {
+  cudasp_stream_batch b{};
+  b.tweak_keys = rows;
+  b.outputs = outputs;
+  b.output_offsets = offs;
+  b.output_lengths = lens;
+  b.n = n;
+  b.match_flags = flags;
+  b.match_rows = nullptr;
+  b.d_mirror = d_mirror;
+  if (!flags) return set_error(CUDASP_ERR_INVALID_ARG, "null flags buffer");
+  return cudasp_stream_publish_batch(st, &b, seq);
+}
+
+int cudasp_stream_close(cudasp_stream* st) {
+  if (!st) return set_error(CUDASP_ERR_INVALID_ARG, "null stream");
+  std::lock_guard<std::mutex> lk(st->mu);
+  __atomic_store_n(&st->ctrl->closed, 1u, __ATOMIC_RELEASE);
+  ST_HOST(103, 0, 0);
+  return CUDASP_OK;
 }
 
 int cudasp_stream_query(cudasp_stream* st, uint64_t seq) {
@@ -2514,50 +2937,162 @@ int cudasp_stream_query(cudasp_stream* st, uint64_t seq) {
   return stream_seq_done(st, seq) ? 1 : 0;
 }
 
+// Spin (yield) for the first 2 ms, then sleep in short steps: a batch's
+// completion is noticed within microseconds while it is close (the end of a
+// query waits for its last batches), and a long wait costs no core.  Fails
+// after timeout_ms without progress (no batch of the stream completed).
 int cudasp_stream_wait(cudasp_stream* st, uint64_t seq) {
-  for (uint32_t i = 0;; i++) {
+  if (!st) return set_error(CUDASP_ERR_INVALID_ARG, "null stream");
+  const auto t0 = std::chrono::steady_clock::now();
+  auto t_prog = t0, t_check = t0;
+  uint64_t prog = stream_progress(st);
+  for (;;) {
     const int q = cudasp_stream_query(st, seq);
     if (q != 0) return q < 0 ? q : CUDASP_OK;
-    if (i < 64)
+    const auto now = std::chrono::steady_clock::now();
+    if (now - t_check > std::chrono::microseconds(100)) {
+      t_check = now;
+      const uint64_t p = stream_progress(st);
+      if (p != prog) {
+        prog = p;
+        t_prog = now;
+      } else if (now - t_prog > std::chrono::milliseconds(st->timeout_ms)) {
+        std::lock_guard<std::mutex> lk(st->mu);
+        st->failed = true;
+        return set_error(CUDASP_ERR_HIP,
+                         "streaming scan: batch %llu not done after %u ms without progress (batches published %u, "
+                         "kernel launches %llu, running %d)",
+                         (unsigned long long)seq, st->timeout_ms, st->next, (unsigned long long)st->launches,
+                         (int)st->running);
+      }
+    }
+    if (now - t0 < std::chrono::milliseconds(2))
       std::this_thread::yield();
     else
-      std::this_thread::sleep_for(std::chrono::microseconds(i < 256 ? 5 : 20));
+      std::this_thread::sleep_for(std::chrono::microseconds(10));
   }
 }
 
+int cudasp_stream_set_timeout(cudasp_stream* st, uint32_t ms) {
+  if (!st || ms == 0) return set_error(CUDASP_ERR_INVALID_ARG, "null stream or zero timeout");
+  std::lock_guard<std::mutex> lk(st->mu);
+  st->timeout_ms = ms;
+  return CUDASP_OK;
+}
+
+int cudasp_stream_matches(cudasp_stream* st, uint64_t seq, uint32_t* count) {
+  if (!st || !count) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  if (seq >= st->next || st->next - seq > STREAM_RING || !stream_seq_done(st, seq))
+    return set_error(CUDASP_ERR_INVALID_ARG, "batch %llu is not a done batch of the last %u", (unsigned long long)seq,
+                     STREAM_RING);
+  *count = __atomic_load_n(&st->ctrl->nmatch[seq % STREAM_RING], __ATOMIC_ACQUIRE);
+  return CUDASP_OK;
+}
+
+#if CUDASP_STREAM_TRACE
+// Caller holds st->mu, the query's kernels have ended: append the query's
+// events to $CUDASP_STREAM_TRACE_FILE (u32 count, then the events) and reset.
+static void stream_trace_dump(cudasp_stream* st) {
+  uint32_t n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_st_n), sizeof(n)) != hipSuccess) return;
+  if (n > STREAM_TRACE_CAP) n = STREAM_TRACE_CAP;
+  std::vector<StreamTraceEv> ev(n);
+  if (n && hipMemcpyFromSymbol(ev.data(), HIP_SYMBOL(g_st_ev), n * sizeof(StreamTraceEv)) != hipSuccess) return;
+  const uint32_t zero = 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_st_n), &zero, sizeof(zero));
+  {
+    std::lock_guard<std::mutex> lk(g_st_host_mu);
+    ev.insert(ev.end(), g_st_host.begin(), g_st_host.end());
+    g_st_host.clear();
+  }
+  n = (uint32_t)ev.size();
+  const char* path = getenv("CUDASP_STREAM_TRACE_FILE");
+  if (!path || !n) return;
+  if (FILE* f = fopen(path, "ab")) {
+    fwrite(&n, sizeof(n), 1, f);
+    fwrite(ev.data(), sizeof(StreamTraceEv), n, f);
+    fclose(f);
+  }
+  (void)st;
+}
+#endif
+
 int cudasp_stream_finish(cudasp_stream* st) {
   if (!st) return set_error(CUDASP_ERR_INVALID_ARG, "null stream");
+  if (st->abandoned) return set_error(CUDASP_ERR_HIP, "streaming scan abandoned after a timeout");
   int rc = CUDASP_OK;
   {
     std::lock_guard<std::mutex> lk(st->mu);
-    __atomic_store_n(&st->ctrl->closed, 1u, __ATOMIC_RELEASE);
+    if (!st->ctrl->closed) {
+      __atomic_store_n(&st->ctrl->closed, 1u, __ATOMIC_RELEASE);
+      ST_HOST(103, 0, 0);
+    }
   }
+  const bool had_failed = st->failed;
   if (st->next > 0) rc = cudasp_stream_wait(st, (uint64_t)st->next - 1);
   for (uint64_t b = st->next > STREAM_RING ? st->next - STREAM_RING : 0; rc == CUDASP_OK && b < st->next; b++)
     rc = cudasp_stream_wait(st, b);
+  if (had_failed && rc != CUDASP_OK) {
+    // a wait of this query timed out: the batches may still complete (a
+    // slow kernel), so give them the deadline once more from here
+    st->failed = false;
+    rc = CUDASP_OK;
+    for (uint64_t b = st->next > STREAM_RING ? st->next - STREAM_RING : 0; rc == CUDASP_OK && b < st->next; b++)
+      rc = cudasp_stream_wait(st, b);
+  }
+  ST_HOST(104, 0, 0);
   std::lock_guard<std::mutex> lk(st->mu);
   DeviceGuard g(st->s->device);
-  if (st->running) {  // its waves leave as soon as they see the closed stream drained (or idle)
-    const hipError_t e = hipEventSynchronize(st->exited);
+  if (st->running) {
+    // its waves leave as soon as they see the closed stream drained (or
+    // idle); bounded like the waits: a kernel that never ends is abandoned
+    // (the caller must then leak everything it may still touch)
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t e;
+    while ((e = hipEventQuery(st->exited)) == hipErrorNotReady) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(st->timeout_ms)) {
+        st->abandoned = true;
+        return set_error(CUDASP_ERR_HIP, "streaming scan kernel still running %u ms after the stream was closed",
+                         st->timeout_ms);
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
     st->running = false;
     if (e != hipSuccess && rc == CUDASP_OK)
       rc = set_error(CUDASP_ERR_HIP, "streaming scan kernel failed: %s", hipGetErrorString(e));
   }
+  ST_HOST(105, 0, 0);
+  if (rc != CUDASP_OK && !st->running && st->next > 0) {
+    // the kernel has ended without finishing every batch (it failed): the
+    // query's error stands; the stream is reset below for the next query
+  }
   st->failed = false;
   st->next_launch_resets = false;
-  // the query's counters (read here: while the kernel runs it holds every
-  // wave slot, and a device-to-host copy could wait for it), then ready for
-  // the next query
+  // Ready for the next query: the control block here, the device state and
+  // the counters' copy queued on the scanner's stream (ordered before its
+  // next launch; cudasp_stream_counters waits for the copy).
   const bool ran = st->next > 0;
   memset(st->ctrl, 0, sizeof(StreamCtrl));
   st->next = 0;
   st->published_wr = 0;
-  if ((ran && hipMemcpyAsync(st->last_stat, st->dev->stat, sizeof(st->last_stat), hipMemcpyDeviceToHost,
-                             st->s->stream) != hipSuccess) ||
-      hipMemsetAsync(st->dev, 0, sizeof(StreamDev), st->s->stream) != hipSuccess ||
-      hipStreamSynchronize(st->s->stream) != hipSuccess) {
-    if (rc == CUDASP_OK) rc = set_error(CUDASP_ERR_HIP, "streaming scan: state reset failed");
+  const uint64_t waves = st->blocks * (BLOCK / 64);
+  const size_t wbytes = (size_t)waves * STREAM_WSTAT * sizeof(unsigned long long);
+  if (ran) {
+    if (hipMemcpyAsync(st->h_counts, st->dev->stat, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                       st->s->stream) != hipSuccess ||
+        hipMemcpyAsync(st->h_counts + 16, st->wstat, wbytes, hipMemcpyDeviceToHost, st->s->stream) != hipSuccess ||
+        hipMemsetAsync(st->wstat, 0, wbytes, st->s->stream) != hipSuccess) {
+      if (rc == CUDASP_OK) rc = set_error(CUDASP_ERR_HIP, "streaming scan: counters copy failed");
+    }
+    st->counts_pending = true;
+    st->counts_waves = waves;
   }
+  if (hipMemsetAsync(st->dev, 0, sizeof(StreamDev), st->s->stream) != hipSuccess && rc == CUDASP_OK)
+    rc = set_error(CUDASP_ERR_HIP, "streaming scan: state reset failed");
+  ST_HOST(106, 0, 0);
+#if CUDASP_STREAM_TRACE
+  stream_trace_dump(st);
+#endif
   return rc;
 }
 
@@ -2571,18 +3106,41 @@ int cudasp_stream_stats(const cudasp_stream* st, uint64_t* launches, uint32_t* b
 int cudasp_stream_counters(cudasp_stream* st, uint64_t* out, uint32_t count) {
   if (!st || !out) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
   std::lock_guard<std::mutex> lk(st->mu);
+  if (st->counts_pending) {
+    DeviceGuard g(st->s->device);
+    HIP_TRY(hipStreamSynchronize(st->s->stream));
+    for (int i = 0; i < 16; i++) st->last_stat[i] = st->h_counts[i];
+    // per-wave counters: pieces, wave-rows, polls, drains, (0), exits, busy, life
+    static const int map[STREAM_WSTAT] = {STREAM_STAT_PIECES,       STREAM_STAT_WAVE_ROWS, STREAM_STAT_WAIT_POLLS,
+                                          STREAM_STAT_DRAINS,       STREAM_STAT_RESERVED,  STREAM_STAT_WORKER_EXITS,
+                                          STREAM_STAT_BUSY_TICKS,   STREAM_STAT_LIFE_TICKS};
+    const unsigned long long* w = st->h_counts + 16;
+    for (uint64_t v = 0; v < st->counts_waves; v++)
+      for (uint32_t i = 0; i < STREAM_WSTAT; i++) st->last_stat[map[i]] += w[v * STREAM_WSTAT + i];
+    st->counts_pending = false;
+  }
   for (uint32_t i = 0; i < count && i < 16; i++) out[i] = st->last_stat[i];
   return CUDASP_OK;
 }
 
+int cudasp_stream_abandoned(const cudasp_stream* st) { return st && st->abandoned ? 1 : 0; }
+
 void cudasp_stream_destroy(cudasp_stream* st) {
   if (!st) return;
-  if (st->ctrl) {
-    (void)cudasp_stream_finish(st);
-    cudasp_host_free(st->ctrl);
+  if (st->ctrl && !st->abandoned) (void)cudasp_stream_finish(st);
+  if (st->abandoned) {
+    // a kernel may still read the control block and write the device state:
+    // leak them (and the caller leaks the scanner and the batch buffers)
+    fprintf(stderr, "cudasp: a streaming scan kernel did not end; its buffers are leaked\n");
+    delete st;
+    return;
   }
+  if (st->ctrl) cudasp_host_free(st->ctrl);
   DeviceGuard g(st->s->device);
+  if (st->s->stream) (void)hipStreamSynchronize(st->s->stream);
   if (st->dev) (void)hipFree(st->dev);
+  if (st->wstat) (void)hipFree(st->wstat);
+  if (st->h_counts) (void)hipHostFree(st->h_counts);
   if (st->exited) (void)hipEventDestroy(st->exited);
   delete st;
 }

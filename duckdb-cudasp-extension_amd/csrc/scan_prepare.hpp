@@ -9,6 +9,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -147,6 +148,33 @@ inline std::vector<uint32_t> fb_window_bases(int bits = FB_BITS) {
   return bases;
 }
 
+// scan_digits of scan key d through a small process-wide cache: the search
+// over ~290 GLV decompositions costs ~0.3 ms of host time per key, paid at
+// every query's bind otherwise (a wallet's key is scanned query after query).
+inline bool scan_digits_cached(const host::Big<8>& d, std::vector<int8_t>& naf, uint32_t* naf_len) {
+  struct Entry {
+    host::Big<8> d;
+    std::vector<int8_t> naf;
+    uint32_t len;
+  };
+  static std::mutex mu;
+  static std::vector<Entry> cache;  // most recent last, at most 16
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (size_t i = 0; i < cache.size(); i++)
+      if (memcmp(cache[i].d.w, d.w, sizeof(d.w)) == 0) {
+        naf = cache[i].naf;
+        *naf_len = cache[i].len;
+        return true;
+      }
+  }
+  if (host::scan_digits(d, naf.data(), NAF_MAX, naf_len) != 0) return false;
+  std::lock_guard<std::mutex> lk(mu);
+  if (cache.size() >= 16) cache.erase(cache.begin());
+  cache.push_back(Entry{d, naf, *naf_len});
+  return true;
+}
+
 // opt (may be NULL = the reference's semantics): K and full_x go to the
 // constants; with label_negation the label buffer holds L_0..L_(L-1) then
 // -L_0..-L_(L-1) and k.label_count = 2 L.
@@ -168,7 +196,7 @@ inline int prepare_scan(const uint8_t scan_private_key[32], const uint8_t spend_
   }
   naf.assign(2 * NAF_MAX, 0);
   uint32_t naf_len = 0;
-  if (host::scan_digits(d, naf.data(), NAF_MAX, &naf_len) != 0) {
+  if (!scan_digits_cached(d, naf, &naf_len)) {
     err = "GLV split out of range";
     return CUDASP_ERR_INVALID_ARG;
   }

@@ -9,20 +9,27 @@
 // 9.4M / 1M rows).  Here the host publishes each closed slot into a
 // descriptor ring in coherent pinned host memory and the kernel's waves take
 // 64-row wave-rows from it as they are published:
-//   * inputs are read straight from the pinned slot (zero copy over PCIe:
-//     the 64-byte row blob, offset, length and outputs, each once per row --
-//     ~90 B per row at k = 2, 16 GB/s at 177 M rows/s against PCIe Gen5 x16);
-//     a row's outputs are copied to a device mirror at the base compare so the
-//     label compares read HBM, not PCIe;
-//   * flags go straight back into the pinned slot; the wave that completes a
-//     batch (one device counter per ring entry) writes the batch's sequence
-//     number into the ring's done word, which the host polls;
+//   * inputs are read straight from the pinned slot (zero copy over PCIe):
+//     when a wave takes a piece of R wave-rows it first fetches all of them
+//     -- the 64-byte row blobs into its scratch, offsets and lengths, and the
+//     rows' outputs into the batch's device mirror, one cooperative copy per
+//     batch of the piece -- so a piece pays a few PCIe latencies, not several
+//     per row, and nothing after the prefetch reads host memory;
+//   * results go straight back into the pinned slot: the matching rows'
+//     indices (ballot compaction, one atomic per wave-row with a match) and/or
+//     one flag per row; the wave that completes a batch (one device counter
+//     per ring entry) writes the batch's match count and then, behind a
+//     system-scope release, its sequence number into the ring's done word,
+//     which the host polls;
 //   * one poller wave per kernel reads the host's control block over PCIe
 //     (published count, descriptors, closed) and mirrors it into device
 //     memory; the worker waves take tickets of R wave-rows from one device
 //     counter (one atomicAdd while published rows are unclaimed: concurrent
 //     claims may pass the published rows, and such a ticket waits for the
-//     next batch) and look each wave-row's batch up in the mirror;
+//     next batch) and look each wave-row's batch up in the mirror once, at
+//     the prefetch (the piece's pointers then live in LDS);
+//   * output_count K > 1 (K <= MULTI_RMAX): K hashes and K fixed-base points
+//     per row, K x R <= MULTI_RMAX per piece, the row's flag the OR;
 //   * the kernel is elastic: every wave leaves once the stream is closed and
 //     drained, or once the poller has seen nothing to do for idle_ticks
 //     (CUDASP_STREAM_IDLE_MS, 100 MHz wall clock; every published row
@@ -32,10 +39,10 @@
 //     that stalls (a slow source, or executor threads busy elsewhere) never
 //     holds the GPU, and a host that never closes leaves no kernel spinning.
 // Pieces and the pipelined schedule are k_scan_multi's (one inversion per
-// piece); a piece never spans two batches.  This header holds the data
-// structures and the pure scheduling rules (host + device;
-// tests/test_stream_rules_cpu.py replays them and the ring lookup); the
-// kernel is in scan_kernels.hip.
+// piece).  A ticket may span two batches: every wave-row is looked up on its
+// own.  This header holds the data structures and the pure scheduling rules
+// (host + device; tests/test_stream_rules_cpu.py replays them and the ring
+// lookup); the kernel is in scan_kernels.hip.
 #pragma once
 #include <stdint.h>
 
@@ -55,8 +62,9 @@ struct StreamBatch {
   const int64_t* outputs;   // outputs CSR values (words: 1 per output, 4 with full_x)
   const uint32_t* offs;     // n, in outputs
   const uint32_t* lens;     // n
-  uint8_t* flags;           // n, written by the kernel
-  int64_t* mirror;          // device copy of the outputs the label compares read
+  uint8_t* flags;           // n, written by the kernel (or null)
+  uint32_t* matches;        // up to n matching row indices, written by the kernel (or null)
+  int64_t* mirror;          // device copy of the outputs the compares read
   uint32_t n;
   uint32_t nwr;             // wave-rows: ceil(n / 64)
   uint64_t first_wr;        // wave-rows published before this batch
@@ -70,6 +78,7 @@ struct StreamCtrl {
   uint64_t published_wr;            // wave-rows published (host)
   uint32_t reserved;
   uint32_t done[STREAM_RING];       // ring entry e: 1 + sequence number of the last batch completed there (kernel)
+  uint32_t nmatch[STREAM_RING];     // matching rows of that batch (kernel; written before `done`)
   StreamBatch desc[STREAM_RING];    // batch b at entry b % STREAM_RING
 };
 
@@ -85,8 +94,11 @@ struct StreamDev {
   uint32_t idle;                    // the poller left idle: the workers leave as they drain
                                     // (reset by the host before it relaunches the kernel)
   uint32_t wr_done[STREAM_RING];    // wave-rows finished of the batch at each entry
+  uint32_t nmatch[STREAM_RING];     // matching rows found so far of the batch at each entry
   StreamBatch desc[STREAM_RING];    // mirror of StreamCtrl::desc
-  // counters (cudasp_stream_counters): STREAM_STAT_* below
+  // the poller's counters (cudasp_stream_counters: STREAM_STAT_* below; the
+  // workers' go to a per-wave array, summed on the host: a same-address
+  // atomic per wave and counter serialized ~20k atomics at the kernel's exit)
   unsigned long long stat[16];
 };
 
@@ -130,5 +142,21 @@ struct StreamWave {
   uint64_t tk, t_start, busy;  // tk: the ticket, wave-rows [tk, tk + tr)
   uint32_t tr, have, mine, pieces, rows, polls, drains;
 };
+
+// Where a wave-row of a piece lives, looked up once at the piece's prefetch
+// and kept in LDS by the wave (wave-uniform): its batch's device mirror and
+// result buffers, its first row in the batch, the batch's rows, wave-rows
+// and sequence number.  Valid while the wave holds the wave-row: the batch
+// cannot complete (nor its ring entry or slot be reused) before it is done.
+struct StreamWr {
+  int64_t* mirror;
+  uint8_t* flags;
+  uint32_t* matches;
+  uint32_t r0, n, nwr, b;
+};
+
+// Worker counters per wave (StreamDev::stat indices), flushed once at exit
+// into the stream's per-wave array: STREAM_WSTAT words per wave.
+constexpr uint32_t STREAM_WSTAT = 8;
 
 }  // namespace cudasp

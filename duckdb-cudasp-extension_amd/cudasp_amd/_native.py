@@ -49,11 +49,17 @@ SIGNATURES = {
     "cudasp_synth_output_values": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _U32, _P, _P, _P, _P]),
     "cudasp_host_alloc": (_I32, [ctypes.POINTER(_P), ctypes.c_size_t]),
     "cudasp_host_free": (None, [_P]),
+    "cudasp_stream_supported": (_I32, [_P]),
     "cudasp_stream_create": (_I32, [_P, _U32, ctypes.POINTER(_P)]),
     "cudasp_stream_publish": (_I32, [_P, _P, _P, _P, _P, _U32, _P, _P, ctypes.POINTER(ctypes.c_uint64)]),
+    "cudasp_stream_publish_batch": (_I32, [_P, _P, ctypes.POINTER(ctypes.c_uint64)]),
+    "cudasp_stream_close": (_I32, [_P]),
     "cudasp_stream_query": (_I32, [_P, ctypes.c_uint64]),
     "cudasp_stream_wait": (_I32, [_P, ctypes.c_uint64]),
+    "cudasp_stream_set_timeout": (_I32, [_P, _U32]),
+    "cudasp_stream_matches": (_I32, [_P, ctypes.c_uint64, ctypes.POINTER(_U32)]),
     "cudasp_stream_finish": (_I32, [_P]),
+    "cudasp_stream_abandoned": (_I32, [_P]),
     "cudasp_stream_stats": (_I32, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_U32)]),
     "cudasp_stream_counters": (_I32, [_P, ctypes.POINTER(ctypes.c_uint64), _U32]),
     "cudasp_stream_destroy": (None, [_P]),
@@ -111,6 +117,12 @@ class DeviceBatch(ctypes.Structure):
     _fields_ = [("tweak_x", _P), ("tweak_y", _P), ("outputs", _P), ("output_offsets", _P),
                 ("output_lengths", _P), ("n", _U32), ("match_flags", _P), ("match_rows", _P),
                 ("match_count", _P)]
+
+
+class StreamBatchDesc(ctypes.Structure):
+    """cudasp_stream_batch (include/cudasp_abi.h)."""
+    _fields_ = [("tweak_keys", _P), ("outputs", _P), ("output_offsets", _P), ("output_lengths", _P),
+                ("n", _U32), ("match_flags", _P), ("match_rows", _P), ("d_mirror", _P)]
 
 
 class ScanOptions(ctypes.Structure):

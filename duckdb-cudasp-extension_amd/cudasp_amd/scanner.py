@@ -247,16 +247,22 @@ class ScanStream:
         _native.check(self._lib.cudasp_stream_create(scanner._h, int(blocks), ctypes.byref(h)))
         self._h = h
 
-    def publish(self, rows, outputs, offsets, lengths, n, flags, mirror=None):
-        """rows / outputs / offsets / lengths / flags: HostBuffers (or their
-        addresses); mirror: a device tensor of the batch's outputs size (with
-        labels).  Returns the batch's sequence number."""
+    def publish(self, rows, outputs, offsets, lengths, n, flags, mirror=None, matches=None):
+        """rows / outputs / offsets / lengths / flags / matches: HostBuffers
+        (or their addresses; flags or matches may be None); mirror: a device
+        tensor of the batch's outputs size.  Returns the batch's sequence
+        number."""
         seq = ctypes.c_uint64()
         addr = lambda b: None if b is None else (b.ptr if isinstance(b, HostBuffer) else int(b))  # noqa: E731
-        _native.check(self._lib.cudasp_stream_publish(
-            self._h, addr(rows), addr(outputs), addr(offsets), addr(lengths), int(n), addr(flags),
-            None if mirror is None else mirror.data_ptr(), ctypes.byref(seq)))
+        d = _native.StreamBatchDesc(addr(rows), addr(outputs), addr(offsets), addr(lengths), int(n), addr(flags),
+                                    addr(matches), None if mirror is None else mirror.data_ptr())
+        _native.check(self._lib.cudasp_stream_publish_batch(self._h, ctypes.byref(d), ctypes.byref(seq)))
         return seq.value
+
+    def close_input(self):
+        """No batch follows (cudasp_stream_close): the kernel ends once the
+        published batches are done."""
+        _native.check(self._lib.cudasp_stream_close(self._h))
 
     def query(self, seq):
         rc = self._lib.cudasp_stream_query(self._h, int(seq))
@@ -266,6 +272,18 @@ class ScanStream:
 
     def wait(self, seq):
         _native.check(self._lib.cudasp_stream_wait(self._h, int(seq)))
+
+    def set_timeout(self, ms):
+        _native.check(self._lib.cudasp_stream_set_timeout(self._h, int(ms)))
+
+    def matches(self, seq):
+        """Matching rows of done batch `seq` (cudasp_stream_matches)."""
+        c = ctypes.c_uint32()
+        _native.check(self._lib.cudasp_stream_matches(self._h, int(seq), ctypes.byref(c)))
+        return c.value
+
+    def abandoned(self):
+        return bool(self._lib.cudasp_stream_abandoned(self._h))
 
     def finish(self):
         _native.check(self._lib.cudasp_stream_finish(self._h))
@@ -304,10 +322,12 @@ class ScanStream:
 
 class StreamBatch:
     """One batch staged in pinned host memory for a ScanStream: the tweak
-    blobs, the outputs CSR (int64 values, or 32-byte keys with full_x) and
-    the flags the kernel writes; plus the device mirror for label scans."""
+    blobs, the outputs CSR (int64 values, or 32-byte keys with full_x), the
+    flags and the match indices the kernel writes, and the device mirror of
+    the outputs the kernel's compares read."""
 
-    def __init__(self, tweak_keys, outputs, offsets, lengths, label_count=0, device=0, full_x=False):
+    def __init__(self, tweak_keys, outputs, offsets, lengths, label_count=0, device=0, full_x=False,
+                 want_flags=True, want_matches=True):
         tk = np.ascontiguousarray(tweak_keys, dtype=np.uint8).reshape(-1, 64)
         self.n = tk.shape[0]
         outs = (np.ascontiguousarray(outputs, dtype=np.uint8).reshape(-1) if full_x
@@ -320,16 +340,29 @@ class StreamBatch:
         self.offsets.view(np.uint32)[:] = np.asarray(offsets, dtype=np.uint32)
         self.lengths = HostBuffer(4 * self.n)
         self.lengths.view(np.uint32)[:] = np.asarray(lengths, dtype=np.uint32)
-        self.flags = HostBuffer(self.n)
-        self.flags.array[:] = 0xEE  # every row must be written
-        self.mirror = None
-        if label_count:
-            import torch
-            self.mirror = torch.empty((max(1, outs.nbytes // 8),), dtype=torch.int64,
-                                      device=torch.device("cuda", device))
+        self.flags = HostBuffer(self.n) if want_flags else None
+        if self.flags is not None:
+            self.flags.array[:] = 0xEE  # every row must be written
+        self.match_rows = HostBuffer(4 * max(1, self.n)) if want_matches else None
+        import torch
+        self.mirror = torch.empty((max(1, outs.nbytes // 8),), dtype=torch.int64, device=torch.device("cuda", device))
+        self.seq = None
 
     def publish(self, stream):
-        return stream.publish(self.rows, self.outputs, self.offsets, self.lengths, self.n, self.flags, self.mirror)
+        self.seq = stream.publish(self.rows, self.outputs, self.offsets, self.lengths, self.n, self.flags,
+                                  self.mirror, self.match_rows)
+        return self.seq
+
+    def reset(self):
+        if self.flags is not None:
+            self.flags.array[:] = 0xEE
+        if self.match_rows is not None:
+            self.match_rows.array[:] = 0xEE
 
     def result(self):
         return self.flags.array.copy()
+
+    def matches(self, stream):
+        """The matching rows (sorted) of this batch once it is done."""
+        c = stream.matches(self.seq)
+        return np.sort(self.match_rows.view(np.uint32)[:c].copy())

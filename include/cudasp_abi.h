@@ -192,48 +192,85 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
  * while the query runs).  ONE persistent kernel per stream scans every batch
  * published into it, reading the batch straight from pinned host memory (the
  * 64-byte tweak blobs as the table holds them, the outputs CSR) and writing
- * its flags back there; the host polls for each batch's completion.  Needs a
- * scanner with the default options (output_count 1) and an HBM fixed-base
- * width (22 or 26 bits); the scanner must not run other launches while a
- * stream on it is open.
+ * its results back there: one flag per row and/or the indices of the
+ * matching rows; the host polls for each batch's completion.  Needs a
+ * scanner with output_count <= 6 and an HBM fixed-base width (22 or 26
+ * bits); the scanner must not run other launches while a stream on it is
+ * open.
  *   cudasp_host_alloc   coherent pinned host memory, device-addressable at
  *                       the same address: every host buffer of a published
- *                       batch must come from it.
+ *                       batch must lie in such an allocation (checked at
+ *                       publish: the kernel's uncached reads and
+ *                       system-scope result stores need coherent memory).
+ *   cudasp_stream_supported  1 when the scanner's current keys and options
+ *                       allow a stream (output_count <= 6, an HBM fixed-base
+ *                       width, a label count whose scratch fits), else 0.
  *   cudasp_stream_create  blocks = 0: the whole device (3 waves per SIMD).
- *   cudasp_stream_publish  a batch of n >= 1 rows; with labels, d_mirror is a
- *                       device buffer as large as the batch's outputs (the
- *                       kernel copies each row's outputs there once).  The
- *                       buffers must stay untouched until the batch is done.
- *                       *seq receives the batch's sequence number.  At most
- *                       64 batches may be published and not yet done
+ *   cudasp_stream_publish_batch  a batch of n >= 1 rows (cudasp_stream_batch):
+ *                       d_mirror is a device buffer as large as the batch's
+ *                       outputs (>= 1 word; the kernel copies each row's
+ *                       outputs there once); match_flags (n bytes) and/or
+ *                       match_rows (room for n indices).  The buffers must
+ *                       stay untouched until the batch is done.  *seq
+ *                       receives the batch's sequence number.  At most 64
+ *                       batches may be published and not yet done
  *                       (CUDASP_ERR_CAPACITY otherwise).  Launches the kernel
  *                       if none is running: a kernel that finds nothing to do
  *                       for CUDASP_STREAM_IDLE_MS (default 20 ms) ends, so a
  *                       stalled host never holds the GPU; publish and wait
  *                       relaunch it.
- *   cudasp_stream_query  1: batch seq done (flags written), 0: not yet, < 0: error.
- *   cudasp_stream_wait   blocks until batch seq is done.
- *   cudasp_stream_finish  end of input: waits for every batch and for the
- *                       kernel, then resets the stream for reuse (sequence
- *                       numbers start again at 0).
+ *   cudasp_stream_publish  the same with match_flags only (no match_rows).
+ *   cudasp_stream_close  no batch follows: the kernel ends as soon as every
+ *                       published batch is done (finish still waits and resets).
+ *   cudasp_stream_query  1: batch seq done (results written), 0: not yet, < 0: error.
+ *   cudasp_stream_wait   blocks until batch seq is done; CUDASP_ERR_HIP when
+ *                       no batch completed for the stream's timeout
+ *                       (cudasp_stream_set_timeout, CUDASP_STREAM_TIMEOUT_MS,
+ *                       default 60000 ms).
+ *   cudasp_stream_matches  matching rows of a done batch (its match_rows
+ *                       entries, in no particular order); valid until 64 more
+ *                       batches are published.
+ *   cudasp_stream_finish  end of input: closes, waits for every batch and for
+ *                       the kernel (bounded by the timeout), then resets the
+ *                       stream for reuse (sequence numbers start again at 0).
+ *   cudasp_stream_abandoned  1 when finish timed out with the kernel still
+ *                       running: nothing the kernel may touch (the stream, its
+ *                       scanner, the batch buffers) may be freed.
  *   cudasp_stream_stats  kernel launches so far and grid blocks.
  *   cudasp_stream_counters  the kernel's counters of the last finished
- *                       query (taken by finish; reading them while the
+ *                       query (queued by finish; reading them while the
  *                       kernel runs could wait for it), summed over its
  *                       launches: pieces, wave-rows, polls with nothing to
  *                       claim, pipeline drains, (unused), worker exits,
  *                       idle exits, poller polls, workers' busy and lifetime
  *                       ticks (100 MHz). */
 typedef struct cudasp_stream cudasp_stream;
+#define CUDASP_STREAM_MAX_OUTPUT_COUNT 6
+typedef struct {
+  const uint8_t* tweak_keys;      /* n x 64 bytes (x then y, little-endian words) */
+  const int64_t* outputs;         /* outputs CSR values (4 words per output with full_x) */
+  const uint32_t* output_offsets; /* n, in outputs */
+  const uint32_t* output_lengths; /* n */
+  uint32_t n;
+  uint8_t* match_flags;           /* n flags, or NULL */
+  uint32_t* match_rows;           /* room for n row indices, or NULL */
+  int64_t* d_mirror;              /* device memory, the batch's outputs words (>= 1) */
+} cudasp_stream_batch;
 int cudasp_host_alloc(void** p, size_t bytes);
 void cudasp_host_free(void* p);
+int cudasp_stream_supported(const cudasp_scanner* s);
 int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out);
+int cudasp_stream_publish_batch(cudasp_stream* st, const cudasp_stream_batch* batch, uint64_t* seq);
 int cudasp_stream_publish(cudasp_stream* st, const uint8_t* h_tweak_keys, const int64_t* h_outputs,
                           const uint32_t* h_output_offsets, const uint32_t* h_output_lengths, uint32_t n,
                           uint8_t* h_match_flags, int64_t* d_mirror, uint64_t* seq);
+int cudasp_stream_close(cudasp_stream* st);
 int cudasp_stream_query(cudasp_stream* st, uint64_t seq);
 int cudasp_stream_wait(cudasp_stream* st, uint64_t seq);
+int cudasp_stream_set_timeout(cudasp_stream* st, uint32_t ms);
+int cudasp_stream_matches(cudasp_stream* st, uint64_t seq, uint32_t* count);
 int cudasp_stream_finish(cudasp_stream* st);
+int cudasp_stream_abandoned(const cudasp_stream* st);
 int cudasp_stream_stats(const cudasp_stream* st, uint64_t* launches, uint32_t* blocks);
 int cudasp_stream_counters(cudasp_stream* st, uint64_t* out, uint32_t count);
 void cudasp_stream_destroy(cudasp_stream* st);

@@ -70,9 +70,9 @@ def _check_rows(out, rows):
 @pytest.mark.parametrize("threads,batch", [(3, 2500), (8, 4000), (5, 300000)])
 def test_host_feed_16_labels_rows(table16, keys, threads, batch):  # noqa: F811
     """Row chunks: several threads, batch sizes giving ~10 launches with the
-    ring wrapping (2500 rows: two 2048-row chunks per slot, 3 streams, 5
-    slots), and one batch larger than the table (everything in the final
-    partial slot)."""
+    ring wrapping (2500 rows: two 2048-row chunks per slot), and one batch
+    larger than the table (the ramp's first slot, then the final partial
+    slot)."""
     from cudasp_amd import cudasp_scan, release_pool
     rows, expected = table16
     scan, spend, labels = keys
@@ -85,7 +85,9 @@ def test_host_feed_16_labels_rows(table16, keys, threads, batch):  # noqa: F811
     if batch < len(rows):
         assert stats["launches"] >= 3
     else:
-        assert stats["launches"] == 1
+        # the streaming feed's ramp (batch_size / 32, / 16, ...) closes its
+        # first slots early: 9375 rows, then the final partial slot
+        assert stats["launches"] <= 2
     assert stats["streams_per_feed"] < stats["hw_queues"]  # one queue is the null stream's
     release_pool()
 
@@ -216,11 +218,13 @@ def test_host_streaming_feed_16_labels(table16, keys, threads, batch, monkeypatc
 
 
 def test_host_concurrent_queries_one_gpu(table16, keys):  # noqa: F811
-    """Two queries at once on one GPU, each with its own executor threads
-    (two DuckDB connections in one process): each query's streaming feed
-    runs its own kernel, and a kernel holds the GPU only while its query has
-    work (it leaves after CUDASP_STREAM_IDLE_MS idle) -- both queries finish
-    with the oracle's rows, with different batch sizes and label sets."""
+    """Two queries at once on one GPU over the same table and keys, each
+    with its own executor threads and batch size (two DuckDB connections in
+    one process): each query's streaming feed runs its own kernel, and a
+    kernel holds the GPU only while its query has work (it leaves after
+    CUDASP_STREAM_IDLE_MS idle) -- both finish with the oracle's rows.
+    Different keys, label sets and input paths at once:
+    test_host_stream_gpu.py::test_host_concurrent_queries_different_keys."""
     import threading
     from cudasp_amd import cudasp_scan, release_pool
     rows, expected = table16

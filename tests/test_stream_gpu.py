@@ -42,21 +42,26 @@ def staged(b, label_count):
 def run_stream(batches, labels, rounds=1, max_in_flight=None):
     """Publish every batch into one stream (`rounds` queries on the same
     stream), waiting for the oldest when max_in_flight are out; returns the
-    last round's flags per batch and the stream's stats."""
+    last round's flags per batch and the stream's stats.  Every batch's
+    compacted matches (match_rows, cudasp_stream_matches) are its flagged
+    rows."""
     from cudasp_amd import Scanner, ScanStream
     stage = [staged(b, len(labels)) for b in batches]
     with Scanner(SCAN, SPEND, labels, max_rows=1000) as s, ScanStream(s) as st:
         for _ in range(rounds):
             for sb in stage:
-                sb.flags.array[:] = 0xEE
+                sb.reset()
             seqs = []
             for sb in stage:
                 if max_in_flight and len(seqs) >= max_in_flight:
                     st.wait(seqs[-max_in_flight])
                 seqs.append(sb.publish(st))
+            st.close_input()
             for q in seqs:
                 st.wait(q)
             assert all(st.query(q) for q in seqs)
+            for sb in stage[-64:]:  # match counts of the last 64 batches stay readable
+                assert (sb.matches(st) == np.nonzero(sb.result())[0]).all()
             st.finish()
         stats = st.stats()
     return [sb.result() for sb in stage], stats
@@ -206,17 +211,113 @@ def test_stream_exceptional_label_sums(torch):
 
 
 def test_stream_rejects_bad_use(torch):
-    from cudasp_amd import CudaspError, Scanner, ScanStream, StreamBatch
+    from cudasp_amd import CudaspError, HostBuffer, Scanner, ScanStream, StreamBatch
     b = tm.make_batch(torch, 1, 100)
     with Scanner(SCAN, SPEND, [LABEL], max_rows=100) as s:
         with ScanStream(s) as st:
-            sb = staged(b, 0)  # no mirror with a label scanner
-            with pytest.raises(CudaspError):
+            sb = staged(b, 1)
+            with pytest.raises(CudaspError):  # no outputs mirror
                 st.publish(sb.rows, sb.outputs, sb.offsets, sb.lengths, sb.n, sb.flags, None)
+            with pytest.raises(CudaspError):  # empty batch
+                st.publish(sb.rows, sb.outputs, sb.offsets, sb.lengths, 0, sb.flags, sb.mirror)
+            with pytest.raises(CudaspError):  # neither flags nor match rows
+                st.publish(sb.rows, sb.outputs, sb.offsets, sb.lengths, sb.n, None, sb.mirror)
+            # host buffers outside cudasp_host_alloc (pageable memory): refused,
+            # the kernel's uncached reads and system-scope stores need coherent memory
+            pageable = np.zeros(100 * 64, dtype=np.uint8)
             with pytest.raises(CudaspError):
-                st.publish(sb.rows, sb.outputs, sb.offsets, sb.lengths, 0, sb.flags, None)
-        s.set_options(output_count=2)
+                st.publish(pageable.ctypes.data, sb.outputs, sb.offsets, sb.lengths, sb.n, sb.flags, sb.mirror)
+            part = HostBuffer(64 * 50)  # coherent, but smaller than the batch
+            with pytest.raises(CudaspError):
+                st.publish(part, sb.outputs, sb.offsets, sb.lengths, sb.n, sb.flags, sb.mirror)
+            part.close()
+            # still usable after the refusals
+            q = sb.publish(st)
+            st.wait(q)
+            st.finish()
+        s.set_options(output_count=7)  # K x rows of a piece must fit the kernel's pending slots
         with pytest.raises(CudaspError):
             ScanStream(s)
     assert StreamBatch is not None
 
+
+def _variant_case(torch, n, K, neg, full_x, labels, first):
+    """n synthetic rows with a decoy and, on 4 of 5 rows, one planted
+    candidate chosen round-robin over every (output index, value column)
+    of the variant (test_variants_gpu's construction); the oracle's flags."""
+    from oracle import oracle
+    from test_variants_gpu import _outputs
+    b = tm.make_batch(torch, first, n)
+    tw = host_rows(b)
+    rows = [{"tweak": bytes(tw[i]).hex()} for i in range(n)]
+    outs, offs, lens = _outputs(SCAN, SPEND, labels, rows, K, neg, full_x)
+    want, _ = oracle.scan_ex(SCAN, SPEND, labels, tw, outs, offs, lens, output_count=K, label_negation=neg,
+                             full_x=full_x, threads=16)
+    return tw, outs, offs, lens, want
+
+
+@pytest.mark.parametrize("K,neg,full_x", [(2, True, False), (2, False, False), (3, False, True), (6, True, False)])
+def test_stream_variants(torch, K, neg, full_x):
+    """output_count K > 1 (K hashes and fixed-base points per row, K x rows
+    per piece <= 6), label negation and full-x compares through the
+    streaming kernel: flags and compacted matches equal the C oracle's
+    scan_ex over ragged batches in one stream (the reference has none of the
+    variants: parity unpinned against it, pinned to tests/variants.py)."""
+    from cudasp_amd import Scanner, ScanStream, StreamBatch
+    labels = [LABEL]
+    n = 700 if full_x else 2200
+    tw, outs, offs, lens, want = _variant_case(torch, n, K, neg, full_x, labels, 4242 + K)
+    assert 0 < int(want.sum()) < n
+    cuts = [0, 1, 65, n // 2, n]
+    ow = 32 if full_x else 1
+    stage = []
+    for a, z in zip(cuts[:-1], cuts[1:]):
+        o0 = int(offs[a])
+        o1 = int(offs[z - 1] + lens[z - 1])
+        sub = outs[o0:o1]
+        stage.append(StreamBatch(tw[a:z], sub, offs[a:z] - o0, lens[a:z], label_count=1, full_x=full_x,
+                                 want_flags=(K != 3)))
+    del ow
+    with Scanner(SCAN, SPEND, labels, max_rows=1000) as s:
+        s.set_options(output_count=K, label_negation=neg, full_x=full_x)
+        with ScanStream(s) as st:
+            seqs = [sb.publish(st) for sb in stage]
+            st.close_input()
+            for q in seqs:
+                st.wait(q)
+            got_rows = np.concatenate([sb.matches(st) + a for sb, a in zip(stage, cuts[:-1])])
+            if K != 3:
+                got_flags = np.concatenate([sb.result() for sb in stage])
+                assert (got_flags == want).all()
+            st.finish()
+    assert (got_rows == np.nonzero(want)[0]).all()
+
+
+def test_stream_timeout_then_recovers(torch):
+    """A wait that sees no batch complete for the stream's timeout fails with
+    an error instead of hanging (cudasp_stream_set_timeout; a 2.4M-row batch
+    takes > 10 ms); finish with the normal timeout then lets the batch
+    complete and resets the stream, and the next query on it returns the
+    per-batch path's flags."""
+    from cudasp_amd import CudaspError, Scanner, ScanStream
+    b = tm.make_batch(torch, 777, 2_400_000)
+    tm.plant(torch, [b], [], every=100_003)
+    sb = staged(b, 0)
+    with Scanner(SCAN, SPEND, [], max_rows=1000) as s, ScanStream(s) as st:
+        st.set_timeout(1)
+        q = sb.publish(st)
+        with pytest.raises(CudaspError) as e:
+            st.wait(q)
+        assert "without progress" in str(e.value)
+        st.set_timeout(60000)
+        st.finish()
+        assert not st.abandoned()
+        first = sb.result()
+        sb.reset()
+        q = sb.publish(st)
+        st.wait(q)
+        st.finish()
+        again = sb.result()
+    want = tm.run_per_batch(torch, [b], [])
+    assert (again == want[0][0]).all()
+    assert (first == want[0][0]).all()  # the timed-out wait's batch completed all the same
