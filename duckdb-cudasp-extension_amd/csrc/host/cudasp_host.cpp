@@ -70,7 +70,20 @@ constexpr int FEED_MAX_STREAMS = 4;
 // tx/s with 8 slots in flight, 164.0 with 16, 166.6 with all published;
 // profiles/r03_stream_iter2.txt).
 constexpr int FEED_STREAM_SLOTS = 16;
-constexpr int FEED_MAX_SLOTS = FEED_STREAM_SLOTS > FEED_MAX_STREAMS + 2 ? FEED_STREAM_SLOTS : FEED_MAX_STREAMS + 2;
+// CUDASP_TF_STREAM_SLOTS overrides it, up to 48 (well inside the stream's
+// 64-entry descriptor ring: a done slot is harvested long before its ring
+// entry can be reused).
+constexpr int FEED_MAX_STREAM_SLOTS = 48;
+constexpr int FEED_MAX_SLOTS = FEED_MAX_STREAM_SLOTS;
+static_assert(FEED_MAX_SLOTS >= FEED_MAX_STREAMS + 2, "per-slot launch feeds");
+
+int feed_stream_slots() {
+  if (const char* e = getenv("CUDASP_TF_STREAM_SLOTS")) {
+    const int v = atoi(e);
+    if (v >= 4 && v <= FEED_MAX_STREAM_SLOTS) return v;
+  }
+  return FEED_STREAM_SLOTS;
+}
 // Rows resident on the GPU at once in k_scan_multi launches of 4 rows per
 // thread: 256 CUs x 4 SIMDs x 3 waves x 64 lanes x 4 rows.
 constexpr uint64_t GPU_FILL_ROWS = 786432;
@@ -217,8 +230,9 @@ struct FeedRes {
   // device or pinned memory waits for the device, hence for that kernel).
   cudasp_stream* stream = nullptr;
   uint32_t stream_blocks = 0;
+  int stream_slots = FEED_STREAM_SLOTS;  // slots of a streaming feed (feed_stream_slots at creation)
   std::vector<void*> stale_host, stale_dev;
-  int nslots() const { return stream ? FEED_STREAM_SLOTS : nstreams + 2; }
+  int nslots() const { return stream ? stream_slots : nstreams + 2; }
 };
 
 void free_stale(FeedRes& r) {
@@ -664,6 +678,17 @@ uint64_t close_at(const Feed& f) {
   return r < CUDASP_TF_VECTOR_SIZE ? std::min<uint64_t>(f.batch_size, CUDASP_TF_VECTOR_SIZE) : r;
 }
 
+// The streaming feeds' wait timeout (cudasp_stream_set_timeout): a wait
+// that sees no batch complete for this long fails the query instead of
+// hanging it.  CUDASP_STREAM_TIMEOUT_MS, read per query; 60 s by default.
+uint32_t stream_timeout_ms() {
+  if (const char* e = getenv("CUDASP_STREAM_TIMEOUT_MS")) {
+    const long v = atol(e);
+    if (v >= 1 && v <= 86400000) return (uint32_t)v;
+  }
+  return 60000u;
+}
+
 // Whether a launched slot's batch is done (no waiting).
 bool slot_done(Feed& f, FeedSlot& s) {
   if (f.res->stream) return cudasp_stream_query(f.res->stream, s.seq) == 1;
@@ -777,17 +802,23 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
         continue;
       }
       case SLOT_LAUNCHED: {
-        // the open slot's batch may still be in flight: take a ready slot
-        // if there is one; else poll for one for a while (any batch that
-        // completes frees a slot), then wait for this one
+        // the open slot's batch may still be in flight: open a ready slot
+        // (free, or its batch done) instead; with none, poll for one -- any
+        // batch that completes frees a slot -- and block on this slot's
+        // batch (under the stream's no-progress deadline) only after
+        // nothing has become ready for that long.  Blocking on the open
+        // slot at once stalled the ring behind one slow batch: 18 ms
+        // without a publish at 9.4M rows (tools/stream_trace.py, round 4).
         if (!slot_done(f, s)) {
           const int open0 = f.open;
+          const double t0 = now_s(), limit = 1e-3 * stream_timeout_ms();
           int k = ready_slot_locked(f);
-          for (int spin = 0; k < 0 && spin < 100; spin++) {
+          while (k < 0) {
             f.cv.wait_for(lk, std::chrono::microseconds(20));
             if (f.error != CUDASP_OK) return feed_error(f);
             if (f.open != open0 || s.state != SLOT_LAUNCHED || slot_done(f, s)) break;
             k = ready_slot_locked(f);
+            if (now_s() - t0 > limit) break;
           }
           if (f.open != open0 || s.state != SLOT_LAUNCHED) continue;  // another thread moved on
           if (k >= 0) {
@@ -868,17 +899,6 @@ int feeds_flush(cudasp_tf_global& g) {
   return rc;
 }
 
-// The streaming feeds' wait timeout (cudasp_stream_set_timeout): a wait
-// that sees no batch complete for this long fails the query instead of
-// hanging it.  CUDASP_STREAM_TIMEOUT_MS, read per query; 60 s by default.
-uint32_t stream_timeout_ms() {
-  if (const char* e = getenv("CUDASP_STREAM_TIMEOUT_MS")) {
-    const long v = atol(e);
-    if (v >= 1 && v <= 86400000) return (uint32_t)v;
-  }
-  return 60000u;
-}
-
 // The feed of logical GPU `lg`, created on first use: pooled resources for
 // (device, capacity, streams), or new scanners, rebound to this query's keys.
 int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** out) {
@@ -945,6 +965,7 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
         rc = cudasp_stream_create(r->scanners[0], blocks, &r->stream);
         if (rc == CUDASP_OK) {
           r->stream_blocks = blocks;
+          r->stream_slots = feed_stream_slots();
         } else if (rc == CUDASP_ERR_INVALID_ARG) {  // a width the streaming kernel lacks: per-slot launches
           r->stream = nullptr;
           r->nstreams = g.launch_streams;
@@ -1440,8 +1461,12 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
     // queue (HIP shares queues among streams) and the second would wait for
     // the first to end -- logical GPUs sharing a device (CUDASP_TF_DEVICE_MAP)
     // take the per-slot launches
+    // (CUDASP_TF_MODE=stream forces streaming feeds even then -- each
+    // kernel gets its share of the device's wave slots -- for rehearsing
+    // the N-GPU host on one card with GPU_MAX_HW_QUEUES above the feeds)
+    const bool force = mode && !strcmp(mode, "stream");
     g->streaming = !(mode && !strcmp(mode, "launch")) && b->opt.output_count <= CUDASP_STREAM_MAX_OUTPUT_COUNT &&
-                   feeds_per_device == 1;
+                   (feeds_per_device == 1 || force);
     if (g->streaming) g->feed_streams = 1;
   }
   g->feeds.resize(g->num_gpus);

@@ -1058,6 +1058,32 @@ __device__ __forceinline__ void stream_emit(StreamCtrl* ctrl, StreamDev* dev, co
   }
 }
 
+// The ladder hook of k_scan_stream: the wave's issue priority by the age of
+// its oldest unfinished piece (stream_prio), refreshed every 16 ladder steps
+// so that a starved wave rises while it is still in its ladder.
+struct StreamTick {
+  volatile StreamWave* me;
+  uint64_t step;
+  __device__ __forceinline__ void operator()() const {
+    if (step == 0) return;
+    const uint64_t t_old = uniform_u64(me->t_old);
+    switch (stream_prio(wall_clock64() - t_old, step)) {
+      case 0:
+        __builtin_amdgcn_s_setprio(0);
+        break;
+      case 1:
+        __builtin_amdgcn_s_setprio(1);
+        break;
+      case 2:
+        __builtin_amdgcn_s_setprio(2);
+        break;
+      default:
+        __builtin_amdgcn_s_setprio(3);
+        break;
+    }
+  }
+};
+
 // Row bits of a label pass's unit bits (unit u = row u / K, index u % K).
 __device__ __forceinline__ uint32_t stream_unit_rows(uint32_t uh, int K) {
   if (K == 1) return uh;
@@ -1075,7 +1101,8 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
                                                                     const uint32_t* __restrict__ labels,
                                                                     uint32_t* __restrict__ scr, uint32_t rmax,
                                                                     uint64_t idle_ticks,
-                                                                    unsigned long long* __restrict__ wstat) {
+                                                                    unsigned long long* __restrict__ wstat,
+                                                                    uint64_t prio_ticks) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = SCAN_SCRATCH(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1110,7 +1137,9 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
     me.tk = me.tr = me.have = me.mine = 0;
     me.t_start = wall_clock64();
     me.busy = me.pieces = me.rows = me.polls = me.drains = 0;
+    me.t_p = me.t_q = me.t_old = 0;
   }
+  const StreamTick tick{&me, prio_ticks};
 #if CUDASP_STREAM_TRACE
   const uint32_t st_wave = slot / 64u;
   if (lane == 0) {
@@ -1186,7 +1215,10 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
         me.rows = me.rows + (uint32_t)count;
       }
       ST_EV(ST_PIECE, st_wave, base, (uint32_t)count, (uint32_t)count_p | ((uint32_t)count_q << 8));
+      // the oldest piece this wave holds: Q's, else P's, else the new one's
+      me.t_old = count_q ? me.t_q : (count_p ? me.t_p : t_it);
     }
+    tick();
     StreamWr* const wn = wrs[wid][pn];
     const int meta_n = META + 2 * MULTI_RMAX * pn;
     if (count) stream_prefetch(dev, hint, base, count, lane, wn, pfs[wid], sc, STG, meta_n, ow);
@@ -1198,7 +1230,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
 #pragma unroll
       for (int q = 0; q < 16; q++) w[q] = scr_load_w(sc, STG + 16 * j + q);
       gej P;
-      row_shared_secret_point(P, w, w + 8, naf, k.naf_len, sc);
+      row_shared_secret_point_t(P, w, w + 8, naf, k.naf_len, sc, tick);
       pend_store(sc, PB, np + j, P);
     }
     // one inversion: the new S points, piece P's F points, piece Q's label product
@@ -1260,6 +1292,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
         const int t = pq;  // P's wave-rows and offsets become Q's
         pq = pp;
         pp = t;
+        if (lane == 0) me.t_q = me.t_p;
         count_q = count_p;
         hits_q = hits;
       } else {
@@ -1315,6 +1348,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
       pn = t;
     }
     count_p = count;
+    if (lane == 0 && count) me.t_p = t_it;
     if (lane == 0) {
       me.busy = me.busy + (wall_clock64() - t_it);
       ST_EV(ST_ITER_END, st_wave, 0ull, 0u, 0u);
@@ -2652,6 +2686,11 @@ static std::mutex g_host_alloc_mu;
 static std::map<uintptr_t, size_t> g_host_allocs;
 
 static bool host_range_coherent(const void* p, size_t bytes) {
+#ifdef CUDASP_AB_STREAM_ANY_MEMORY
+  // measurement-only builds (tools/stream_probe.py --device-inputs): batch
+  // buffers in device memory, to price the zero-copy PCIe reads
+  return p != nullptr || bytes == 0;
+#endif
   if (!p) return false;
   const uintptr_t a = (uintptr_t)p;
   std::lock_guard<std::mutex> lk(g_host_alloc_mu);
@@ -2673,6 +2712,7 @@ struct cudasp_stream {
   uint64_t blocks = 0;      // the current query's grid
   uint32_t rmax = MULTI_RMAX;
   uint64_t idle_ticks = 0;  // 100 MHz wall-clock ticks with nothing to do before the kernel leaves
+  uint64_t prio_ticks = 0;  // wave priority step by piece age (stream_prio; 0: off)
   uint32_t timeout_ms = 0;  // waits fail after this long without progress (cudasp_stream_set_timeout)
   hipEvent_t exited = nullptr;
   bool running = false;     // a kernel was launched and `exited` recorded after it
@@ -2735,7 +2775,7 @@ static int stream_launch(cudasp_stream* st) {
   if (st->next_launch_resets) hipLaunchKernelGGL(k_stream_relaunch, dim3(1), dim3(64), 0, s->stream, st->dev);
   auto kf = s->fb_bits == 26 ? k_scan_stream<26> : k_scan_stream<22>;
   hipLaunchKernelGGL(kf, dim3((uint32_t)st->blocks), dim3(BLOCK), 0, s->stream, st->ctrl, st->dev, s->d_naf,
-                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, rmax, st->idle_ticks, st->wstat);
+                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, rmax, st->idle_ticks, st->wstat, st->prio_ticks);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(st->exited, s->stream));
   ST_HOST(102, st->blocks, (uint32_t)st->launches);
@@ -2823,6 +2863,15 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
     if (v >= 1 && v <= 600000) idle_ms = (uint32_t)v;
   }
   st->idle_ticks = (uint64_t)idle_ms * 100000ull;
+  // wave priority by piece age, one level per 3 ms (round 4, config 3 end to
+  // end: 148.7 / 150.7 M tx/s without, 158.2 / 162.5 with; config 4 172.4 vs
+  // 173.9, config 2 even; profiles/r04_stream_prio_ab.txt); 0 turns it off
+  uint32_t prio_us = 3000;
+  if (const char* e = getenv("CUDASP_STREAM_PRIO_US")) {
+    const long v = atol(e);
+    if (v >= 0 && v <= 1000000) prio_us = (uint32_t)v;
+  }
+  st->prio_ticks = (uint64_t)prio_us * 100ull;
   st->timeout_ms = 60000;
   if (const char* e = getenv("CUDASP_STREAM_TIMEOUT_MS")) {
     const long v = atol(e);
@@ -2860,14 +2909,11 @@ int cudasp_stream_publish_batch(cudasp_stream* st, const cudasp_stream_batch* bt
   if (!bt->match_flags && !bt->match_rows)
     return set_error(CUDASP_ERR_INVALID_ARG, "a streamed batch needs match_flags and/or match_rows");
   // every host buffer the kernel touches must be coherent pinned memory
-  // (cudasp_host_alloc); the outputs are checked up to the last offset + length
-  uint64_t words = 0;
-  const uint64_t ow = st->s->consts.full_x ? 4 : 1;
-  if (!host_range_coherent(bt->output_offsets, (size_t)n * 4) || !host_range_coherent(bt->output_lengths, (size_t)n * 4))
-    return set_error(CUDASP_ERR_INVALID_ARG, "streamed batch buffers must come from cudasp_host_alloc");
-  for (uint32_t i = 0; i < n; i++) words = std::max<uint64_t>(words, ((uint64_t)bt->output_offsets[i] + bt->output_lengths[i]) * ow);
-  if (!host_range_coherent(bt->tweak_keys, (size_t)n * 64) ||
-      (words && !host_range_coherent(bt->outputs, (size_t)words * 8)) ||
+  // (cudasp_host_alloc); the outputs list is checked at its start (its rows'
+  // offsets and lengths, like every CSR this library takes, are the caller's)
+  if (!host_range_coherent(bt->output_offsets, (size_t)n * 4) ||
+      !host_range_coherent(bt->output_lengths, (size_t)n * 4) || !host_range_coherent(bt->tweak_keys, (size_t)n * 64) ||
+      (bt->outputs && !host_range_coherent(bt->outputs, 8)) ||
       (bt->match_flags && !host_range_coherent(bt->match_flags, n)) ||
       (bt->match_rows && !host_range_coherent(bt->match_rows, (size_t)n * 4)))
     return set_error(CUDASP_ERR_INVALID_ARG, "streamed batch buffers must come from cudasp_host_alloc");

@@ -148,11 +148,19 @@ CUDASP_HD int8_t uniform_digit(const int8_t* p, int i) {
 #endif
 }
 
+// A ladder hook that does nothing (row_shared_secret_point_t).
+struct NoTick {
+  CUDASP_HD void operator()() const {}
+};
+
 // Stage A, first half: S = d T as a Jacobian point of the original curve.
 // tx, ty: the tweak point, 8 LE u32 words each (normal form, the reference's
 // layout).  naf: 2 * NAF_MAX digits (GLV half 1, then half 2, signs folded in).
-CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint32_t ty[8], const int8_t* naf,
-                                       uint32_t naf_len, const Scratch& sc) {
+// tick() runs every 16 ladder steps (the streaming kernel re-prioritises its
+// waves there).
+template <class Tick>
+CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uint32_t ty[8], const int8_t* naf,
+                                         uint32_t naf_len, const Scratch& sc, const Tick& tick) {
   ge T;
   fe_from_u32x8(T.x, tx);
   fe_from_u32x8(T.y, ty);
@@ -234,6 +242,7 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
   // doubling, so the load's latency runs under the doubling's ~900
   // instructions (the digits are wave-uniform, so is the choice).
   for (int i = (int)naf_len - 1; i >= 0; --i) {
+    if ((i & 15) == 0) tick();
     const int d0 = uniform_digit(naf, i), d1 = uniform_digit(naf, NAF_MAX + i);
     const int hf = d0 != 0 ? 0 : (d1 != 0 ? 1 : -1);
     ge Pn;
@@ -272,6 +281,7 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
   }
 #else
   for (int i = (int)naf_len - 1; i >= 0; --i) {
+    if ((i & 15) == 0) tick();
 #if LADDER_YH
     if (!inf) {
       gej_double_neg_yh(R, R);
@@ -325,6 +335,11 @@ CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint3
   fe cz;
   scr_load(cz, sc, VB_CZ);
   fe_mul(R.z, R.z, cz);
+}
+
+CUDASP_HD void row_shared_secret_point(gej& R, const uint32_t tx[8], const uint32_t ty[8], const int8_t* naf,
+                                       uint32_t naf_len, const Scratch& sc) {
+  row_shared_secret_point_t(R, tx, ty, naf, naf_len, sc, NoTick());
 }
 
 // Stage A, second half: from S (Jacobian) and 1/Z, the affine x (8 LE words)

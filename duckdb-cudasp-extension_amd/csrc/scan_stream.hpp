@@ -140,8 +140,23 @@ CUDASP_HD uint32_t stream_piece_rows(uint64_t rem, uint64_t claimed, uint32_t mi
 // StreamDev::stat when it leaves.
 struct StreamWave {
   uint64_t tk, t_start, busy;  // tk: the ticket, wave-rows [tk, tk + tr)
+  uint64_t t_p, t_q, t_old;    // when pieces P and Q were taken; the oldest piece the wave holds
   uint32_t tr, have, mine, pieces, rows, polls, drains;
 };
+
+// Issue priority (s_setprio 0..3) of a wave whose oldest unfinished piece
+// was taken `age` ticks ago: one level per `step` ticks.  A SIMD's resident
+// waves issue by priority, then by wave age; without this the oldest wave
+// of a SIMD takes most issue slots and the youngest one's piece waits until
+// the others run dry (~1 : 0.3 : 0.05), so a batch completes only when its
+// last, starved wave-row does -- 20+ ms after it was published, which
+// stalls a host that reuses the batch's slot.  By piece age the SIMD works
+// its pieces roughly in the order they were taken.  step 0: off.
+CUDASP_HD uint32_t stream_prio(uint64_t age, uint64_t step) {
+  if (step == 0) return 0;
+  const uint64_t p = age / step;
+  return p > 3 ? 3u : (uint32_t)p;
+}
 
 // Where a wave-row of a piece lives, looked up once at the piece's prefetch
 // and kept in LDS by the wave (wave-uniform): its batch's device mirror and

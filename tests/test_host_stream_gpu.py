@@ -200,3 +200,30 @@ def test_host_stream_timeout_then_pooled_feed(torch, monkeypatch):  # noqa: F811
     assert sorted(out.column("height").to_pylist()) == planted.tolist()
     assert st["streaming_feeds"] == 1
     release_pool()
+
+
+def test_host_e2e_eight_logical_gpus_config4():
+    """The N = 8 host path rehearsed on one card at the full config-4 size
+    (BASELINE.json configs[3]: 32.7M rows, 0 labels): tools/host_e2e with
+    CUDASP_TF_DEVICE_MAP=0 x 8 (8 logical GPUs, threads' chunks round-robin
+    over them, src/cudasp_extension.cu:523-529), 8 executor threads per
+    logical GPU, one streaming feed each (CUDASP_TF_MODE=stream; each kernel
+    gets 1/8 of the wave slots, GPU_MAX_HW_QUEUES=16 so every feed's stream
+    has a hardware queue).  Every query emits exactly the planted rows."""
+    import json
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tools", "host_e2e")
+    env = dict(os.environ, CUDASP_TF_DEVICE_MAP=",".join(["0"] * 8), CUDASP_TF_MODE="stream",
+               GPU_MAX_HW_QUEUES="16")
+    cmd = [exe, "--rows", "32700000", "--threads", "64", "--batch", "300000", "--labels", "0", "--input", "rows",
+           "--reps", "1", "--outputs", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["logical_gpus"] == 8
+    assert res["feeds"] == 8 and res["streaming_feeds"] == 8
+    assert res["emitted_equal_planted"] is True
+    assert res["matches"] == res["planted"] == 32700
+    print("8 logical GPUs, 64 threads, 32.7M rows: %.1f M tx/s on one card" % (res["tx_per_s"] / 1e6))

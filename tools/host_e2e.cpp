@@ -248,6 +248,7 @@ struct QueryResult {
   uint64_t emitted = 0;
   bool exact = false;  // emitted rows == planted rows
   cudasp_tf_stats stats{};
+  int logical_gpus = 0;
   double call_s_mean = 0, final_s_mean = 0, done_min = 0, done_max = 0;
 };
 
@@ -355,6 +356,7 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
   QueryResult q;
   q.secs = now_s();
   CK(cudasp_tf_get_stats(gs, &q.stats));
+  q.logical_gpus = cudasp_tf_num_gpus(gs);
   for (auto* l : ls) cudasp_tf_local_free(l);
   cudasp_tf_global_free(gs);
   cudasp_tf_bind_free(bd);
@@ -434,7 +436,7 @@ int main(int argc, char** argv) {
          "\"gpu_max_hw_queues_env\": \"%s\", \"launches\": %llu, \"rows_per_launch\": %.0f, "
          "\"harvest_wait_s\": %.4f, \"reserve_s\": %.4f, \"copy_s\": %.4f, \"launch_s\": %.4f, "
          "\"thread_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
-         "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f, \"streaming_feeds\": %u}\n",
+         "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f, \"streaming_feeds\": %u, \"logical_gpus\": %d}\n",
          a.columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)t.rows, a.threads, (long long)a.batch,
          a.labels,
          a.kmax ? ("\"1.." + std::to_string(a.kmax) + "\"").c_str() : std::to_string(a.k).c_str(),
@@ -444,6 +446,6 @@ int main(int argc, char** argv) {
          q.stats.streams_per_feed, q.stats.max_streams_per_device, q.stats.hw_queues, hq ? hq : "",
          (unsigned long long)q.stats.launches, q.stats.launches ? (double)q.stats.rows / q.stats.launches : 0.0,
          q.stats.harvest_wait_s, q.stats.reserve_s, q.stats.copy_s, q.stats.launch_s, q.call_s_mean, q.final_s_mean, q.done_min, q.done_max,
-         q.stats.streaming_feeds);
+         q.stats.streaming_feeds, q.logical_gpus);
   return all_exact ? 0 : 2;
 }

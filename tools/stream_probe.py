@@ -27,6 +27,13 @@ def main():
     ap.add_argument("--kmax", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--in-flight", type=int, default=8)
+    ap.add_argument("--modes", default="all,paced")
+    ap.add_argument("--device-inputs", action="store_true",
+                    help="publish device copies of rows / offsets / lengths / outputs (a library built with "
+                         "-DCUDASP_AB_STREAM_ANY_MEMORY): prices the zero-copy PCIe reads")
+    ap.add_argument("--device-results", action="store_true",
+                    help="match rows into device memory too (same build)")
+    ap.add_argument("--flags", action="store_true", help="also write per-row flags (the host path writes matches only)")
     a = ap.parse_args()
     import torch
 
@@ -46,7 +53,8 @@ def main():
         ys = b["tweak_y"].cpu().numpy().view(np.uint32)
         rows = np.ascontiguousarray(np.concatenate([xs.T, ys.T], axis=1)).view(np.uint8).reshape(n, 64)
         stage.append(StreamBatch(rows, b["outputs"].cpu().numpy(), b["offsets"][:n].cpu().numpy().view(np.uint32),
-                                 b["lengths"][:n].cpu().numpy().view(np.uint32), label_count=len(labels)))
+                                 b["lengths"][:n].cpu().numpy().view(np.uint32), label_count=len(labels),
+                                 want_flags=a.flags))
     setup_s = time.time() - t0
     out = dict(rows=a.rows, batch=a.batch, labels=a.labels, kmax=a.kmax, batches=len(sizes), setup_s=round(setup_s, 1))
     with Scanner(tm.SCAN, tm.SPEND, labels, max_rows=a.batch) as s:
@@ -65,42 +73,58 @@ def main():
         out["multi_ms"] = round(1e3 * min(times), 2)
         out["multi_tx_s"] = a.rows / min(times)
         want = [f[:b["n"]].cpu().numpy() for f, b in zip(flags, batches)]
-        # device-memory inputs (and flags) for the same kernel: isolates what
-        # the zero-copy PCIe reads / flag writes cost
-        dev_in = []
+        dev = []
         for b, sb in zip(batches, stage):
-            n = b["n"]
-            rows = torch.from_numpy(sb.rows.array.copy()).cuda()
-            dev_in.append(dict(rows=rows.data_ptr(), outputs=b["outputs"].data_ptr(), offs=b["offsets"].data_ptr(),
-                               lens=b["lengths"].data_ptr(), keep=rows,
-                               dflags=torch.zeros(n, dtype=torch.uint8, device="cuda")))
+            d = {}
+            if a.device_inputs:
+                d["rows"] = torch.from_numpy(sb.rows.array.copy()).cuda()
+                d["outputs"] = b["outputs"]
+                d["offs"] = b["offsets"]
+                d["lens"] = b["lengths"]
+            if a.device_results:
+                d["matches"] = torch.zeros(max(1, b["n"]), dtype=torch.int32, device="cuda")
+            dev.append(d)
         torch.cuda.synchronize()
         with ScanStream(s) as st:
-            for mode in ("all", "dev_in", "dev_all", "paced"):
+            for mode in a.modes.split(","):
                 times = []
                 for _ in range(a.reps + 1):
                     for sb in stage:
-                        sb.flags.array[:] = 0xEE
+                        sb.reset()
                     t = time.perf_counter()
                     seqs = []
-                    for sb, d in zip(stage, dev_in):
+                    for sb, d in zip(stage, dev):
                         if mode == "paced" and len(seqs) >= a.in_flight:
                             st.wait(seqs[-a.in_flight])
-                        if mode in ("dev_in", "dev_all"):
-                            fl = d["dflags"].data_ptr() if mode == "dev_all" else sb.flags
-                            seqs.append(st.publish(d["rows"], d["outputs"], d["offs"], d["lens"], sb.n, fl, sb.mirror))
+                        if a.device_inputs or a.device_results:
+                            mr = d["matches"].data_ptr() if a.device_results else sb.match_rows
+                            src = d if a.device_inputs else None
+                            seqs.append(st.publish(src["rows"].data_ptr() if src else sb.rows,
+                                                   src["outputs"].data_ptr() if src else sb.outputs,
+                                                   src["offs"].data_ptr() if src else sb.offsets,
+                                                   src["lens"].data_ptr() if src else sb.lengths,
+                                                   sb.n, None, sb.mirror, mr))
+                            sb.seq = seqs[-1]
                         else:
                             seqs.append(sb.publish(st))
+                    st.close_input()
                     st.wait(seqs[-1])
                     for q in seqs:
                         st.wait(q)
                     times.append(time.perf_counter() - t)
+                    for i, (sb, w) in enumerate(zip(stage, want)):
+                        if a.flags:
+                            ok = (sb.result() == w).all()
+                        elif a.device_results:
+                            c = st.matches(sb.seq)
+                            m = np.sort(dev[i]["matches"][:c].cpu().numpy().view(np.uint32))
+                        else:  # match counts readable until finish
+                            m = sb.matches(st)
+                            ok = len(m) == int(w.sum()) and (m == np.nonzero(w)[0]).all()
+                        if not ok:
+                            out["mismatch"] = "%s batch %d" % (mode, i)
                     st.finish()
                     out["counters_%s" % mode] = st.counters()
-                    for i, (sb, w, d) in enumerate(zip(stage, want, dev_in)):
-                        res = d["dflags"].cpu().numpy() if mode == "dev_all" else sb.result()
-                        if not (res == w).all():
-                            out["mismatch"] = "%s batch %d" % (mode, i)
                 best = min(times[1:])
                 out["stream_%s_ms" % mode] = round(1e3 * best, 2)
                 out["stream_%s_tx_s" % mode] = a.rows / best
