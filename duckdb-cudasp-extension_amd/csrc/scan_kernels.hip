@@ -794,7 +794,16 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_tick
     const uint64_t now = wall_clock64();
     if (pub != seen) {
       uint64_t pub_wr = 0;
-      for (uint32_t b = seen; b != pub; b++) {
+      uint32_t b = seen;
+      for (; b != pub; b++) {
+        // a staged batch is mirrored only once its DMA copies are done
+        // (cudasp_stream_publish_batch sets ready[e] from the copy stream's
+        // completion); batches go out in order
+        if (sys_load_u32(&ctrl->desc[b % STREAM_RING].staged)) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (sys_load_u32(&ctrl->ready[b % STREAM_RING]) != b + 1u) break;
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         const uint64_t* src = reinterpret_cast<const uint64_t*>(&ctrl->desc[b % STREAM_RING]);
         StreamBatch* de = &dev->desc[b % STREAM_RING];
         uint64_t* dst = reinterpret_cast<uint64_t*>(de);
@@ -814,13 +823,18 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_tick
         // already count a batch published after `pub` was read)
         pub_wr = d.first_wr + d.nwr;
       }
-      __hip_atomic_store(&dev->pub_wr, pub_wr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&dev->pub, pub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      ST_EV(ST_PUB, 0u, pub_wr, pub, seen);
-      seen = pub;
-      last = now;
+      if (b != seen) {
+        __hip_atomic_store(&dev->pub_wr, pub_wr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&dev->pub, b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        ST_EV(ST_PUB, 0u, pub_wr, b, seen);
+        seen = b;
+        last = now;
+      }
+      // (a batch still waiting for its copies does not keep the kernel from
+      // going idle: if the copy engine needed this kernel's compute units,
+      // holding them would never let it finish)
     }
-    if (cl) {  // `published` was read after `closed`: every batch is mirrored
+    if (cl && seen == pub) {  // `published` was read after `closed`: every batch is mirrored
       __hip_atomic_store(&dev->closed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
@@ -909,9 +923,14 @@ __device__ __forceinline__ void stream_copy_range(int64_t* mirror, const int64_t
 // group of wave-rows of one batch whose outputs lie close together (else
 // each lane copies its own row's) -- so the piece's PCIe latencies are paid
 // here, a few per piece, and nothing later reads host memory.
+// coal: the row blobs are read lane-contiguously (lane i the i-th 16 bytes
+// of each 1 KB of the wave-row's 4 KB, so every 4 lanes make one 64-byte
+// request) and transposed through the wave's 4 KB of LDS (`tr`), instead of
+// each lane reading its own 64-byte row in 16-byte pieces (64-byte-strided
+// lanes: over uncached pinned memory every piece is a request of its own).
 __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, uint64_t base, int count,
                                                 uint32_t lane, StreamWr* wr, StreamPf* pf, const Scratch& sc,
-                                                int stg, int meta, uint32_t ow) {
+                                                int stg, int meta, uint32_t ow, bool coal, uint4* tr) {
 #pragma unroll 1
   for (int j = 0; j < count; j++) {
     const StreamRow sr = stream_row(dev, hint, base + (uint32_t)j);
@@ -944,9 +963,21 @@ __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, 
         const uint32_t r0 = wr[g + i].r0;
         act[i] = r0 + lane < wr[g + i].n;
         const uint32_t r = act[i] ? r0 + lane : 0u;
-        const uint4* src = reinterpret_cast<const uint4*>(pf[g + i].rows + (size_t)r * 64);
+        if (coal) {
+          // 16-byte pieces lane + 64 q of the wave-row's rows (only those of
+          // rows the batch has: the last wave-row may be partial)
+          const uint32_t pieces = (wr[g + i].n - r0 < 64u ? wr[g + i].n - r0 : 64u) * 4u;
+          const uint4* src = reinterpret_cast<const uint4*>(pf[g + i].rows + (size_t)r0 * 64);
 #pragma unroll
-        for (int q = 0; q < 4; q++) v[i][q] = src[q];
+          for (int q = 0; q < 4; q++) {
+            const uint32_t idx = lane + 64u * q;
+            v[i][q] = idx < pieces ? src[idx] : make_uint4(0, 0, 0, 0);
+          }
+        } else {
+          const uint4* src = reinterpret_cast<const uint4*>(pf[g + i].rows + (size_t)r * 64);
+#pragma unroll
+          for (int q = 0; q < 4; q++) v[i][q] = src[q];
+        }
         of[i] = pf[g + i].offs[r];
         ln[i] = pf[g + i].lens[r];
       }
@@ -955,6 +986,15 @@ __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, 
     for (int i = 0; i < 3; i++) {
       if (g + i < count) {
         const int s0 = stg + 16 * (g + i);
+        if (coal) {  // transpose: piece lane + 64 q to LDS, then this lane's row
+#pragma unroll
+          for (int q = 0; q < 4; q++) tr[lane + 64 * q] = v[i][q];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int q = 0; q < 4; q++) v[i][q] = tr[4 * lane + q];
+          __builtin_amdgcn_wave_barrier();
+        }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           scr_store_w(sc, s0 + 4 * q, v[i][q].x);
@@ -969,7 +1009,13 @@ __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, 
     }
     // the outputs: runs of wave-rows of one batch whose lists span at most
     // 48 words per lane are copied by the whole wave; anything else (a
-    // scattered CSR) lane by lane
+    // scattered CSR) lane by lane.  A batch whose outputs are already in
+    // device memory (mirror == outputs: staged by DMA) needs no copy.
+    bool staged = true;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+      if (g + i < count) staged = staged && wr[g + i].mirror == pf[g + i].outputs;
+    if (staged) continue;
     uint32_t lo = ~0u, hi = 0;
     int i0 = 0;
 #pragma unroll
@@ -1102,7 +1148,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
                                                                     uint32_t* __restrict__ scr, uint32_t rmax,
                                                                     uint64_t idle_ticks,
                                                                     unsigned long long* __restrict__ wstat,
-                                                                    uint64_t prio_ticks) {
+                                                                    uint64_t prio_ticks, uint32_t pf_coal) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = SCAN_SCRATCH(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1131,6 +1177,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
   __shared__ StreamWave waves[BLOCK / 64];
   __shared__ StreamWr wrs[BLOCK / 64][3][MULTI_RMAX];
   __shared__ StreamPf pfs[BLOCK / 64][MULTI_RMAX];
+  __shared__ uint4 pftr[BLOCK / 64][256];  // the row blobs' transpose (stream_prefetch, coal)
   const uint32_t wid = threadIdx.x >> 6;
   volatile StreamWave& me = waves[wid];
   if (lane == 0) {
@@ -1221,7 +1268,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
     tick();
     StreamWr* const wn = wrs[wid][pn];
     const int meta_n = META + 2 * MULTI_RMAX * pn;
-    if (count) stream_prefetch(dev, hint, base, count, lane, wn, pfs[wid], sc, STG, meta_n, ow);
+    if (count) stream_prefetch(dev, hint, base, count, lane, wn, pfs[wid], sc, STG, meta_n, ow, pf_coal != 0, pftr[wid]);
     const int np = count_p * K;  // F points of piece P in pending slots 0 .. np - 1
     // stage A: S = d T of the new piece's rows (staged by the prefetch)
 #pragma unroll 1
@@ -2702,6 +2749,17 @@ static bool host_range_coherent(const void* p, size_t bytes) {
 
 constexpr uint32_t STREAM_MAX_WAVES = MAX_BLOCKS * (BLOCK / 64);
 
+// A staged batch's readiness, set from the copy stream once its DMA copies
+// are done (hipLaunchHostFunc: a runtime thread stores, no HIP call).
+struct StreamReadyArg {
+  StreamCtrl* ctrl;
+  uint32_t e, v;
+};
+static void stream_ready_cb(void* p) {
+  const StreamReadyArg* a = static_cast<const StreamReadyArg*>(p);
+  __atomic_store_n(&a->ctrl->ready[a->e], a->v, __ATOMIC_RELEASE);
+}
+
 struct cudasp_stream {
   cudasp_scanner* s = nullptr;
   StreamCtrl* ctrl = nullptr;  // coherent pinned host memory (same address on the device)
@@ -2713,8 +2771,11 @@ struct cudasp_stream {
   uint32_t rmax = MULTI_RMAX;
   uint64_t idle_ticks = 0;  // 100 MHz wall-clock ticks with nothing to do before the kernel leaves
   uint64_t prio_ticks = 0;  // wave priority step by piece age (stream_prio; 0: off)
+  uint32_t pf_coal = 1;     // row blobs read lane-contiguously + LDS transpose (stream_prefetch)
   uint32_t timeout_ms = 0;  // waits fail after this long without progress (cudasp_stream_set_timeout)
   hipEvent_t exited = nullptr;
+  hipStream_t copy = nullptr;             // staged batches' DMA copies (created at the first one)
+  StreamReadyArg ready_arg[STREAM_RING];  // their completion callbacks' arguments
   bool running = false;     // a kernel was launched and `exited` recorded after it
   bool failed = false;      // a kernel of this query failed or a wait timed out (sticky until finish)
   bool abandoned = false;   // finish timed out with the kernel alive: nothing may be freed
@@ -2775,7 +2836,7 @@ static int stream_launch(cudasp_stream* st) {
   if (st->next_launch_resets) hipLaunchKernelGGL(k_stream_relaunch, dim3(1), dim3(64), 0, s->stream, st->dev);
   auto kf = s->fb_bits == 26 ? k_scan_stream<26> : k_scan_stream<22>;
   hipLaunchKernelGGL(kf, dim3((uint32_t)st->blocks), dim3(BLOCK), 0, s->stream, st->ctrl, st->dev, s->d_naf,
-                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, rmax, st->idle_ticks, st->wstat, st->prio_ticks);
+                     s->consts, s->d_fb, s->d_labels, s->d_mscratch, rmax, st->idle_ticks, st->wstat, st->prio_ticks, st->pf_coal);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(st->exited, s->stream));
   ST_HOST(102, st->blocks, (uint32_t)st->launches);
@@ -2872,6 +2933,7 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
     if (v >= 0 && v <= 1000000) prio_us = (uint32_t)v;
   }
   st->prio_ticks = (uint64_t)prio_us * 100ull;
+  if (const char* e = getenv("CUDASP_STREAM_PF_COAL")) st->pf_coal = atoi(e) != 0 ? 1u : 0u;
   st->timeout_ms = 60000;
   if (const char* e = getenv("CUDASP_STREAM_TIMEOUT_MS")) {
     const long v = atol(e);
@@ -2904,18 +2966,24 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
 int cudasp_stream_publish_batch(cudasp_stream* st, const cudasp_stream_batch* bt, uint64_t* seq) {
   if (!st || !bt) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
   const uint32_t n = bt->n;
+  const bool staged = bt->d_tweak_keys != nullptr;
   if (n == 0 || !bt->tweak_keys || !bt->output_offsets || !bt->output_lengths || !bt->d_mirror)
     return set_error(CUDASP_ERR_INVALID_ARG, "empty batch or null buffer (the outputs mirror included)");
   if (!bt->match_flags && !bt->match_rows)
     return set_error(CUDASP_ERR_INVALID_ARG, "a streamed batch needs match_flags and/or match_rows");
+  if (staged && (!bt->d_output_offsets || !bt->d_output_lengths || (bt->output_words && !bt->outputs)))
+    return set_error(CUDASP_ERR_INVALID_ARG, "a staged batch needs device offsets and lengths buffers");
   // every host buffer the kernel touches must be coherent pinned memory
-  // (cudasp_host_alloc); the outputs list is checked at its start (its rows'
-  // offsets and lengths, like every CSR this library takes, are the caller's)
-  if (!host_range_coherent(bt->output_offsets, (size_t)n * 4) ||
-      !host_range_coherent(bt->output_lengths, (size_t)n * 4) || !host_range_coherent(bt->tweak_keys, (size_t)n * 64) ||
-      (bt->outputs && !host_range_coherent(bt->outputs, 8)) ||
-      (bt->match_flags && !host_range_coherent(bt->match_flags, n)) ||
-      (bt->match_rows && !host_range_coherent(bt->match_rows, (size_t)n * 4)))
+  // (cudasp_host_alloc): the result buffers always, the inputs unless the
+  // batch is staged by DMA; the outputs list is checked at its start (its
+  // rows' offsets and lengths, like every CSR this library takes, are the
+  // caller's)
+  if ((bt->match_flags && !host_range_coherent(bt->match_flags, n)) ||
+      (bt->match_rows && !host_range_coherent(bt->match_rows, (size_t)n * 4)) ||
+      (!staged && (!host_range_coherent(bt->output_offsets, (size_t)n * 4) ||
+                   !host_range_coherent(bt->output_lengths, (size_t)n * 4) ||
+                   !host_range_coherent(bt->tweak_keys, (size_t)n * 64) ||
+                   (bt->outputs && !host_range_coherent(bt->outputs, 8)))))
     return set_error(CUDASP_ERR_INVALID_ARG, "streamed batch buffers must come from cudasp_host_alloc");
   std::lock_guard<std::mutex> lk(st->mu);
   if (st->ctrl->closed) return set_error(CUDASP_ERR_INVALID_ARG, "stream already closed");
@@ -2925,15 +2993,34 @@ int cudasp_stream_publish_batch(cudasp_stream* st, const cudasp_stream_batch* bt
   if (b >= STREAM_RING && !stream_seq_done(st, (uint64_t)b - STREAM_RING))
     return set_error(CUDASP_ERR_CAPACITY, "more than %u streamed batches in flight", STREAM_RING);
   StreamBatch& d = st->ctrl->desc[e];
-  d.rows = bt->tweak_keys;
-  d.outputs = bt->outputs;
-  d.offs = bt->output_offsets;
-  d.lens = bt->output_lengths;
+  if (staged) {
+    DeviceGuard g(st->s->device);
+    if (!st->copy) HIP_TRY(hipStreamCreateWithFlags(&st->copy, hipStreamNonBlocking));
+    __atomic_store_n(&st->ctrl->ready[e], 0u, __ATOMIC_RELAXED);
+    HIP_TRY(hipMemcpyAsync(bt->d_tweak_keys, bt->tweak_keys, (size_t)n * 64, hipMemcpyHostToDevice, st->copy));
+    HIP_TRY(hipMemcpyAsync(bt->d_output_offsets, bt->output_offsets, (size_t)n * 4, hipMemcpyHostToDevice, st->copy));
+    HIP_TRY(hipMemcpyAsync(bt->d_output_lengths, bt->output_lengths, (size_t)n * 4, hipMemcpyHostToDevice, st->copy));
+    if (bt->output_words)
+      HIP_TRY(hipMemcpyAsync(bt->d_mirror, bt->outputs, bt->output_words * 8, hipMemcpyHostToDevice, st->copy));
+    st->ready_arg[e] = StreamReadyArg{st->ctrl, e, b + 1u};
+    HIP_TRY(hipLaunchHostFunc(st->copy, stream_ready_cb, &st->ready_arg[e]));
+    d.rows = bt->d_tweak_keys;
+    d.outputs = bt->d_mirror;
+    d.offs = bt->d_output_offsets;
+    d.lens = bt->d_output_lengths;
+  } else {
+    d.rows = bt->tweak_keys;
+    d.outputs = bt->outputs;
+    d.offs = bt->output_offsets;
+    d.lens = bt->output_lengths;
+  }
   d.flags = bt->match_flags;
   d.matches = bt->match_rows;
   d.mirror = bt->d_mirror;
   d.n = n;
   d.nwr = (n + 63u) / 64u;
+  d.staged = staged ? 1u : 0u;
+  d.reserved = 0;
   d.first_wr = st->published_wr;
   d.seq = b;
   st->published_wr += d.nwr;
@@ -2958,6 +3045,10 @@ int cudasp_stream_publish(cudasp_stream* st, const uint8_t* rows, const int64_t*
   b.match_flags = flags;
   b.match_rows = nullptr;
   b.d_mirror = d_mirror;
+  b.d_tweak_keys = nullptr;
+  b.d_output_offsets = nullptr;
+  b.d_output_lengths = nullptr;
+  b.output_words = 0;
   if (!flags) return set_error(CUDASP_ERR_INVALID_ARG, "null flags buffer");
   return cudasp_stream_publish_batch(st, &b, seq);
 }
@@ -3118,6 +3209,7 @@ int cudasp_stream_finish(cudasp_stream* st) {
   // the counters' copy queued on the scanner's stream (ordered before its
   // next launch; cudasp_stream_counters waits for the copy).
   const bool ran = st->next > 0;
+  if (st->copy) (void)hipStreamSynchronize(st->copy);  // every staged batch's callback has run
   memset(st->ctrl, 0, sizeof(StreamCtrl));
   st->next = 0;
   st->published_wr = 0;
@@ -3184,6 +3276,10 @@ void cudasp_stream_destroy(cudasp_stream* st) {
   if (st->ctrl) cudasp_host_free(st->ctrl);
   DeviceGuard g(st->s->device);
   if (st->s->stream) (void)hipStreamSynchronize(st->s->stream);
+  if (st->copy) {
+    (void)hipStreamSynchronize(st->copy);
+    (void)hipStreamDestroy(st->copy);
+  }
   if (st->dev) (void)hipFree(st->dev);
   if (st->wstat) (void)hipFree(st->wstat);
   if (st->h_counts) (void)hipHostFree(st->h_counts);

@@ -67,6 +67,8 @@ struct StreamBatch {
   int64_t* mirror;          // device copy of the outputs the compares read
   uint32_t n;
   uint32_t nwr;             // wave-rows: ceil(n / 64)
+  uint32_t staged;          // 1: the pointers are device copies made by DMA; mirror once ctrl->ready says so
+  uint32_t reserved;
   uint64_t first_wr;        // wave-rows published before this batch
   uint64_t seq;             // the batch's sequence number (tells a reused ring entry)
 };
@@ -79,6 +81,7 @@ struct StreamCtrl {
   uint32_t reserved;
   uint32_t done[STREAM_RING];       // ring entry e: 1 + sequence number of the last batch completed there (kernel)
   uint32_t nmatch[STREAM_RING];     // matching rows of that batch (kernel; written before `done`)
+  uint32_t ready[STREAM_RING];      // staged batch: 1 + its sequence number once its DMA copies are done (host)
   StreamBatch desc[STREAM_RING];    // batch b at entry b % STREAM_RING
 };
 

@@ -32,21 +32,21 @@ def host_rows(b):
     return np.ascontiguousarray(np.concatenate([xs.T, ys.T], axis=1).astype("<u4")).view(np.uint8).reshape(n, 64)
 
 
-def staged(b, label_count):
+def staged(b, label_count, dma=False):
     from cudasp_amd import StreamBatch
     n = b["n"]
     return StreamBatch(host_rows(b), b["outputs"].cpu().numpy(), b["offsets"][:n].cpu().numpy().view(np.uint32),
-                       b["lengths"][:n].cpu().numpy().view(np.uint32), label_count=label_count)
+                       b["lengths"][:n].cpu().numpy().view(np.uint32), label_count=label_count, staged=dma)
 
 
-def run_stream(batches, labels, rounds=1, max_in_flight=None):
+def run_stream(batches, labels, rounds=1, max_in_flight=None, dma=False):
     """Publish every batch into one stream (`rounds` queries on the same
     stream), waiting for the oldest when max_in_flight are out; returns the
     last round's flags per batch and the stream's stats.  Every batch's
     compacted matches (match_rows, cudasp_stream_matches) are its flagged
     rows."""
     from cudasp_amd import Scanner, ScanStream
-    stage = [staged(b, len(labels)) for b in batches]
+    stage = [staged(b, len(labels), dma=dma and i % 2 == 0) for i, b in enumerate(batches)]
     with Scanner(SCAN, SPEND, labels, max_rows=1000) as s, ScanStream(s) as st:
         for _ in range(rounds):
             for sb in stage:
@@ -76,14 +76,16 @@ def flags_equal(got, want):
 SIZES = [3001, 64, 1, 129, 70000, 65, 2047, 300000]
 
 
-@pytest.mark.parametrize("nlabels", [0, 2])
-def test_stream_equals_per_batch(torch, nlabels):
+@pytest.mark.parametrize("nlabels,dma", [(0, False), (2, False), (2, True)])
+def test_stream_equals_per_batch(torch, nlabels, dma):
+    """dma: every other batch staged into device buffers by DMA before the
+    kernel takes it (cudasp_stream_batch.d_*), mixed with in-place ones."""
     labels = [LABEL, SPEND][:nlabels]
     batches = [tm.make_batch(torch, 1000 + 300000 * i, n) for i, n in enumerate(SIZES)]
     tm.plant(torch, batches, labels)
     want = tm.run_per_batch(torch, batches, labels)
     assert sum(c for _, _, c in want) > 0
-    got, stats = run_stream(batches, labels, rounds=2)
+    got, stats = run_stream(batches, labels, rounds=2, dma=dma)
     flags_equal(got, want)
     assert stats["launches"] >= 2  # one kernel per query at least
 

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--device-inputs", action="store_true",
                     help="publish device copies of rows / offsets / lengths / outputs (a library built with "
                          "-DCUDASP_AB_STREAM_ANY_MEMORY): prices the zero-copy PCIe reads")
+    ap.add_argument("--staged", action="store_true", help="stage every batch into device buffers by DMA (product path)")
     ap.add_argument("--device-results", action="store_true",
                     help="match rows into device memory too (same build)")
     ap.add_argument("--flags", action="store_true", help="also write per-row flags (the host path writes matches only)")
@@ -54,7 +55,7 @@ def main():
         rows = np.ascontiguousarray(np.concatenate([xs.T, ys.T], axis=1)).view(np.uint8).reshape(n, 64)
         stage.append(StreamBatch(rows, b["outputs"].cpu().numpy(), b["offsets"][:n].cpu().numpy().view(np.uint32),
                                  b["lengths"][:n].cpu().numpy().view(np.uint32), label_count=len(labels),
-                                 want_flags=a.flags))
+                                 want_flags=a.flags, staged=a.staged))
     setup_s = time.time() - t0
     out = dict(rows=a.rows, batch=a.batch, labels=a.labels, kmax=a.kmax, batches=len(sizes), setup_s=round(setup_s, 1))
     with Scanner(tm.SCAN, tm.SPEND, labels, max_rows=a.batch) as s:
@@ -103,7 +104,7 @@ def main():
                                                    src["outputs"].data_ptr() if src else sb.outputs,
                                                    src["offs"].data_ptr() if src else sb.offsets,
                                                    src["lens"].data_ptr() if src else sb.lengths,
-                                                   sb.n, None, sb.mirror, mr))
+                                                   sb.n, None, src["outputs"] if src else sb.mirror, mr))
                             sb.seq = seqs[-1]
                         else:
                             seqs.append(sb.publish(st))
