@@ -809,23 +809,33 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_tick
         uint64_t* dst = reinterpret_cast<uint64_t*>(de);
         StreamBatch d;
         uint64_t* dw = reinterpret_cast<uint64_t*>(&d);
-        // seqlock write (stream_batch_of): seq invalid, the fields, then seq
+        // seqlock write (stream_batch_of): seq invalid, the fields, then seq.
+        // Every store is an agent-scope relaxed one (global_store sc1: written
+        // through to memory, the line dropped from this XCD's L2) and each
+        // step waits for the previous one's stores to complete (vmcnt), which
+        // orders them for the workers' sc1 loads on any XCD -- no release
+        // fence: on gfx950 that is buffer_wbl2, a write-back of the whole
+        // L2's dirty lines (here the workers' scratch), stalling this XCD's
+        // memory traffic several times per mirrored batch (round 4)
         static_assert(offsetof(StreamBatch, seq) + 8 == sizeof(StreamBatch), "seq is the descriptor's last word");
         __hip_atomic_store(&de->seq, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 #pragma unroll
         for (int i = 0; i < (int)(sizeof(StreamBatch) / 8); i++) dw[i] = sys_load_u64(src + i);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int i = 0; i < (int)(sizeof(StreamBatch) / 8) - 1; i++)
           __hip_atomic_store(dst + i, dw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&de->seq, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&de->seq, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the rows mirrored so far (not the host's published_wr, which may
         // already count a batch published after `pub` was read)
         pub_wr = d.first_wr + d.nwr;
       }
       if (b != seen) {
-        __hip_atomic_store(&dev->pub_wr, pub_wr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&dev->pub, b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the descriptors before the counts
+        __hip_atomic_store(&dev->pub_wr, pub_wr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&dev->pub, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ST_EV(ST_PUB, 0u, pub_wr, b, seen);
         seen = b;
         last = now;
@@ -835,13 +845,13 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_tick
       // holding them would never let it finish)
     }
     if (cl && seen == pub) {  // `published` was read after `closed`: every batch is mirrored
-      __hip_atomic_store(&dev->closed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&dev->closed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
     if (dev_load_u64(&dev->ticket) < dev_load_u64(&dev->pub_wr)) {
       last = now;  // rows still unclaimed: not idle
     } else if (now - last > idle_ticks) {
-      __hip_atomic_store(&dev->idle, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&dev->idle, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       atomicAdd(&dev->stat[STREAM_STAT_IDLE_EXITS], 1ull);
       break;
     }
@@ -850,6 +860,12 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_tick
   }
   atomicAdd(&dev->stat[STREAM_STAT_POLLER_POLLS], (unsigned long long)polls);
 }
+
+// The batch-complete word's release (stream_emit): 1 = a system-scope
+// release fence before it (A/B; see the comment there).
+#ifndef CUDASP_STREAM_RELEASE_FENCE
+#define CUDASP_STREAM_RELEASE_FENCE 1
+#endif
 
 // Raw scratch words (column-major like scr_load / scr_store).
 __device__ __forceinline__ void scr_store_w(const Scratch& sc, int w, uint32_t v) {
@@ -933,6 +949,15 @@ __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, 
                                                 int stg, int meta, uint32_t ow, bool coal, uint4* tr) {
 #pragma unroll 1
   for (int j = 0; j < count; j++) {
+    if (j > 0 && wr[j - 1].r0 / 64u + 1u < wr[j - 1].nwr) {
+      // the next wave-row of the previous one's batch: no lookup (the
+      // batch's descriptor cannot change while this wave holds its rows)
+      StreamWr w = wr[j - 1];
+      w.r0 += 64u;
+      wr[j] = w;
+      pf[j] = pf[j - 1];
+      continue;
+    }
     const StreamRow sr = stream_row(dev, hint, base + (uint32_t)j);
     StreamWr w;
     w.mirror = sr.mirror;
@@ -1081,12 +1106,16 @@ __device__ __forceinline__ void stream_emit(StreamCtrl* ctrl, StreamDev* dev, co
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's stores are written before its rows count
   if (lane == 0) {
+    // one count per run of wave-rows of one batch (a piece's usually are)
 #pragma unroll 1
-    for (int j = 0; j < count; j++) {
+    for (int j = 0; j < count;) {
+      int j1 = j + 1;
+      while (j1 < count && wr[j1].b == wr[j].b) j1++;
+      const uint32_t run = (uint32_t)(j1 - j);
       const uint32_t e = wr[j].b % STREAM_RING;
       const uint32_t nwr = wr[j].nwr;
-      const uint32_t before = atomicAdd(&dev->wr_done[e], 1u);
-      if (before + 1u == nwr) {
+      const uint32_t before = atomicAdd(&dev->wr_done[e], run);
+      if (before + run == nwr) {
         // the entry's counts back to 0 for batch b + STREAM_RING (published
         // only after the host has seen this batch done); the subtraction
         // commutes with that batch's counts however late it lands
@@ -1095,11 +1124,14 @@ __device__ __forceinline__ void stream_emit(StreamCtrl* ctrl, StreamDev* dev, co
         __hip_atomic_store(&ctrl->nmatch[e], nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         // system-scope release, then the done word: the host's acquire of
         // `done` sees the match count and every result store before it
+#if CUDASP_STREAM_RELEASE_FENCE
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(&ctrl->done[e], wr[j].b + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         ST_EV(ST_DONE, 0u, (uint64_t)nm, wr[j].b, nwr);
       }
+      j = j1;
     }
   }
 }

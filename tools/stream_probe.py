@@ -114,13 +114,15 @@ def main():
                         st.wait(q)
                     times.append(time.perf_counter() - t)
                     for i, (sb, w) in enumerate(zip(stage, want)):
+                        ok = True
                         if a.flags:
                             ok = (sb.result() == w).all()
-                        elif a.device_results:
-                            c = st.matches(sb.seq)
-                            m = np.sort(dev[i]["matches"][:c].cpu().numpy().view(np.uint32))
                         else:  # match counts readable until finish
-                            m = sb.matches(st)
+                            if a.device_results:
+                                c = st.matches(sb.seq)
+                                m = np.sort(dev[i]["matches"][:c].cpu().numpy().view(np.uint32))
+                            else:
+                                m = sb.matches(st)
                             ok = len(m) == int(w.sum()) and (m == np.nonzero(w)[0]).all()
                         if not ok:
                             out["mismatch"] = "%s batch %d" % (mode, i)
