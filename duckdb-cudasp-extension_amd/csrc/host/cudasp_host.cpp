@@ -77,14 +77,6 @@ constexpr int FEED_MAX_STREAM_SLOTS = 48;
 constexpr int FEED_MAX_SLOTS = FEED_MAX_STREAM_SLOTS;
 static_assert(FEED_MAX_SLOTS >= FEED_MAX_STREAMS + 2, "per-slot launch feeds");
 
-// Streaming feeds stage each batch into device memory by DMA (the kernel then
-// reads HBM) instead of reading the pinned slot in place over PCIe:
-// CUDASP_TF_STAGE=1 / 0.
-bool feed_stream_stage() {
-  if (const char* e = getenv("CUDASP_TF_STAGE")) return atoi(e) != 0;
-  return false;
-}
-
 int feed_stream_slots() {
   if (const char* e = getenv("CUDASP_TF_STREAM_SLOTS")) {
     const int v = atoi(e);
@@ -239,7 +231,6 @@ struct FeedRes {
   cudasp_stream* stream = nullptr;
   uint32_t stream_blocks = 0;
   int stream_slots = FEED_STREAM_SLOTS;  // slots of a streaming feed (feed_stream_slots at creation)
-  bool stream_stage = false;  // streaming feed: batches staged into device buffers by DMA (feed_stream_stage)
   std::vector<void*> stale_host, stale_dev;
   int nslots() const { return stream ? stream_slots : nstreams + 2; }
 };
@@ -393,13 +384,6 @@ int prepare_slot_streaming(FeedRes& r, FeedSlot& s, size_t words, size_t txid) {
     if (rc == CUDASP_OK) rc = host((void**)&s.h_lens, n * 4);
     if (rc == CUDASP_OK) rc = host((void**)&s.h_matches, n * 4);
     if (rc != CUDASP_OK) return rc;
-    if (r.stream_stage) {  // the DMA copies' destinations
-      if (hipMalloc((void**)&s.d_rows, n * 64) != hipSuccess || hipMalloc((void**)&s.d_offs, n * 4) != hipSuccess ||
-          hipMalloc((void**)&s.d_lens, n * 4) != hipSuccess) {
-        (void)hipGetLastError();
-        return host_fail(CUDASP_ERR_HIP, "staging buffers of %zu rows on device %d: allocation failed", n, r.device);
-      }
-    }
     s.txid_off.resize(n);
     s.txid_size.resize(n);
     s.heights.resize(n);
@@ -543,12 +527,6 @@ int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
       b.match_flags = nullptr;
       b.match_rows = s.h_matches;
       b.d_mirror = s.d_outputs;
-      if (r.stream_stage) {
-        b.d_tweak_keys = s.d_rows;
-        b.d_output_offsets = s.d_offs;
-        b.d_output_lengths = s.d_lens;
-        b.output_words = words;
-      }
       rc = cudasp_stream_publish_batch(r.stream, &b, &s.seq);
       if (rc != CUDASP_OK)
         rc = host_fail(rc, "cudasp_scan batch of %u rows on device %d failed: %s", n, r.device, cudasp_last_error());
@@ -988,7 +966,6 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
         if (rc == CUDASP_OK) {
           r->stream_blocks = blocks;
           r->stream_slots = feed_stream_slots();
-          r->stream_stage = feed_stream_stage();
         } else if (rc == CUDASP_ERR_INVALID_ARG) {  // a width the streaming kernel lacks: per-slot launches
           r->stream = nullptr;
           r->nstreams = g.launch_streams;

@@ -1040,6 +1040,9 @@ __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, 
 #pragma unroll
     for (int i = 0; i < 3; i++)
       if (g + i < count) staged = staged && wr[g + i].mirror == pf[g + i].outputs;
+#ifdef CUDASP_AB_NO_OUTCOPY
+    staged = true;  // measurement only: compares read a stale mirror
+#endif
     if (staged) continue;
     uint32_t lo = ~0u, hi = 0;
     int i0 = 0;
@@ -1104,7 +1107,9 @@ __device__ __forceinline__ void stream_emit(StreamCtrl* ctrl, StreamDev* dev, co
       }
     }
   }
+#ifndef CUDASP_AB_NO_EMIT_WAIT
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's stores are written before its rows count
+#endif
   if (lane == 0) {
     // one count per run of wave-rows of one batch (a piece's usually are)
 #pragma unroll 1
@@ -1143,6 +1148,9 @@ struct StreamTick {
   volatile StreamWave* me;
   uint64_t step;
   __device__ __forceinline__ void operator()() const {
+#ifdef CUDASP_AB_NO_TICK
+    return;
+#endif
     if (step == 0) return;
     const uint64_t t_old = uniform_u64(me->t_old);
     switch (stream_prio(wall_clock64() - t_old, step)) {

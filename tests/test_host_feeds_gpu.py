@@ -191,8 +191,8 @@ def test_host_error_mid_query_then_pool_reuse(table16, keys):  # noqa: F811
     assert _heights(out) == expected
 
 
-@pytest.mark.parametrize("threads,batch,stage", [(3, 2500, "0"), (8, 300000, "0"), (3, 2500, "1")])
-def test_host_streaming_feed_16_labels(table16, keys, threads, batch, stage, monkeypatch):  # noqa: F811
+@pytest.mark.parametrize("threads,batch", [(3, 2500), (8, 300000)])
+def test_host_streaming_feed_16_labels(table16, keys, threads, batch, monkeypatch):  # noqa: F811
     """Streaming feeds (the host's default, CUDASP_TF_MODE=stream: each
     closed slot is published to the feed's one persistent k_scan_stream
     kernel, which reads it from pinned host memory in place): the emitted
@@ -203,7 +203,6 @@ def test_host_streaming_feed_16_labels(table16, keys, threads, batch, stage, mon
     rows, expected = table16
     scan, spend, labels = keys
     monkeypatch.setenv("CUDASP_TF_MODE", "stream")
-    monkeypatch.setenv("CUDASP_TF_STAGE", stage)  # 1: each slot staged into device buffers by DMA
     release_pool()
     stats = {}
     out = cudasp_scan(rows, scan, spend, labels, batch_size=batch, threads=threads, stats=stats)
