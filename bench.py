@@ -511,7 +511,9 @@ def e2e_leg(args, labels, world, fb_bits, mode=None):
     --e2e-hw-queues sets one).  The host's default is its streaming feeds
     (one persistent kernel per device reading the slots in place, DESIGN.md
     section 7c); mode="launch" selects its per-slot launches
-    (CUDASP_TF_MODE=launch)."""
+    (CUDASP_TF_MODE=launch).  Each query starts from an idle GPU, whose clock
+    ramps up during the query; `reps` more queries start right after a 30 ms
+    busy kernel (warm_tx_per_s: the host path at full clock)."""
     import subprocess
     import tempfile
     exe = os.path.join(ROOT, "tools", "host_e2e")
@@ -527,7 +529,7 @@ def e2e_leg(args, labels, world, fb_bits, mode=None):
         env["GPU_MAX_HW_QUEUES"] = str(args.e2e_hw_queues)
     lf = None
     cmd = [exe, "--rows", str(args.rows), "--threads", str(threads), "--batch", str(args.batch_size),
-           "--labels", str(len(labels)), "--input", args.e2e_input, "--reps", str(reps)]
+           "--labels", str(len(labels)), "--input", args.e2e_input, "--reps", str(reps), "--warm-reps", str(reps)]
     if labels:
         lf = tempfile.NamedTemporaryFile(prefix="cudasp_labels_", suffix=".bin", delete=False)
         lf.write(b"".join(labels))
@@ -872,6 +874,8 @@ def main():
     ap.add_argument("--e2e-hw-queues", type=int, default=0,
                     help="GPU_MAX_HW_QUEUES for the e2e child; 0 = the environment's (HIP default 4)")
     ap.add_argument("--e2e-timeout", type=int, default=600)
+    ap.add_argument("--idle-samples", type=int, default=3,
+                    help="device-resident steps each after 100 ms of GPU idle (device_after_idle); 0 = none")
     ap.add_argument("--pmc-summary", default="",
                     help="HBM traffic summary (default: profiles/r03_pmc_hbm_multi.json with --launch multi, "
                          "profiles/r02_pmc_hbm_k_shared_secret.json with --launch batches)")
@@ -950,6 +954,22 @@ def main():
         print("rank %d: %d found, %d flagged, %d planted; found per step %s; batches (index, found, planted) "
               "that differ: %s" % (rank, found, flagged, tab.expected, step_found, bad[:16]), file=sys.stderr, flush=True)
     total_s, found, flagged, expected = aggregate(world, args.dist_backend, total_s, found, flagged, tab.expected)
+    after_idle = None
+    if multi and world == 1 and args.idle_samples:
+        # The same step started after 100 ms of GPU idle, as every end-to-end
+        # query starts (the clock ramps up within it): the device rate to set
+        # the e2e leg against.  After the timed region; never the value.
+        idle_s = []
+        for _ in range(args.idle_samples):
+            torch.cuda.synchronize(device)
+            time.sleep(0.1)
+            t0 = time.perf_counter()
+            step()
+            torch.cuda.synchronize(device)
+            idle_s.append(time.perf_counter() - t0)
+        med = float(np.median(idle_s))
+        after_idle = dict(tx_s=args.rows / med, ms=med * 1e3, samples=[round(x * 1e3, 3) for x in idle_s],
+                          note="one device-resident step after 100 ms of GPU idle, median of the samples")
 
     # Per-launch kernel durations.  multi: the step is ONE k_scan_multi launch,
     # timed by the HIP events around it on its stream (it runs alone), so
@@ -1032,6 +1052,8 @@ def main():
                      exclusive_pass_matches_equal_planted=excl["matches_equal_planted"]),
         setup_s=round(setup_s, 2),
     )
+    if after_idle:
+        result["device_after_idle"] = after_idle
     if not args.no_layout_probe:
         result["layout_probe"] = layout_probe(lib, tab)
         if os.path.exists(args.pmc_summary) and not args.outputs_max and args.outputs_per_row == 2:
@@ -1094,6 +1116,13 @@ def main():
             e2e = e2e_leg(args, labels, world, args.fb_bits)
             result["e2e"] = e2e
             result["e2e_tx_s"] = e2e.get("tx_per_s")
+            result["e2e_warm_tx_s"] = e2e.get("warm_tx_per_s")
+            if after_idle and e2e.get("tx_per_s"):
+                # like for like: both start from an idle GPU / both at full clock
+                result["e2e_vs_device"] = dict(
+                    cold=e2e["tx_per_s"] / after_idle["tx_s"],
+                    warm=(e2e.get("warm_tx_per_s") or 0) / value,
+                    note="e2e_tx_s / device_after_idle.tx_s, and e2e_warm_tx_s / value (back-to-back steps)")
             if not args.no_e2e_launch:
                 # the same child with the host's per-slot launches (each slot
                 # copied to the device and scanned by its own k_scan_multi)

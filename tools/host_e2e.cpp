@@ -21,7 +21,9 @@
 //
 //   host_e2e [--rows N] [--threads T] [--batch B] [--labels L --labels-file F]
 //            [--outputs K | --outputs-max KMAX] [--input rows|columns]
-//            [--reps R]
+//            [--reps R] [--warm-reps W [--warm-ms MS]]
+// (W more queries, each started right after MS ms of a busy kernel on every
+// GPU: the rate at full clock, without the ramp from idle; warm_tx_per_s)
 // Label keys: F holds L 64-byte keys (x || y, little-endian, bench.label_keys);
 // without F, L must be 0 or 1 (the SQL test's label, test/sql/cudasp.test:104).
 // Prints one JSON line; exit 0 iff every timed query emitted exactly the
@@ -83,6 +85,8 @@ struct Args {
   int kmax = 0;  // > 0: 1..kmax outputs per row
   bool columnar = false;
   int reps = 1;
+  int warm_reps = 0;    // more queries, each right after a busy kernel on every GPU (clock at speed)
+  int warm_ms = 30;
 };
 
 static Args parse(int argc, char** argv) {
@@ -105,6 +109,8 @@ static Args parse(int argc, char** argv) {
     else if (s == "--outputs-max") a.kmax = atoi(val());
     else if (s == "--input") a.columnar = std::string(val()) == "columns";
     else if (s == "--reps") a.reps = std::max(1, atoi(val()));
+    else if (s == "--warm-reps") a.warm_reps = std::max(0, atoi(val()));
+    else if (s == "--warm-ms") a.warm_ms = std::max(1, atoi(val()));
     else {
       fprintf(stderr, "unknown argument %s\n", s.c_str());
       exit(1);
@@ -252,8 +258,44 @@ struct QueryResult {
   double call_s_mean = 0, final_s_mean = 0, done_min = 0, done_max = 0;
 };
 
+// A GPU left idle lowers its clock, and the first milliseconds of the next
+// work run below speed (tools/stream_probe.py --gap-ms / --prewarm: 100 ms of
+// idle costs k_scan_multi 1.2 ms at 1M rows, 3.4 ms at 9.4M).  The warm
+// queries start right after this: every wave slot busy with FMAs for `ms`
+// (the 100 MHz constant clock; an iteration cap bounds it regardless).
+__global__ void k_busy(uint64_t ticks, float* sink) {
+  const uint64_t t0 = wall_clock64();
+  float v = (float)threadIdx.x, m = 1.0000001f;
+  for (uint32_t it = 0; it < (1u << 22); it++) {
+#pragma unroll
+    for (int j = 0; j < 32; j++) v = fmaf(v, m, 1e-7f);
+    if (wall_clock64() - t0 > ticks) break;
+  }
+  if (v == 12345.0f) sink[threadIdx.x] = v;
+}
+
+static void busy_all_gpus(int ms) {
+  int n = 0;
+  HK(hipGetDeviceCount(&n));
+  std::vector<float*> sinks(n);
+  for (int d = 0; d < n; d++) {
+    HK(hipSetDevice(d));
+    HK(hipMalloc(&sinks[d], 1024 * sizeof(float)));
+    hipDeviceProp_t p;
+    HK(hipGetDeviceProperties(&p, d));
+    k_busy<<<p.multiProcessorCount * 8, 256>>>((uint64_t)ms * 100000ull, sinks[d]);
+    HK(hipGetLastError());
+  }
+  for (int d = 0; d < n; d++) {
+    HK(hipSetDevice(d));
+    HK(hipDeviceSynchronize());
+    HK(hipFree(sinks[d]));
+  }
+  HK(hipSetDevice(0));
+}
+
 static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_t spend[64],
-                             const std::vector<uint8_t>& labels, const Table& t) {
+                             const std::vector<uint8_t>& labels, const Table& t, int warm_ms = 0) {
   const int L = a.labels, T = a.threads;
   const uint64_t rows = t.rows;
   cudasp_tf_blob_arg a_scan{scan, 32, 1}, a_spend{spend, 64, 1};
@@ -272,6 +314,7 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
   std::atomic<uint64_t> next{0};
   std::vector<uint64_t> got;  // emitted row indices (from the txids)
   std::vector<double> t_calls(T, 0.0), t_final(T, 0.0), t_done(T, 0.0);
+  if (warm_ms) busy_all_gpus(warm_ms);
   const auto t0 = std::chrono::steady_clock::now();
   auto now_s = [&t0]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
   auto finish = [&](int th) {
@@ -411,8 +454,17 @@ int main(int argc, char** argv) {
   const QueryResult warm = run_query(a, scan, spend, labels, t);  // scanners, slots, tables
   std::vector<QueryResult> qs;
   for (int r = 0; r < a.reps; r++) qs.push_back(run_query(a, scan, spend, labels, t));
+  std::vector<double> warm_secs;
+  bool warm_exact = true;
+  for (int r = 0; r < a.warm_reps; r++) {
+    const QueryResult w = run_query(a, scan, spend, labels, t, a.warm_ms);
+    warm_secs.push_back(w.secs);
+    warm_exact = warm_exact && w.exact;
+  }
+  std::sort(warm_secs.begin(), warm_secs.end());
+  const double warm_med = warm_secs.empty() ? 0.0 : warm_secs[warm_secs.size() / 2];
   std::vector<double> secs;
-  bool all_exact = warm.exact;
+  bool all_exact = warm.exact && warm_exact;
   for (const auto& q : qs) {
     secs.push_back(q.secs);
     all_exact = all_exact && q.exact;
@@ -436,7 +488,8 @@ int main(int argc, char** argv) {
          "\"gpu_max_hw_queues_env\": \"%s\", \"launches\": %llu, \"rows_per_launch\": %.0f, "
          "\"harvest_wait_s\": %.4f, \"reserve_s\": %.4f, \"copy_s\": %.4f, \"launch_s\": %.4f, "
          "\"thread_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
-         "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f, \"streaming_feeds\": %u, \"logical_gpus\": %d}\n",
+         "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f, \"streaming_feeds\": %u, \"logical_gpus\": %d, "
+         "\"warm_reps\": %d, \"warm_ms\": %d, \"warm_seconds\": %.5f, \"warm_tx_per_s\": %.1f}\n",
          a.columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)t.rows, a.threads, (long long)a.batch,
          a.labels,
          a.kmax ? ("\"1.." + std::to_string(a.kmax) + "\"").c_str() : std::to_string(a.k).c_str(),
@@ -446,6 +499,7 @@ int main(int argc, char** argv) {
          q.stats.streams_per_feed, q.stats.max_streams_per_device, q.stats.hw_queues, hq ? hq : "",
          (unsigned long long)q.stats.launches, q.stats.launches ? (double)q.stats.rows / q.stats.launches : 0.0,
          q.stats.harvest_wait_s, q.stats.reserve_s, q.stats.copy_s, q.stats.launch_s, q.call_s_mean, q.final_s_mean, q.done_min, q.done_max,
-         q.stats.streaming_feeds, q.logical_gpus);
+         q.stats.streaming_feeds, q.logical_gpus, a.warm_reps, a.warm_ms, warm_med,
+         warm_med > 0 ? t.rows / warm_med : 0.0);
   return all_exact ? 0 : 2;
 }

@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--staged", action="store_true", help="stage every batch into device buffers by DMA (product path)")
     ap.add_argument("--device-results", action="store_true",
                     help="match rows into device memory too (same build)")
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="sleep this long (GPU idle) before every timed run of either kernel")
+    ap.add_argument("--prewarm", action="store_true",
+                    help="run k_scan_multi (untimed) right before every timed streaming run")
     ap.add_argument("--flags", action="store_true", help="also write per-row flags (the host path writes matches only)")
     a = ap.parse_args()
     import torch
@@ -67,6 +71,8 @@ def main():
         times = []
         for _ in range(a.reps):
             torch.cuda.synchronize()
+            if a.gap_ms:
+                time.sleep(a.gap_ms / 1e3)
             t = time.perf_counter()
             s.scan_device_batches(descs)
             s.sync()
@@ -92,6 +98,11 @@ def main():
                 for _ in range(a.reps + 1):
                     for sb in stage:
                         sb.reset()
+                    if a.gap_ms:
+                        time.sleep(a.gap_ms / 1e3)
+                    if a.prewarm:
+                        s.scan_device_batches(descs)
+                        s.sync()
                     t = time.perf_counter()
                     seqs = []
                     for sb, d in zip(stage, dev):
