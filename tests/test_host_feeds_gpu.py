@@ -153,7 +153,8 @@ def test_host_e2e_tool_config5_shape(torch, keys, tmp_path):  # noqa: F811
     16 distinct label keys (bench.label_keys), 1..15 outputs per row, 8
     executor threads, row chunks and Arrow columns: every query emits exactly
     the planted rows (base values on rows 0 mod 1000, label j = (g / 1000)
-    mod 16 on rows 1 mod 1000: all 16 label indices)."""
+    mod 16 on rows 1 mod 1000: all 16 label indices), also for a query started
+    right after a busy kernel (--warm-reps)."""
     import json
     exe = os.path.join(ROOT, "tools", "host_e2e")
     if not os.path.exists(exe):
@@ -162,7 +163,7 @@ def test_host_e2e_tool_config5_shape(torch, keys, tmp_path):  # noqa: F811
     lf.write_bytes(b"".join(keys[2]))
     for mode in ("rows", "columns"):
         cmd = [exe, "--rows", "700000", "--threads", "8", "--batch", "300000", "--labels", "16",
-               "--labels-file", str(lf), "--outputs-max", "15", "--input", mode]
+               "--labels-file", str(lf), "--outputs-max", "15", "--input", mode, "--warm-reps", "1"]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, (mode, r.stdout[-2000:], r.stderr[-2000:])
         res = json.loads(r.stdout.strip().splitlines()[-1])
@@ -170,6 +171,8 @@ def test_host_e2e_tool_config5_shape(torch, keys, tmp_path):  # noqa: F811
         assert res["matches"] == res["planted"] == 1400
         assert res["label_indices_planted"] == 16
         assert res["launches"] >= 3
+        # one more query right after a busy kernel on the GPU (bench's e2e_warm_tx_s); exit 0 covers its rows
+        assert res["warm_reps"] == 1 and res["warm_tx_per_s"] > 0
 
 
 def test_host_error_mid_query_then_pool_reuse(table16, keys):  # noqa: F811

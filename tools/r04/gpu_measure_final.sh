@@ -22,6 +22,7 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 e = d.get("e2e", {})
 print(sys.argv[1].split("/")[-1], "value %.1f M" % (d["value"] / 1e6), "kernel_ms %.2f ms_per_step %.2f" % (d["roofline"]["kernel_ms"], d["ms_per_step"]),
       "e2e %.1f M" % ((d.get("e2e_tx_s") or 0) / 1e6), "ratio %.3f" % ((d.get("e2e_tx_s") or 0) / d["value"]),
+      "like-for-like", d.get("e2e_vs_device"), "warm %.1f M" % ((d.get("e2e_warm_tx_s") or 0) / 1e6),
       "found %s" % d["matches"]["found"], "planted %s" % d["matches"]["expected_planted"], "e2e exact", e.get("emitted_equal_planted"), "e2e_launch %.1f M" % ((d.get("e2e_launch_tx_s") or 0) / 1e6), d.get("e2e_launch", {}).get("emitted_equal_planted"), "streaming_feeds", e.get("streaming_feeds"))
 PY
 }
