@@ -12,7 +12,7 @@ if [ "$1" != "notests" ]; then
 fi
 cd /tmp && export TMPDIR=/tmp
 rm -rf $O/prof_bench
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o bench -- python3 $R/bench.py --no-cpu-baseline --no-e2e --no-layout-probe --steps 3 --warmup 1 > $O/prof_bench.log 2>&1 || { echo prof failed; tail -20 $O/prof_bench.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o bench -- python3 $R/bench.py --no-cpu-baseline --no-e2e --no-layout-probe --idle-samples 0 --steps 3 --warmup 1 > $O/prof_bench.log 2>&1 || { echo prof failed; tail -20 $O/prof_bench.log; exit 1; }
 tail -1 $O/prof_bench.log | cut -c1-200
 cd $R
 python3 tools/prof_summary.py $(ls $O/prof_bench/*kernel_trace.csv $O/prof_bench/*/*kernel_trace.csv 2>/dev/null | head -1) --out $O/rocprof_bench_summary.json > $O/prof_summary.txt && head -20 $O/prof_summary.txt
