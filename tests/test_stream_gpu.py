@@ -148,6 +148,40 @@ def test_stream_slow_publisher(torch):
     flags_equal([sb.result() for sb in stage], want)
 
 
+def test_stream_publish_around_idle_exit(torch):
+    """Publishes that land while the kernel is leaving: 40 batches, each after
+    a pause drawn around the 20 ms idle time (0, 17..23 ms), some waited for
+    and some not -- the poller's idle exit, the host's relaunch and the
+    claim counter's reset to pub_wr race on every batch.  Every batch's
+    flags are the per-batch path's, and the query's counters account for
+    every wave-row exactly once."""
+    from cudasp_amd import Scanner, ScanStream
+    rng = np.random.default_rng(4020)
+    labels = [LABEL]
+    sizes = [int(x) for x in rng.integers(1, 3000, 40)]
+    batches = [tm.make_batch(torch, 91000 + 4000 * i, n) for i, n in enumerate(sizes)]
+    tm.plant(torch, batches, labels, every=11)
+    want = tm.run_per_batch(torch, batches, labels)
+    stage = [staged(b, 1) for b in batches]
+    pauses = rng.choice([0.0, 0.017, 0.019, 0.020, 0.021, 0.023], size=len(stage))
+    with Scanner(SCAN, SPEND, labels, max_rows=1000) as s, ScanStream(s) as st:
+        seqs = []
+        for i, sb in enumerate(stage):
+            time.sleep(float(pauses[i]))
+            seqs.append(sb.publish(st))
+            if i % 3 == 0:
+                st.wait(seqs[-1])
+        st.close_input()
+        for q in seqs:
+            st.wait(q)
+        st.finish()
+        c = st.counters()
+        launches = st.stats()["launches"]
+    assert c["wave_rows"] == sum((n + 63) // 64 for n in sizes)
+    assert launches >= 2  # some pauses outlasted the idle time
+    flags_equal([sb.result() for sb in stage], want)
+
+
 def test_stream_idle_kernel_releases_gpu(torch):
     """While a stream is open but the host publishes nothing, the kernel
     leaves after the idle time, so other work on the GPU runs (a kernel that
