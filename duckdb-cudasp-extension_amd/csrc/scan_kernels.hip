@@ -1221,7 +1221,9 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
   const uint32_t wid = threadIdx.x >> 6;
   volatile StreamWave& me = waves[wid];
   if (lane == 0) {
-    me.tk = me.tr = me.have = me.mine = 0;
+    // the first ticket: one wave-row, worker w's at first_wr + w (k_stream_start)
+    me.tk = dev_load_u64(&dev->first_wr) + (slot / 64u - 1u);
+    me.tr = me.have = me.mine = 1;
     me.t_start = wall_clock64();
     me.busy = me.pieces = me.rows = me.polls = me.drains = 0;
     me.t_p = me.t_q = me.t_old = 0;
@@ -2819,7 +2821,6 @@ struct cudasp_stream {
   bool running = false;     // a kernel was launched and `exited` recorded after it
   bool failed = false;      // a kernel of this query failed or a wait timed out (sticky until finish)
   bool abandoned = false;   // finish timed out with the kernel alive: nothing may be freed
-  bool next_launch_resets = false;  // a kernel of this query ran: the next one follows k_stream_relaunch
   bool counts_pending = false;      // finish queued the counters' copy; counters() waits for it
   uint64_t counts_waves = 0;        // wave slots of the last finished query's grid
   uint32_t next = 0;        // batches published
@@ -2844,12 +2845,18 @@ static bool stream_kernel_alive(cudasp_stream* st, int* err) {
   return false;
 }
 
-// Before a relaunch (same stream, after the idle kernel ended): the claim
-// counter back to the rows mirrored so far -- claims past them were never
-// processed (the idle kernel's pub_wr was final) -- and `idle` cleared.
-__global__ void k_stream_relaunch(StreamDev* dev) {
+// Before every launch (same stream; a relaunch follows the idle kernel's
+// end): the claim counter back to the rows mirrored so far -- claims past
+// them were never processed (the idle kernel's pub_wr was final) -- and
+// `idle` cleared.  Each worker's first ticket is one wave-row, worker w's at
+// first_wr + w, and the counter starts past them: the grid's ~3k first
+// claims would otherwise be same-address atomics that the L2 serializes
+// (~45 ns each, ~150 us before the last wave starts, profiles/r04_*).
+__global__ void k_stream_start(StreamDev* dev, uint32_t workers) {
   if (threadIdx.x == 0) {
-    dev->ticket = dev->pub_wr;
+    const uint64_t w0 = dev->pub_wr;
+    dev->first_wr = w0;
+    dev->ticket = w0 + workers;
     dev->idle = 0;
   }
 }
@@ -2873,7 +2880,8 @@ static int stream_launch(cudasp_stream* st) {
   }
   const uint32_t K = s->consts.output_count;
   const uint32_t rmax = std::max(1u, std::min(st->rmax, (uint32_t)MULTI_RMAX / K));
-  if (st->next_launch_resets) hipLaunchKernelGGL(k_stream_relaunch, dim3(1), dim3(64), 0, s->stream, st->dev);
+  hipLaunchKernelGGL(k_stream_start, dim3(1), dim3(64), 0, s->stream, st->dev,
+                     (uint32_t)st->blocks * (BLOCK / 64u) - 1u);  // every wave but the poller
   auto kf = s->fb_bits == 26 ? k_scan_stream<26> : k_scan_stream<22>;
   hipLaunchKernelGGL(kf, dim3((uint32_t)st->blocks), dim3(BLOCK), 0, s->stream, st->ctrl, st->dev, s->d_naf,
                      s->consts, s->d_fb, s->d_labels, s->d_mscratch, rmax, st->idle_ticks, st->wstat, st->prio_ticks, st->pf_coal);
@@ -2881,7 +2889,6 @@ static int stream_launch(cudasp_stream* st) {
   HIP_TRY(hipEventRecord(st->exited, s->stream));
   ST_HOST(102, st->blocks, (uint32_t)st->launches);
   st->running = true;
-  st->next_launch_resets = true;
   st->launches++;
   return CUDASP_OK;
 }
@@ -3244,7 +3251,6 @@ int cudasp_stream_finish(cudasp_stream* st) {
     // query's error stands; the stream is reset below for the next query
   }
   st->failed = false;
-  st->next_launch_resets = false;
   // Ready for the next query: the control block here, the device state and
   // the counters' copy queued on the scanner's stream (ordered before its
   // next launch; cudasp_stream_counters waits for the copy).

@@ -23,11 +23,12 @@
 //     which the host polls;
 //   * one poller wave per kernel reads the host's control block over PCIe
 //     (published count, descriptors, closed) and mirrors it into device
-//     memory; the worker waves take tickets of R wave-rows from one device
-//     counter (one atomicAdd while published rows are unclaimed: concurrent
-//     claims may pass the published rows, and such a ticket waits for the
-//     next batch) and look each wave-row's batch up in the mirror once, at
-//     the prefetch (the piece's pointers then live in LDS);
+//     memory; each worker wave's first ticket is one wave-row given by its
+//     index, the later ones R wave-rows from one device counter (one
+//     atomicAdd while published rows are unclaimed: concurrent claims may
+//     pass the published rows, and such a ticket waits for the next batch);
+//     a wave looks each wave-row's batch up in the mirror once, at the
+//     prefetch (the piece's pointers then live in LDS);
 //   * output_count K > 1 (K <= MULTI_RMAX): K hashes and K fixed-base points
 //     per row, K x R <= MULTI_RMAX per piece, the row's flag the OR;
 //   * the kernel is elastic: every wave leaves once the stream is closed and
@@ -35,7 +36,7 @@
 //     (CUDASP_STREAM_IDLE_MS, 100 MHz wall clock; every published row
 //     claimed, no new batch).  Rows past the mirrored pub_wr were never
 //     processed, so the host's next publish or wait relaunches the kernel
-//     with the claim counter reset to pub_wr (k_stream_relaunch).  A host
+//     with the claim counter reset to pub_wr (k_stream_start).  A host
 //     that stalls (a slow source, or executor threads busy elsewhere) never
 //     holds the GPU, and a host that never closes leaves no kernel spinning.
 // Pieces and the pipelined schedule are k_scan_multi's (one inversion per
@@ -91,6 +92,8 @@ struct StreamCtrl {
 // claims and polls touch device memory only, never PCIe.
 struct StreamDev {
   uint64_t ticket;                  // wave-rows handed out to the workers
+  uint64_t first_wr;                // this launch's first wave-row: worker w's first ticket is
+                                    // [first_wr + w, +1), handed out without an atomic (k_stream_start)
   uint64_t pub_wr;                  // mirror of StreamCtrl::published_wr
   uint32_t pub;                     // mirror of StreamCtrl::published
   uint32_t closed;                  // mirror of StreamCtrl::closed (set after the last pub)

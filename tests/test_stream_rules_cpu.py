@@ -120,8 +120,9 @@ def test_idle_exit_and_relaunch_process_every_row_once():
     """The elastic protocol replayed with random interleavings: waves claim
     with a single fetch-and-add while published rows are unclaimed (so
     concurrent claims pass pub_wr), process only the published part of a
-    ticket, and drop the rest when the poller declares the kernel idle; the
-    relaunch resets the claim counter to the mirrored pub_wr.  Over many
+    ticket, and drop the rest when the poller declares the kernel idle; every
+    launch hands worker w its first ticket at the mirrored pub_wr + w and
+    starts the claim counter past those.  Over many
     publish / stall / relaunch cycles every published wave-row is processed
     exactly once and nothing past the published rows ever is."""
     rng = random.Random(11)
@@ -134,11 +135,12 @@ def test_idle_exit_and_relaunch_process_every_row_once():
         launches = 0
         for cycle in range(rng.randint(1, 8)):
             host_wr += rng.randint(1, 60)
-            # relaunch: k_stream_relaunch resets the claim counter
-            ticket = pub_wr
+            # (re)launch: k_stream_start resets the claim counter past the
+            # workers' first tickets, one wave-row each at pub_wr + w
+            ticket = pub_wr + nwaves
             launches += 1
-            waves = [None] * nwaves      # (tk, tr) tickets
-            mine = [0] * nwaves
+            waves = [(pub_wr + w, 1) for w in range(nwaves)]      # (tk, tr) tickets
+            mine = [1] * nwaves
             idle = False
             steps = 0
             while True:
