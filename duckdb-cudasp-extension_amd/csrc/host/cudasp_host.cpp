@@ -70,10 +70,13 @@ constexpr int FEED_MAX_STREAMS = 4;
 // tx/s with 8 slots in flight, 164.0 with 16, 166.6 with all published;
 // profiles/r03_stream_iter2.txt).
 constexpr int FEED_STREAM_SLOTS = 16;
-// CUDASP_TF_STREAM_SLOTS overrides it, up to 48 (well inside the stream's
-// 64-entry descriptor ring: a done slot is harvested long before its ring
-// entry can be reused).
+// CUDASP_TF_STREAM_SLOTS overrides it, up to 48, inside the stream's
+// descriptor ring: at most STREAM_RING batches may be published and not yet
+// harvested (include/cudasp_abi.h, cudasp_stream_publish_batch and
+// cudasp_stream_matches), which ring_overdue_locked enforces even when slots
+// are reused out of order.
 constexpr int FEED_MAX_STREAM_SLOTS = 48;
+constexpr uint64_t STREAM_RING = 64;
 constexpr int FEED_MAX_SLOTS = FEED_MAX_STREAM_SLOTS;
 static_assert(FEED_MAX_SLOTS >= FEED_MAX_STREAMS + 2, "per-slot launch feeds");
 
@@ -104,6 +107,7 @@ double now_s() {
 
 extern "C" void cudasp_internal_set_error(const char* msg);
 extern "C" void* cudasp_internal_scanner_stream(cudasp_scanner* s);
+extern "C" void cudasp_internal_clear_key_cache(void);
 #if CUDASP_STREAM_TRACE
 extern "C" void cudasp_internal_trace_host(uint32_t kind, uint64_t a, uint32_t b);
 #define ST_HOST(...) cudasp_internal_trace_host(__VA_ARGS__)
@@ -214,6 +218,8 @@ struct FeedSlot {
   int writers = 0;       // reservations still copying
   int stream = 0;        // stream (scanner) of its launch
   uint64_t seq = 0;      // streaming feed: the batch's sequence number in the stream
+  bool in_ring = false;  // streaming feed: published and not yet harvested (its seq holds a ring entry)
+  double t_pub = 0;      // when it was published (the late-batch test hook)
 };
 
 // The GPU resources of a device feed, kept in a process-wide pool between
@@ -435,6 +441,12 @@ struct Feed {
   int ramp = 3;          // ramp slots (close_at); CUDASP_TF_RAMP=N sets them, 0 turns the ramp off
   bool upload_null = true;  // H2D on the null stream; CUDASP_TF_UPLOAD=stream: on the scan stream (A/B)
   uint32_t closed = 0;   // slots closed so far
+  uint64_t pub_next = 0;  // streaming feed: one past the highest sequence number published
+  // test hook (CUDASP_TF_TEST_LATE_SEQ / _MS): batch late_seq reads as not
+  // done to the non-blocking checks for late_s after its publish, so the ring
+  // moves on without it (a starved batch; a blocking harvest still takes it)
+  int64_t late_seq = -1;
+  double late_s = 0;
   int error = CUDASP_OK;
   std::string error_msg;
   std::mutex stream_mu[FEED_MAX_STREAMS];  // a scanner's host state is not re-entrant
@@ -583,6 +595,11 @@ int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
     s.state = SLOT_LAUNCHED;
     f.launches++;
     f.rows += n;
+    if (r.stream) {
+      s.in_ring = true;
+      s.t_pub = now_s();
+      f.pub_next = std::max(f.pub_next, s.seq + 1);
+    }
   }
   f.cv.notify_all();
   return rc;
@@ -646,6 +663,7 @@ int harvest_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   }
   lk.lock();
   f.harvest_wait_s += waited;
+  s.in_ring = false;
   s.state = SLOT_FREE;
   f.cv.notify_all();
   if (e != hipSuccess)
@@ -691,7 +709,10 @@ uint32_t stream_timeout_ms() {
 
 // Whether a launched slot's batch is done (no waiting).
 bool slot_done(Feed& f, FeedSlot& s) {
-  if (f.res->stream) return cudasp_stream_query(f.res->stream, s.seq) == 1;
+  if (f.res->stream) {
+    if (f.late_seq >= 0 && s.seq == (uint64_t)f.late_seq && now_s() - s.t_pub < f.late_s) return false;
+    return cudasp_stream_query(f.res->stream, s.seq) == 1;
+  }
   DeviceSet dg(f.res->device);
   return hipEventQuery(s.done) == hipSuccess;
 }
@@ -701,9 +722,8 @@ bool slot_done(Feed& f, FeedSlot& s) {
 // (-1: none).  Slots are taken out of order, so a batch held up by a slow
 // wave-row occupies its slot alone instead of stalling the whole ring (a
 // streaming kernel's youngest waves get few issue slots: one batch of the
-// 9.4M-row table finished 27 ms after it was published).  A done slot is
-// reached within one pass of the ring, long before its match count could be
-// overwritten (STREAM_RING = 64 batches later).
+// 9.4M-row table finished 27 ms after it was published).  Out-of-order reuse
+// is bounded by ring_overdue_locked, checked before every slot opens.
 int ready_slot_locked(Feed& f) {
   const int n = f.res->nslots();
   for (int i = 1; i < n; i++) {
@@ -712,6 +732,28 @@ int ready_slot_locked(Feed& f) {
     if (t.state == SLOT_FREE || (t.state == SLOT_LAUNCHED && slot_done(f, t))) return k;
   }
   return -1;
+}
+
+// Streaming feed: the slot holding the oldest published, unharvested batch
+// if opening another slot could let the stream run STREAM_RING batches past
+// it (-1 otherwise).  Every batch published after this open comes from a
+// slot opened by now or later, at most nslots of which are unpublished, so
+// requiring pub_next + nslots - oldest < STREAM_RING at every open keeps
+// each publish within STREAM_RING of the oldest batch not yet harvested:
+// publish never finds its ring entry's previous batch undone
+// (CUDASP_ERR_CAPACITY) and a late batch's match count is read before its
+// entry is reused (cudasp_stream_matches).  The caller then harvests that
+// slot first, however long its batch takes.
+int ring_overdue_locked(Feed& f) {
+  if (!f.res->stream) return -1;
+  const int n = f.res->nslots();
+  int k = -1;
+  for (int i = 0; i < n; i++) {
+    const FeedSlot& t = f.res->slots[i];
+    if (t.in_ring && (k < 0 || t.seq < f.res->slots[k].seq)) k = i;
+  }
+  if (k < 0) return -1;
+  return f.pub_next + (uint64_t)n - f.res->slots[k].seq >= STREAM_RING ? k : -1;
 }
 
 struct Reservation {
@@ -732,6 +774,17 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
     FeedSlot& s = r.slots[f.open];
     switch (s.state) {
       case SLOT_FREE: {
+        const int overdue = ring_overdue_locked(f);
+        if (overdue >= 0) {
+          FeedSlot& o = r.slots[overdue];
+          if (o.state == SLOT_LAUNCHED) {
+            const int rc = harvest_locked(f, o, lk);
+            if (rc != CUDASP_OK) return rc;
+          } else {
+            f.cv.wait(lk);  // another thread is harvesting it
+          }
+          continue;
+        }
         const size_t want_words = std::max(
             std::min((size_t)(f.words_per_row * r.cap_rows), (size_t)UINT32_MAX * f.ow), nwords);
         const size_t want_tx = std::max((size_t)(f.txid_per_row * r.cap_rows), ntx);
@@ -894,7 +947,8 @@ int feeds_flush(cudasp_tf_global& g) {
     DeviceSet dg(fp->res->device);
     const int r2 = cudasp_stream_finish(fp->res->stream);
     if (r2 != CUDASP_OK && rc == CUDASP_OK) rc = feed_fail(*fp, host_fail(r2, "%s", cudasp_last_error()));
-    free_stale(*fp->res);
+    // an abandoned kernel may still read the outgrown buffers: feeds_release leaks them
+    if (!cudasp_stream_abandoned(fp->res->stream)) free_stale(*fp->res);
   }
   return rc;
 }
@@ -981,6 +1035,11 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
   }
   if (r->stream) (void)cudasp_stream_set_timeout(r->stream, stream_timeout_ms());
   auto f = std::make_unique<Feed>();
+  if (const char* e = getenv("CUDASP_TF_TEST_LATE_SEQ")) {
+    f->late_seq = atoll(e);
+    const char* ms = getenv("CUDASP_TF_TEST_LATE_MS");
+    f->late_s = 1e-3 * (ms ? atof(ms) : 1000.0);
+  }
   f->res = r;
   f->g = &g;
   f->batch_size = b.batch_size;
@@ -1280,6 +1339,7 @@ void feeds_release(cudasp_tf_global& g) {
         while (s.state == SLOT_CLOSED || s.state == SLOT_BUSY) f.cv.wait(lk);
         s.state = SLOT_FREE;
         s.writers = 0;
+        s.in_ring = false;
       }
     }
     // The resources go back to the pool when the device is done with them
@@ -1296,6 +1356,15 @@ void feeds_release(cudasp_tf_global& g) {
       if (r->stream) {
         (void)cudasp_stream_set_timeout(r->stream, std::max<uint32_t>(stream_timeout_ms(), 60000u));
         ok = cudasp_stream_finish(r->stream) == CUDASP_OK;
+        if (cudasp_stream_abandoned(r->stream)) {
+          // its kernel may still run, reading the slots and writing the
+          // scanner's scratch: free nothing and wait for nothing (a scanner
+          // sync would wait on that kernel, possibly forever) -- release_res
+          // leaks the feed
+          fp.reset();
+          release_res(r);
+          continue;
+        }
         free_stale(*r);
       }
       for (int k = 0; k < r->nstreams; k++) ok = cudasp_scanner_sync(r->scanners[k]) == CUDASP_OK && ok;
@@ -1553,6 +1622,8 @@ void cudasp_tf_release_pool(void) {
     all.swap(g_pool);
   }
   for (FeedRes* r : all) release_res(r);
+  // the pool held the last queries' keys: drop the cached scan-key digits too
+  cudasp_internal_clear_key_cache();
 }
 
 uint32_t cudasp_tf_pool_size(void) {

@@ -796,14 +796,6 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_tick
       uint64_t pub_wr = 0;
       uint32_t b = seen;
       for (; b != pub; b++) {
-        // a staged batch is mirrored only once its DMA copies are done
-        // (cudasp_stream_publish_batch sets ready[e] from the copy stream's
-        // completion); batches go out in order
-        if (sys_load_u32(&ctrl->desc[b % STREAM_RING].staged)) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (sys_load_u32(&ctrl->ready[b % STREAM_RING]) != b + 1u) break;
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
         const uint64_t* src = reinterpret_cast<const uint64_t*>(&ctrl->desc[b % STREAM_RING]);
         StreamBatch* de = &dev->desc[b % STREAM_RING];
         uint64_t* dst = reinterpret_cast<uint64_t*>(de);
@@ -840,9 +832,6 @@ __device__ void stream_poll(StreamCtrl* ctrl, StreamDev* dev, uint64_t idle_tick
         seen = b;
         last = now;
       }
-      // (a batch still waiting for its copies does not keep the kernel from
-      // going idle: if the copy engine needed this kernel's compute units,
-      // holding them would never let it finish)
     }
     if (cl && seen == pub) {  // `published` was read after `closed`: every batch is mirrored
       __hip_atomic_store(&dev->closed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1034,16 +1023,19 @@ __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, 
     }
     // the outputs: runs of wave-rows of one batch whose lists span at most
     // 48 words per lane are copied by the whole wave; anything else (a
-    // scattered CSR) lane by lane.  A batch whose outputs are already in
-    // device memory (mirror == outputs: staged by DMA) needs no copy.
-    bool staged = true;
+    // scattered CSR) lane by lane.
+#ifdef CUDASP_AB_STREAM_ANY_MEMORY
+    // measurement builds only (tools/stream_probe.py --device-inputs): a
+    // batch whose outputs already are its device mirror needs no copy
+    bool resident = true;
 #pragma unroll
     for (int i = 0; i < 3; i++)
-      if (g + i < count) staged = staged && wr[g + i].mirror == pf[g + i].outputs;
-#ifdef CUDASP_AB_NO_OUTCOPY
-    staged = true;  // measurement only: compares read a stale mirror
+      if (g + i < count) resident = resident && wr[g + i].mirror == pf[g + i].outputs;
+    if (resident) continue;
 #endif
-    if (staged) continue;
+#ifdef CUDASP_AB_NO_OUTCOPY
+    continue;  // measurement only: compares read a stale mirror
+#endif
     uint32_t lo = ~0u, hi = 0;
     int i0 = 0;
 #pragma unroll
@@ -1924,6 +1916,7 @@ void free_scanner(cudasp_scanner* s) {
   for (hipEvent_t e : s->multi_copied)
     if (e) (void)hipEventDestroy(e);
   if (s->stream) (void)hipStreamDestroy(s->stream);
+  if (!s->keys.empty()) wipe_bytes(s->keys.data(), s->keys.size());  // the scan private key
   delete s;
 }
 
@@ -2251,6 +2244,8 @@ void cudasp_internal_set_error(const char* msg) { g_last_error = msg ? msg : "";
 // The table-function host's device feeds launch each batch's copies and
 // kernels on the stream of the scanner that scans it; not public either.
 void* cudasp_internal_scanner_stream(cudasp_scanner* s) { return s ? (void*)s->stream : nullptr; }
+// Wipe the process-wide scan-key digit cache (cudasp_tf_release_pool).
+void cudasp_internal_clear_key_cache(void) { scan_digits_cache_clear(); }
 
 const char* cudasp_version(void) { return CUDASP_VERSION_STRING; }
 
@@ -2420,6 +2415,7 @@ int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32
     keys.insert(keys.end(), spend_public_key, spend_public_key + 64);
     if (raw_label_count) keys.insert(keys.end(), label_keys, label_keys + 64 * (size_t)raw_label_count);
     s->keys.swap(keys);
+    if (!keys.empty()) wipe_bytes(keys.data(), keys.size());  // the previous scan key
     s->raw_label_count = raw_label_count;
   }
   return CUDASP_OK;
@@ -2791,17 +2787,6 @@ static bool host_range_coherent(const void* p, size_t bytes) {
 
 constexpr uint32_t STREAM_MAX_WAVES = MAX_BLOCKS * (BLOCK / 64);
 
-// A staged batch's readiness, set from the copy stream once its DMA copies
-// are done (hipLaunchHostFunc: a runtime thread stores, no HIP call).
-struct StreamReadyArg {
-  StreamCtrl* ctrl;
-  uint32_t e, v;
-};
-static void stream_ready_cb(void* p) {
-  const StreamReadyArg* a = static_cast<const StreamReadyArg*>(p);
-  __atomic_store_n(&a->ctrl->ready[a->e], a->v, __ATOMIC_RELEASE);
-}
-
 struct cudasp_stream {
   cudasp_scanner* s = nullptr;
   StreamCtrl* ctrl = nullptr;  // coherent pinned host memory (same address on the device)
@@ -2816,8 +2801,6 @@ struct cudasp_stream {
   uint32_t pf_coal = 1;     // row blobs read lane-contiguously + LDS transpose (stream_prefetch)
   uint32_t timeout_ms = 0;  // waits fail after this long without progress (cudasp_stream_set_timeout)
   hipEvent_t exited = nullptr;
-  hipStream_t copy = nullptr;             // staged batches' DMA copies (created at the first one)
-  StreamReadyArg ready_arg[STREAM_RING];  // their completion callbacks' arguments
   bool running = false;     // a kernel was launched and `exited` recorded after it
   bool failed = false;      // a kernel of this query failed or a wait timed out (sticky until finish)
   bool abandoned = false;   // finish timed out with the kernel alive: nothing may be freed
@@ -3013,24 +2996,19 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
 int cudasp_stream_publish_batch(cudasp_stream* st, const cudasp_stream_batch* bt, uint64_t* seq) {
   if (!st || !bt) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
   const uint32_t n = bt->n;
-  const bool staged = bt->d_tweak_keys != nullptr;
   if (n == 0 || !bt->tweak_keys || !bt->output_offsets || !bt->output_lengths || !bt->d_mirror)
     return set_error(CUDASP_ERR_INVALID_ARG, "empty batch or null buffer (the outputs mirror included)");
   if (!bt->match_flags && !bt->match_rows)
     return set_error(CUDASP_ERR_INVALID_ARG, "a streamed batch needs match_flags and/or match_rows");
-  if (staged && (!bt->d_output_offsets || !bt->d_output_lengths || (bt->output_words && !bt->outputs)))
-    return set_error(CUDASP_ERR_INVALID_ARG, "a staged batch needs device offsets and lengths buffers");
   // every host buffer the kernel touches must be coherent pinned memory
-  // (cudasp_host_alloc): the result buffers always, the inputs unless the
-  // batch is staged by DMA; the outputs list is checked at its start (its
-  // rows' offsets and lengths, like every CSR this library takes, are the
-  // caller's)
+  // (cudasp_host_alloc), inputs and results; the outputs list is checked at
+  // its start (its rows' offsets and lengths, like every CSR this library
+  // takes, are the caller's)
   if ((bt->match_flags && !host_range_coherent(bt->match_flags, n)) ||
       (bt->match_rows && !host_range_coherent(bt->match_rows, (size_t)n * 4)) ||
-      (!staged && (!host_range_coherent(bt->output_offsets, (size_t)n * 4) ||
-                   !host_range_coherent(bt->output_lengths, (size_t)n * 4) ||
-                   !host_range_coherent(bt->tweak_keys, (size_t)n * 64) ||
-                   (bt->outputs && !host_range_coherent(bt->outputs, 8)))))
+      !host_range_coherent(bt->output_offsets, (size_t)n * 4) ||
+      !host_range_coherent(bt->output_lengths, (size_t)n * 4) ||
+      !host_range_coherent(bt->tweak_keys, (size_t)n * 64) || (bt->outputs && !host_range_coherent(bt->outputs, 8)))
     return set_error(CUDASP_ERR_INVALID_ARG, "streamed batch buffers must come from cudasp_host_alloc");
   std::lock_guard<std::mutex> lk(st->mu);
   if (st->ctrl->closed) return set_error(CUDASP_ERR_INVALID_ARG, "stream already closed");
@@ -3040,34 +3018,17 @@ int cudasp_stream_publish_batch(cudasp_stream* st, const cudasp_stream_batch* bt
   if (b >= STREAM_RING && !stream_seq_done(st, (uint64_t)b - STREAM_RING))
     return set_error(CUDASP_ERR_CAPACITY, "more than %u streamed batches in flight", STREAM_RING);
   StreamBatch& d = st->ctrl->desc[e];
-  if (staged) {
-    DeviceGuard g(st->s->device);
-    if (!st->copy) HIP_TRY(hipStreamCreateWithFlags(&st->copy, hipStreamNonBlocking));
-    __atomic_store_n(&st->ctrl->ready[e], 0u, __ATOMIC_RELAXED);
-    HIP_TRY(hipMemcpyAsync(bt->d_tweak_keys, bt->tweak_keys, (size_t)n * 64, hipMemcpyHostToDevice, st->copy));
-    HIP_TRY(hipMemcpyAsync(bt->d_output_offsets, bt->output_offsets, (size_t)n * 4, hipMemcpyHostToDevice, st->copy));
-    HIP_TRY(hipMemcpyAsync(bt->d_output_lengths, bt->output_lengths, (size_t)n * 4, hipMemcpyHostToDevice, st->copy));
-    if (bt->output_words)
-      HIP_TRY(hipMemcpyAsync(bt->d_mirror, bt->outputs, bt->output_words * 8, hipMemcpyHostToDevice, st->copy));
-    st->ready_arg[e] = StreamReadyArg{st->ctrl, e, b + 1u};
-    HIP_TRY(hipLaunchHostFunc(st->copy, stream_ready_cb, &st->ready_arg[e]));
-    d.rows = bt->d_tweak_keys;
-    d.outputs = bt->d_mirror;
-    d.offs = bt->d_output_offsets;
-    d.lens = bt->d_output_lengths;
-  } else {
-    d.rows = bt->tweak_keys;
-    d.outputs = bt->outputs;
-    d.offs = bt->output_offsets;
-    d.lens = bt->output_lengths;
-  }
+  d.rows = bt->tweak_keys;
+  d.outputs = bt->outputs;
+  d.offs = bt->output_offsets;
+  d.lens = bt->output_lengths;
   d.flags = bt->match_flags;
   d.matches = bt->match_rows;
   d.mirror = bt->d_mirror;
   d.n = n;
   d.nwr = (n + 63u) / 64u;
-  d.staged = staged ? 1u : 0u;
-  d.reserved = 0;
+  d.reserved0 = 0;
+  d.reserved1 = 0;
   d.first_wr = st->published_wr;
   d.seq = b;
   st->published_wr += d.nwr;
@@ -3092,10 +3053,6 @@ int cudasp_stream_publish(cudasp_stream* st, const uint8_t* rows, const int64_t*
   b.match_flags = flags;
   b.match_rows = nullptr;
   b.d_mirror = d_mirror;
-  b.d_tweak_keys = nullptr;
-  b.d_output_offsets = nullptr;
-  b.d_output_lengths = nullptr;
-  b.output_words = 0;
   if (!flags) return set_error(CUDASP_ERR_INVALID_ARG, "null flags buffer");
   return cudasp_stream_publish_batch(st, &b, seq);
 }
@@ -3255,7 +3212,6 @@ int cudasp_stream_finish(cudasp_stream* st) {
   // the counters' copy queued on the scanner's stream (ordered before its
   // next launch; cudasp_stream_counters waits for the copy).
   const bool ran = st->next > 0;
-  if (st->copy) (void)hipStreamSynchronize(st->copy);  // every staged batch's callback has run
   memset(st->ctrl, 0, sizeof(StreamCtrl));
   st->next = 0;
   st->published_wr = 0;
@@ -3322,10 +3278,6 @@ void cudasp_stream_destroy(cudasp_stream* st) {
   if (st->ctrl) cudasp_host_free(st->ctrl);
   DeviceGuard g(st->s->device);
   if (st->s->stream) (void)hipStreamSynchronize(st->s->stream);
-  if (st->copy) {
-    (void)hipStreamSynchronize(st->copy);
-    (void)hipStreamDestroy(st->copy);
-  }
   if (st->dev) (void)hipFree(st->dev);
   if (st->wstat) (void)hipFree(st->wstat);
   if (st->h_counts) (void)hipHostFree(st->h_counts);

@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -148,30 +149,95 @@ inline std::vector<uint32_t> fb_window_bases(int bits = FB_BITS) {
   return bases;
 }
 
-// scan_digits of scan key d through a small process-wide cache: the search
-// over ~290 GLV decompositions costs ~0.3 ms of host time per key, paid at
-// every query's bind otherwise (a wallet's key is scanned query after query).
-inline bool scan_digits_cached(const host::Big<8>& d, std::vector<int8_t>& naf, uint32_t* naf_len) {
+// Overwrite memory that held key material (not optimised away).
+inline void wipe_bytes(void* p, size_t n) {
+  volatile uint8_t* v = static_cast<volatile uint8_t*>(p);
+  for (size_t i = 0; i < n; i++) v[i] = 0;
+}
+
+// A small process-wide cache of scan_digits: the search over ~290 GLV
+// decompositions costs ~0.3 ms of host time per key, paid at every new
+// scanner's bind otherwise (a wallet's key is scanned query after query).
+// The key itself is not stored: entries are found by SHA-256(salt || d) with
+// a per-process random salt, compared in constant time.  The digits are
+// equivalent to the key, so entries are wiped on eviction and by
+// scan_digits_cache_clear (cudasp_tf_release_pool, library unload).
+struct ScanDigitsCache {
   struct Entry {
-    host::Big<8> d;
+    uint8_t tag[32];
     std::vector<int8_t> naf;
     uint32_t len;
   };
-  static std::mutex mu;
-  static std::vector<Entry> cache;  // most recent last, at most 16
-  {
+  std::mutex mu;
+  std::vector<Entry> entries;  // most recent last, at most 16
+  uint8_t salt[32];
+  ScanDigitsCache() {
+    std::random_device rd;
+    for (int i = 0; i < 32; i += 4) {
+      const uint32_t v = rd();
+      memcpy(salt + i, &v, 4);
+    }
+  }
+  ~ScanDigitsCache() { clear(); }
+  static void wipe(Entry& e) {
+    wipe_bytes(e.tag, sizeof(e.tag));
+    if (!e.naf.empty()) wipe_bytes(e.naf.data(), e.naf.size());
+    e.len = 0;
+  }
+  void clear() {
     std::lock_guard<std::mutex> lk(mu);
-    for (size_t i = 0; i < cache.size(); i++)
-      if (memcmp(cache[i].d.w, d.w, sizeof(d.w)) == 0) {
-        naf = cache[i].naf;
-        *naf_len = cache[i].len;
-        return true;
-      }
+    for (Entry& e : entries) wipe(e);
+    entries.clear();
+  }
+  void tag_of(const host::Big<8>& d, uint8_t tag[32]) const {
+    uint8_t buf[64];
+    memcpy(buf, salt, 32);
+    for (int i = 0; i < 8; i++) memcpy(buf + 32 + 4 * i, &d.w[i], 4);
+    sha256_bytes(tag, buf, sizeof(buf));
+    wipe_bytes(buf, sizeof(buf));
+  }
+  static bool tag_eq(const uint8_t* a, const uint8_t* b) {
+    uint8_t x = 0;
+    for (int i = 0; i < 32; i++) x |= a[i] ^ b[i];
+    return x == 0;
+  }
+};
+
+inline ScanDigitsCache& scan_digits_cache() {
+  static ScanDigitsCache c;
+  return c;
+}
+
+inline void scan_digits_cache_clear() { scan_digits_cache().clear(); }
+
+inline bool scan_digits_cached(const host::Big<8>& d, std::vector<int8_t>& naf, uint32_t* naf_len) {
+  ScanDigitsCache& c = scan_digits_cache();
+  uint8_t tag[32];
+  c.tag_of(d, tag);
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    int hit = -1;
+    for (size_t i = 0; i < c.entries.size(); i++)  // every entry compared: no early exit on the key
+      if (ScanDigitsCache::tag_eq(c.entries[i].tag, tag)) hit = (int)i;
+    if (hit >= 0) {
+      naf = c.entries[hit].naf;
+      *naf_len = c.entries[hit].len;
+      wipe_bytes(tag, sizeof(tag));
+      return true;
+    }
   }
   if (host::scan_digits(d, naf.data(), NAF_MAX, naf_len) != 0) return false;
-  std::lock_guard<std::mutex> lk(mu);
-  if (cache.size() >= 16) cache.erase(cache.begin());
-  cache.push_back(Entry{d, naf, *naf_len});
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (c.entries.size() >= 16) {
+    ScanDigitsCache::wipe(c.entries.front());
+    c.entries.erase(c.entries.begin());
+  }
+  ScanDigitsCache::Entry e;
+  memcpy(e.tag, tag, 32);
+  e.naf = naf;
+  e.len = *naf_len;
+  c.entries.push_back(std::move(e));
+  wipe_bytes(tag, sizeof(tag));
   return true;
 }
 

@@ -45,7 +45,17 @@
 // (host + device; tests/test_stream_rules_cpu.py replays them and the ring
 // lookup); the kernel is in scan_kernels.hip.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
+
+// The kernel's host/device ordering (the poller's write-through descriptor
+// stores ordered by vmcnt waits, the done word behind a system-scope release)
+// rests on gfx950's memory model and cache-policy bits, and
+// tests/test_stream_isa_cpu.py checks the generated code for exactly that
+// target: any other one must be re-verified before it is built.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "the streaming scan's ordering protocol is verified for gfx950 only (tests/test_stream_isa_cpu.py)"
+#endif
 
 #include "secp256k1_fe.hpp"  // CUDASP_HD
 
@@ -68,8 +78,8 @@ struct StreamBatch {
   int64_t* mirror;          // device copy of the outputs the compares read
   uint32_t n;
   uint32_t nwr;             // wave-rows: ceil(n / 64)
-  uint32_t staged;          // 1: the pointers are device copies made by DMA; mirror once ctrl->ready says so
-  uint32_t reserved;
+  uint32_t reserved0;
+  uint32_t reserved1;
   uint64_t first_wr;        // wave-rows published before this batch
   uint64_t seq;             // the batch's sequence number (tells a reused ring entry)
 };
@@ -82,7 +92,6 @@ struct StreamCtrl {
   uint32_t reserved;
   uint32_t done[STREAM_RING];       // ring entry e: 1 + sequence number of the last batch completed there (kernel)
   uint32_t nmatch[STREAM_RING];     // matching rows of that batch (kernel; written before `done`)
-  uint32_t ready[STREAM_RING];      // staged batch: 1 + its sequence number once its DMA copies are done (host)
   StreamBatch desc[STREAM_RING];    // batch b at entry b % STREAM_RING
 };
 

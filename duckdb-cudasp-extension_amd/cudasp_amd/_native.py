@@ -122,9 +122,7 @@ class DeviceBatch(ctypes.Structure):
 class StreamBatchDesc(ctypes.Structure):
     """cudasp_stream_batch (include/cudasp_abi.h)."""
     _fields_ = [("tweak_keys", _P), ("outputs", _P), ("output_offsets", _P), ("output_lengths", _P),
-                ("n", _U32), ("match_flags", _P), ("match_rows", _P), ("d_mirror", _P),
-                ("d_tweak_keys", _P), ("d_output_offsets", _P), ("d_output_lengths", _P),
-                ("output_words", ctypes.c_size_t)]
+                ("n", _U32), ("match_flags", _P), ("match_rows", _P), ("d_mirror", _P)]
 
 
 class ScanOptions(ctypes.Structure):

@@ -247,20 +247,15 @@ class ScanStream:
         _native.check(self._lib.cudasp_stream_create(scanner._h, int(blocks), ctypes.byref(h)))
         self._h = h
 
-    def publish(self, rows, outputs, offsets, lengths, n, flags, mirror=None, matches=None, stage=None,
-                output_words=0):
+    def publish(self, rows, outputs, offsets, lengths, n, flags, mirror=None, matches=None):
         """rows / outputs / offsets / lengths / flags / matches: HostBuffers
-        (or their addresses; flags or matches may be None); mirror: a device
-        tensor of the batch's outputs size.  stage: None (the kernel reads the
-        host buffers in place) or device tensors (rows, offsets, lengths) the
-        batch is copied into by DMA first, with output_words outputs words
-        copied into the mirror.  Returns the batch's sequence number."""
+        (or their addresses; flags or matches may be None) that the kernel
+        reads and writes in place; mirror: a device tensor of the batch's
+        outputs size.  Returns the batch's sequence number."""
         seq = ctypes.c_uint64()
         addr = lambda b: None if b is None else (b.ptr if isinstance(b, HostBuffer) else int(b))  # noqa: E731
-        st = [None, None, None] if stage is None else [t.data_ptr() for t in stage]
         d = _native.StreamBatchDesc(addr(rows), addr(outputs), addr(offsets), addr(lengths), int(n), addr(flags),
-                                    addr(matches), None if mirror is None else mirror.data_ptr(), st[0], st[1],
-                                    st[2], int(output_words) if stage is not None else 0)
+                                    addr(matches), None if mirror is None else mirror.data_ptr())
         _native.check(self._lib.cudasp_stream_publish_batch(self._h, ctypes.byref(d), ctypes.byref(seq)))
         return seq.value
 
@@ -332,7 +327,7 @@ class StreamBatch:
     the outputs the kernel's compares read."""
 
     def __init__(self, tweak_keys, outputs, offsets, lengths, label_count=0, device=0, full_x=False,
-                 want_flags=True, want_matches=True, staged=False):
+                 want_flags=True, want_matches=True):
         tk = np.ascontiguousarray(tweak_keys, dtype=np.uint8).reshape(-1, 64)
         self.n = tk.shape[0]
         outs = (np.ascontiguousarray(outputs, dtype=np.uint8).reshape(-1) if full_x
@@ -353,17 +348,11 @@ class StreamBatch:
         dev = torch.device("cuda", device)
         self.mirror = torch.empty((max(1, outs.nbytes // 8),), dtype=torch.int64, device=dev)
         self.output_words = outs.nbytes // 8
-        # DMA staging buffers (cudasp_stream_batch.d_*): the kernel reads HBM
-        self.stage = None
-        if staged:
-            self.stage = (torch.empty((max(1, self.n) * 64,), dtype=torch.uint8, device=dev),
-                          torch.empty((max(1, self.n),), dtype=torch.int32, device=dev),
-                          torch.empty((max(1, self.n),), dtype=torch.int32, device=dev))
         self.seq = None
 
     def publish(self, stream):
         self.seq = stream.publish(self.rows, self.outputs, self.offsets, self.lengths, self.n, self.flags,
-                                  self.mirror, self.match_rows, self.stage, self.output_words)
+                                  self.mirror, self.match_rows)
         return self.seq
 
     def reset(self):

@@ -255,20 +255,6 @@ typedef struct {
   uint8_t* match_flags;           /* n flags, or NULL */
   uint32_t* match_rows;           /* room for n row indices, or NULL */
   int64_t* d_mirror;              /* device memory, the batch's outputs words (>= 1) */
-  /* Optional DMA staging (all NULL: the kernel reads the host buffers in
-   * place over PCIe).  With d_tweak_keys set, publish copies the rows, the
-   * offsets, the lengths and output_words outputs words (to d_mirror) into
-   * these device buffers on the stream's copy stream, and the kernel takes
-   * the batch once the copies are done; the host inputs are then free to
-   * reuse as soon as the batch is done, like the in-place ones.  It measured
- * no faster than the in-place reads, and a copy the
- * runtime performs with a blit kernel rather than a copy engine waits for
- * free wave slots, i.e. for the running kernel's idle exit
- * (CUDASP_STREAM_IDLE_MS); the table-function host does not use it. */
-  uint8_t* d_tweak_keys;          /* n x 64 */
-  uint32_t* d_output_offsets;     /* n */
-  uint32_t* d_output_lengths;     /* n */
-  size_t output_words;            /* words of `outputs` to copy (staged) */
 } cudasp_stream_batch;
 int cudasp_host_alloc(void** p, size_t bytes);
 void cudasp_host_free(void* p);

@@ -14,6 +14,7 @@
 
 #include "../../duckdb-cudasp-extension_amd/csrc/scan_prepare.hpp"
 #include "../../duckdb-cudasp-extension_amd/csrc/scan_multi.hpp"
+#include "../../duckdb-cudasp-extension_amd/csrc/scan_stream.hpp"
 
 namespace cudasp {
 void fe_check_fail(const char* what, int limb, uint32_t v) {
@@ -450,6 +451,18 @@ int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, ui
     }
   }
   return 0;
+}
+
+// Byte offsets of the streaming scan's host/device control structures
+// (scan_stream.hpp), for tests/test_stream_isa_cpu.py, which finds the
+// kernel's stores to them in the gfx950 disassembly: StreamCtrl done,
+// nmatch, desc; StreamBatch size, seq; StreamDev desc, pub_wr, pub.
+int emu_stream_layout(uint64_t* out, int n) {
+  const uint64_t v[8] = {offsetof(StreamCtrl, done),   offsetof(StreamCtrl, nmatch), offsetof(StreamCtrl, desc),
+                         sizeof(StreamBatch),          offsetof(StreamBatch, seq),   offsetof(StreamDev, desc),
+                         offsetof(StreamDev, pub_wr), offsetof(StreamDev, pub)};
+  for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
+  return 8;
 }
 
 }  // extern "C"

@@ -15,7 +15,10 @@ back into the pinned slot) beyond the default options and single query:
   slot: its device mirror still exists);
 * a wait timeout (CUDASP_STREAM_TIMEOUT_MS): the query fails with an error
   instead of hanging, its feed drains and is pooled, and the next query on
-  it returns the planted rows."""
+  it returns the planted rows; a kernel the bounded finish gives up on is
+  leaked without any wait;
+* a batch made late (test hook) while ~150 small batches pass: the feed's
+  ring bound harvests it before the stream runs 64 batches past it."""
 import numpy as np
 import pytest
 
@@ -160,24 +163,18 @@ def test_host_stream_labels_no_output_words(torch, keys):  # noqa: F811
     release_pool()
 
 
-def test_host_stream_timeout_then_pooled_feed(torch, monkeypatch):  # noqa: F811
-    """CUDASP_STREAM_TIMEOUT_MS=1 on a 2.4M-row Arrow query with
-    batch_size 2.4M (the ramp's last slot holds 1.2M rows, ~7 ms of GPU
-    work, still running when the input ends): the end-of-query wait sees no
-    batch complete for 1 ms and the query fails with an error instead of
-    hanging; freeing it drains the kernel with the default bound and pools
-    the feed; the next query (the default timeout) takes the pooled feed and
-    emits exactly the planted rows."""
+def _planted_arrow(torch, n, first, every=100_003):  # noqa: F811
+    """n synthetic rows as an Arrow table (2 outputs per row, txid = BE row
+    index, height = row index) with the true base value (C oracle) planted
+    on every `every`-th row from row 17; returns (table, planted rows)."""
     import pyarrow as pa
-    from cudasp_amd import CudaspError, cudasp_scan_arrow, pool_size, release_pool
     from oracle import oracle
-    n = 2_400_000
-    b = tm.make_batch(torch, 123_456, n)
+    b = tm.make_batch(torch, first, n)
     xs = b["tweak_x"].cpu().numpy().view(np.uint32)
     ys = b["tweak_y"].cpu().numpy().view(np.uint32)
     tw = np.ascontiguousarray(np.concatenate([xs.T, ys.T], axis=1).astype("<u4")).view(np.uint8).reshape(n, 64)
     outs = b["outputs"][:2 * n].cpu().numpy().copy()
-    planted = np.arange(17, n, 100_003)
+    planted = np.arange(17, n, every)
     _, ov = oracle.scan(tm.SCAN, tm.SPEND, [], tw[planted], threads=16, want_values=True)
     outs[2 * planted] = ov[:, 0]
     txid = np.zeros((n, 32), dtype=np.uint8)
@@ -188,17 +185,82 @@ def test_host_stream_timeout_then_pooled_feed(torch, monkeypatch):  # noqa: F811
         "tweak_key": pa.FixedSizeBinaryArray.from_buffers(pa.binary(64), n, [None, pa.py_buffer(tw.tobytes())]),
         "outputs": pa.ListArray.from_arrays(pa.array(np.arange(0, 2 * n + 1, 2, dtype=np.int32)), pa.array(outs)),
     })
+    return tab, planted
+
+
+def test_host_stream_timeout_then_pooled_feed(torch, monkeypatch):  # noqa: F811
+    """CUDASP_STREAM_TIMEOUT_MS=1 on a 2.4M-row Arrow query with
+    batch_size 2.4M (the ramp's last slot holds 1.2M rows, ~7 ms of GPU
+    work, still running when the input ends): the end-of-query wait sees no
+    batch complete for 1 ms and the query fails with an error instead of
+    hanging; freeing it drains the kernel with the default bound and pools
+    the feed (or, if the query's own bounded finish gave up on the kernel,
+    leaks it); the next query (the default timeout) emits exactly the
+    planted rows."""
+    from cudasp_amd import CudaspError, cudasp_scan_arrow, pool_size, release_pool
+    n = 2_400_000
+    tab, planted = _planted_arrow(torch, n, 123_456)
     release_pool()
     monkeypatch.setenv("CUDASP_STREAM_TIMEOUT_MS", "1")
     with pytest.raises(CudaspError) as e:
         cudasp_scan_arrow(tab, tm.SCAN, tm.SPEND, [], batch_size=n, threads=8)
-    assert "without progress" in str(e.value)
-    assert pool_size() == 1  # drained and pooled, not leaked
+    assert "without progress" in str(e.value) or "still running" in str(e.value)
+    assert pool_size() <= 1  # drained and pooled, or abandoned and leaked
     monkeypatch.delenv("CUDASP_STREAM_TIMEOUT_MS")
     st = {}
     out = cudasp_scan_arrow(tab, tm.SCAN, tm.SPEND, [], batch_size=n, threads=8, stats=st)
     assert sorted(out.column("height").to_pylist()) == planted.tolist()
     assert st["streaming_feeds"] == 1
+    release_pool()
+
+
+def test_host_stream_abandoned_feed_is_leaked(torch, monkeypatch):  # noqa: F811
+    """A kernel still running when the query's bounded finish gives up
+    (CUDASP_STREAM_TIMEOUT_MS=1, one 4M-row slot: ~25 ms of GPU work, no
+    ramp): the stream is abandoned, and freeing the query frees nothing the
+    kernel may touch and waits for nothing -- the feed is leaked, not pooled
+    (feeds_release goes straight to release_res).  The GPU then finishes the
+    abandoned kernel on its own and the next query, on a new feed, emits
+    exactly the planted rows."""
+    from cudasp_amd import CudaspError, cudasp_scan_arrow, pool_size, release_pool
+    n = 4_000_000
+    tab, planted = _planted_arrow(torch, n, 7_000_001, every=250_007)
+    release_pool()
+    monkeypatch.setenv("CUDASP_STREAM_TIMEOUT_MS", "1")
+    monkeypatch.setenv("CUDASP_TF_RAMP", "0")
+    with pytest.raises(CudaspError) as e:
+        cudasp_scan_arrow(tab, tm.SCAN, tm.SPEND, [], batch_size=n, threads=4)
+    assert "without progress" in str(e.value) or "still running" in str(e.value)
+    assert pool_size() == 0  # abandoned: leaked, never pooled
+    monkeypatch.delenv("CUDASP_STREAM_TIMEOUT_MS")
+    monkeypatch.delenv("CUDASP_TF_RAMP")
+    out = cudasp_scan_arrow(tab, tm.SCAN, tm.SPEND, [], batch_size=300000, threads=4)
+    assert sorted(out.column("height").to_pylist()) == planted.tolist()
+    release_pool()
+
+
+def test_host_stream_late_batch_ring_bound(torch, monkeypatch):  # noqa: F811
+    """Out-of-order slot reuse cannot run the stream 64 batches past a late
+    batch: 2048-row batches (~150 of them), 48 slots, no
+    wave priority, and batch 3 made late by the test hook
+    (CUDASP_TF_TEST_LATE_SEQ: the non-blocking checks read it as not done
+    for 60 s, so the ring moves on without it).  Before the ring bound, the
+    late batch was harvested more than 64 publishes later and the query
+    failed (cudasp_stream_matches: not a done batch of the last 64); with it,
+    the feed harvests the late slot first once the bound is reached, and the
+    query emits exactly the planted rows."""
+    from cudasp_amd import cudasp_scan_arrow, release_pool
+    n = 300_000
+    tab, planted = _planted_arrow(torch, n, 55_555, every=1_009)
+    release_pool()
+    monkeypatch.setenv("CUDASP_TF_STREAM_SLOTS", "48")
+    monkeypatch.setenv("CUDASP_STREAM_PRIO_US", "0")
+    monkeypatch.setenv("CUDASP_TF_TEST_LATE_SEQ", "3")
+    monkeypatch.setenv("CUDASP_TF_TEST_LATE_MS", "60000")
+    st = {}
+    out = cudasp_scan_arrow(tab, tm.SCAN, tm.SPEND, [], batch_size=2048, threads=8, piece_rows=2048, stats=st)
+    assert sorted(out.column("height").to_pylist()) == planted.tolist()
+    assert st["streaming_feeds"] == 1 and st["launches"] > 100
     release_pool()
 
 

@@ -1,9 +1,9 @@
-# Round 4 measurement set of the final tree (e2e legs: streaming feeds and per-slot launches), on one box: GPU suite + smoke,
+# Measurement set of a tree (e2e legs: streaming feeds and per-slot launches), on one box: GPU suite + smoke,
 # rocprofv3 kernel trace (+ --stats) of the default bench command, then the
 # bench lines at the configs' shapes and the 2-rank rehearsal.
 #   $1: "notests" skips pytest + smoke
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${MEASURE_TAG:-r04a}_measure; mkdir -p $O; cd $R
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${MEASURE_TAG:-r05}_measure; mkdir -p $O; cd $R
 if [ "$1" != "notests" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { grep -E "PASS|FAIL|Error|error" $O/gpu_tests.log | tail -30; tail -60 $O/gpu_tests.log; exit 1; }
   tail -1 $O/gpu_tests.log

@@ -1,11 +1,11 @@
-# Round 3: the VALU ceiling of k_scan_multi's instruction mix.  PMC passes
+# The VALU ceiling of k_scan_multi's instruction mix.  PMC passes
 # (each its own run, SQ / GRBM blocks within their slot limits) over
 #   (a) tools/microbench/int_throughput: issue-bound loops of one opcode each
 #       (calibration: what SQ_ACTIVE_INST_VALU reads when the VALU is saturated)
 #   (b) the bench's k_scan_multi (one launch over 3M rows, 0 and 16 labels)
 # then tools/valu_ceiling.py.
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r03_valu; mkdir -p $O; cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${MEASURE_TAG:-r05}_valu; mkdir -p $O; cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
 grep -oE "SQ_[A-Z0-9_]+" $O/counters.txt | sort -u > $O/sq_counters.txt; wc -l $O/sq_counters.txt
 grep -E "^SQ_(INSTS_VALU|ACTIVE_INST|INST_CYCLES|VALU|BUSY)" $O/sq_counters.txt | tr '\n' ' '; echo

@@ -31,7 +31,6 @@ def main():
     ap.add_argument("--device-inputs", action="store_true",
                     help="publish device copies of rows / offsets / lengths / outputs (a library built with "
                          "-DCUDASP_AB_STREAM_ANY_MEMORY): prices the zero-copy PCIe reads")
-    ap.add_argument("--staged", action="store_true", help="stage every batch into device buffers by DMA (product path)")
     ap.add_argument("--device-results", action="store_true",
                     help="match rows into device memory too (same build)")
     ap.add_argument("--gap-ms", type=float, default=0.0,
@@ -59,7 +58,7 @@ def main():
         rows = np.ascontiguousarray(np.concatenate([xs.T, ys.T], axis=1)).view(np.uint8).reshape(n, 64)
         stage.append(StreamBatch(rows, b["outputs"].cpu().numpy(), b["offsets"][:n].cpu().numpy().view(np.uint32),
                                  b["lengths"][:n].cpu().numpy().view(np.uint32), label_count=len(labels),
-                                 want_flags=a.flags, staged=a.staged))
+                                 want_flags=a.flags))
     setup_s = time.time() - t0
     out = dict(rows=a.rows, batch=a.batch, labels=a.labels, kmax=a.kmax, batches=len(sizes), setup_s=round(setup_s, 1))
     with Scanner(tm.SCAN, tm.SPEND, labels, max_rows=a.batch) as s:

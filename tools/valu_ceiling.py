@@ -1,5 +1,5 @@
 """The VALU ceiling of k_scan_multi's own instruction mix, from rocprofv3
-PMC passes (tools/r03/gpu_valu_ceiling.sh writes the directory this reads).
+PMC passes (tools/recipes/valu_ceiling.sh writes the directory this reads).
 
 Per dispatch (median over a kernel's dispatches):
   cycles C   GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs)
