@@ -43,10 +43,14 @@ mod n and g the global row index; 2 splitmix64 outputs per row (seed
 L labels the next row gets label j's value, j cycling over all L labels, so the
 expected match count is known exactly and checked after the run.
 
-Only the cpu_baseline leg touches oracle/ (the C restatement, timed on a
-bounded sample on this box's host cores, and checked against the GPU flags;
-it also recomputes the planted values of 256 planted rows spread over the
-whole rank table: `planted_oracle_check`).
+Only the CPU legs touch oracle/ (the C restatement: timed on a bounded sample
+on this box's host cores as `cpu_baseline_port` and checked against the GPU
+flags; it also recomputes the planted values of 256 planted rows spread over
+the whole rank table, `planted_oracle_check`, and of a 256-row sample of the
+end-to-end leg's planted and unplanted rows, `e2e.planted_oracle_check`).
+`cpu_baseline` itself is the strongest CPU stand-in the image allows:
+`port-optimized` (tools/cpu_port, the product's row pipeline compiled for the
+host) where it covers the options, else the oracle port.
 """
 import argparse
 import hashlib
@@ -528,8 +532,11 @@ def e2e_leg(args, labels, world, fb_bits, mode=None):
     if args.e2e_hw_queues:
         env["GPU_MAX_HW_QUEUES"] = str(args.e2e_hw_queues)
     lf = None
+    sample = tempfile.NamedTemporaryFile(prefix="cudasp_e2e_sample_", suffix=".json", delete=False)
+    sample.close()
     cmd = [exe, "--rows", str(args.rows), "--threads", str(threads), "--batch", str(args.batch_size),
-           "--labels", str(len(labels)), "--input", args.e2e_input, "--reps", str(reps), "--warm-reps", str(reps)]
+           "--labels", str(len(labels)), "--input", args.e2e_input, "--reps", str(reps), "--warm-reps", str(reps),
+           "--plant-sample", sample.name]
     if labels:
         lf = tempfile.NamedTemporaryFile(prefix="cudasp_labels_", suffix=".bin", delete=False)
         lf.write(b"".join(labels))
@@ -540,6 +547,7 @@ def e2e_leg(args, labels, world, fb_bits, mode=None):
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.e2e_timeout, env=env)
     except subprocess.TimeoutExpired:
+        os.unlink(sample.name)
         return dict(error="timed out after %d s" % args.e2e_timeout, cmd=" ".join(cmd[1:]))
     finally:
         if lf is not None:
@@ -548,7 +556,25 @@ def e2e_leg(args, labels, world, fb_bits, mode=None):
     try:
         res = json.loads(line)
     except ValueError:
+        os.unlink(sample.name)
         return dict(error="exit %d: %s" % (r.returncode, (r.stderr or r.stdout)[-400:]), cmd=" ".join(cmd[1:]))
+    # the planted values host_e2e wrote came from the GPU's own values path:
+    # recompute a strided sample of planted and unplanted rows with the C
+    # oracle (checker use of oracle/), so the e2e line's "emitted == planted"
+    # is tied to the oracle, not only to the GPU
+    try:
+        with open(sample.name) as f:
+            smp = json.load(f)
+        sys.path.insert(0, ROOT)
+        from oracle import oracle
+        res["planted_oracle_check"] = oracle.check_planted_sample(smp, threads=min(16, host_cores()[0]))
+        res["planted_oracle_check"]["note"] = ("host_e2e --plant-sample: 256 planted + 256 unplanted rows strided "
+                                               "over the table, recomputed by oracle/cudasp_oracle.c (tweak = "
+                                               "(s0 + g) G, planted value, flag, emitted)")
+    except (OSError, ValueError, KeyError) as e:
+        res["planted_oracle_check"] = dict(error=str(e))
+    finally:
+        os.unlink(sample.name)
     res["exit_code"] = r.returncode
     res["wall_s"] = round(time.perf_counter() - t0, 2)
     res["args"] = " ".join(c if c != (lf.name if lf else None) else "<label keys>" for c in cmd[1:])
@@ -1070,11 +1096,22 @@ def main():
         smp = cpu_sample(tab, args.cpu_rows)
         result["host_cores_allotted"] = dict(cores=use, source=source, visible=visible,
                                              omp_num_threads=os.environ.get("OMP_NUM_THREADS"))
-        result["cpu_baseline"] = cpu_baseline(smp, labels, threads, args.output_count, args.label_negation)
-        result["cpu_baseline"]["host_cpus_visible"] = visible
+        # cpu_baseline is the strongest CPU restatement the image allows:
+        # port-optimized (the product's GLV/wNAF/co-Z row pipeline compiled
+        # for the host) where it covers the options, else the oracle port;
+        # the oracle port is kept beside it as cpu_baseline_port
+        port = cpu_baseline(smp, labels, threads, args.output_count, args.label_negation)
+        port["host_cpus_visible"] = visible
+        result["cpu_baseline"] = port
         result["planted_oracle_check"] = planted_oracle_check(tab, labels, threads)
         if args.output_count == 1 and not args.label_negation:
-            result["cpu_baseline_optimized"] = cpu_baseline_optimized(smp, labels, threads)
+            opt = cpu_baseline_optimized(smp, labels, threads)
+            if "value" in opt:
+                opt["host_cpus_visible"] = visible
+                result["cpu_baseline"] = opt
+                result["cpu_baseline_port"] = port
+            else:
+                result["cpu_baseline_optimized_error"] = opt.get("error")
             if args.cpu_sweep_rows:
                 result["cpu_baseline_optimized_sweep"] = cpu_port_sweep(smp, labels, use, args.cpu_sweep_rows)
             if args.cpu_openssl_rows:

@@ -447,6 +447,12 @@ struct Feed {
   // moves on without it (a starved batch; a blocking harvest still takes it)
   int64_t late_seq = -1;
   double late_s = 0;
+  // measurement only (CUDASP_TF_NULL_DEVICE=1): slots are marked done by
+  // the host at launch, with no publish, copy or kernel -- reservation,
+  // copies into the slots and harvest unchanged, nothing emitted -- so a
+  // query runs at the executor threads' own ceiling (the host's capacity
+  // for N GPUs; tools/host_e2e --null-device)
+  bool null_device = false;
   int error = CUDASP_OK;
   std::string error_msg;
   std::mutex stream_mu[FEED_MAX_STREAMS];  // a scanner's host state is not re-entrant
@@ -520,7 +526,9 @@ int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   lk.unlock();
   const double t0 = now_s();
   int rc = CUDASP_OK;
-  if (r.stream) {
+  if (f.null_device) {
+    // measurement only: no device work
+  } else if (r.stream) {
     // Streaming feed: publish the slot to the feed's kernel, which reads it
     // in place (no copies, no launch), copies each row's outputs to the
     // slot's device mirror (sized with the slot, prepare_slot_streaming) and
@@ -595,7 +603,7 @@ int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
     s.state = SLOT_LAUNCHED;
     f.launches++;
     f.rows += n;
-    if (r.stream) {
+    if (r.stream && !f.null_device) {
       s.in_ring = true;
       s.t_pub = now_s();
       f.pub_next = std::max(f.pub_next, s.seq + 1);
@@ -613,7 +621,9 @@ int harvest_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   const double t0 = now_s();
   hipError_t e;
   std::string stream_err;
-  {
+  if (f.null_device) {
+    e = hipSuccess;
+  } else {
     DeviceSet dg(f.res->device);
     if (f.res->stream) {
       e = hipSuccess;
@@ -627,7 +637,7 @@ int harvest_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   }
   const double waited = now_s() - t0;
   ST_HOST(112, (uint64_t)(waited * 1e9), (uint32_t)s.seq);
-  if (e == hipSuccess) {
+  if (e == hipSuccess && !f.null_device) {
     cudasp_tf_global& g = *f.g;
     const auto emit = [&](uint32_t i) {
       g.output_txids.emplace_back((const char*)s.txid_bytes.data() + s.txid_off[i], s.txid_size[i]);
@@ -709,6 +719,7 @@ uint32_t stream_timeout_ms() {
 
 // Whether a launched slot's batch is done (no waiting).
 bool slot_done(Feed& f, FeedSlot& s) {
+  if (f.null_device) return true;
   if (f.res->stream) {
     if (f.late_seq >= 0 && s.seq == (uint64_t)f.late_seq && now_s() - s.t_pub < f.late_s) return false;
     return cudasp_stream_query(f.res->stream, s.seq) == 1;
@@ -1035,6 +1046,7 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
   }
   if (r->stream) (void)cudasp_stream_set_timeout(r->stream, stream_timeout_ms());
   auto f = std::make_unique<Feed>();
+  if (const char* e = getenv("CUDASP_TF_NULL_DEVICE")) f->null_device = atoi(e) != 0;
   if (const char* e = getenv("CUDASP_TF_TEST_LATE_SEQ")) {
     f->late_seq = atoll(e);
     const char* ms = getenv("CUDASP_TF_TEST_LATE_MS");

@@ -1195,7 +1195,11 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
   const int STG = (int)multi_scratch_words(k.label_count, true);
   const int META = STG + STREAM_STG_WORDS;  // piece area a: META + 2 MULTI_RMAX a
   const int SXA = META + STREAM_META_WORDS;
-  const int K = (int)k.output_count;  // 1 .. MULTI_RMAX (cudasp_stream_create); K x rmax <= MULTI_RMAX
+  // 1 .. CUDASP_MAX_OUTPUT_COUNT; K <= MULTI_RMAX: K x rmax <= MULTI_RMAX
+  // units in the pipelined schedule; K > MULTI_RMAX (`wide`): one row per
+  // piece, its K indices in groups of MULTI_RMAX, unpipelined (stream_wide)
+  const int K = (int)k.output_count;
+  const bool wide = K > MULTI_RMAX;
   const bool with_labels = k.label_count != 0;
   const uint32_t ow = k.full_x ? 4u : 1u;
   // pieces of the pipelined schedule: P (F points pending), Q (labels
@@ -1382,7 +1386,78 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
     }
     // t of each new row (K output indices), then stage B's F = t G + B into
     // slots u = j K + kk
-    if (K == 1) {
+    if (wide) {
+      // K > MULTI_RMAX: the piece (count rows, rmax 1: one) is finished here,
+      // its indices in groups of g <= MULTI_RMAX F points with one inversion
+      // each (the S points were inverted above, alone: P and Q stay empty)
+      const StreamWr* wn = wrs[wid][pn];
+      const int meta_n = META + 2 * MULTI_RMAX * pn;
+      uint32_t hits = 0;
+#pragma unroll 1
+      for (int j = 0; j < count; j++) {
+        uint32_t sx[8];
+        {
+          gej P;
+          fe zi;
+          pend_load(P, sc, PB, j);
+          scr_load(zi, sc, PEND_ZI(PB, j));
+          const uint32_t y_odd = row_shared_secret_affine(sx, P, zi);
+#pragma unroll
+          for (int q = 0; q < 8; q++) scr_store_w(sc, SXA + q, sx[q]);
+          scr_store_w(sc, SXA + 8, y_odd);
+        }
+        const uint32_t off = scr_load_w(sc, meta_n + 2 * j);
+        const uint32_t len = scr_load_w(sc, meta_n + 2 * j + 1);  // 0 for padding lanes
+        const auto out = [&](int, const int64_t*& o, uint32_t& of, uint32_t& ln, int64_t*& vrow, uint32_t& vstride) {
+          o = wn[j].mirror;
+          of = off;
+          ln = len;
+          vrow = nullptr;
+          vstride = 0;
+        };
+        const auto f_at = [&](int u, ge& F) {
+          scr_load(F.x, sc, PEND_X(PB, u));
+          scr_load(F.y, sc, PEND_Y(PB, u));
+        };
+        bool hit = false;
+#pragma unroll 1
+        for (int kk0 = 0; kk0 < K; kk0 += MULTI_RMAX) {
+          const int g = K - kk0 < MULTI_RMAX ? K - kk0 : MULTI_RMAX;
+#pragma unroll 1
+          for (int u = 0; u < g; u++) {
+            uint32_t t[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) sx[q] = scr_load_w(sc, SXA + q);
+            bip352_shared_secret_hash(t, k.mid, sx, scr_load_w(sc, SXA + 8), (uint32_t)(kk0 + u));
+            gej F;
+            row_match_point<FBB>(F, t, fb, k);
+            pend_store(sc, PB, u, F);
+          }
+          pend_invert<2 * MULTI_RMAX + 1>(sc, PB, g);
+#pragma unroll 1
+          for (int u = 0; u < g; u++) {
+            gej F;
+            fe zi;
+            pend_load(F, sc, PB, u);
+            scr_load(zi, sc, PEND_ZI(PB, u));
+            // F affine over the slot's X / Y (the labels read it there)
+            if (row_match_base(F, zi, k, wn[j].mirror, off, len, sc, PB, u, nullptr)) hit = true;
+          }
+          if (with_labels) {
+            // the g x L label sums with one more inversion: their product
+            // goes through pend_invert in pending slot g (same instance)
+            fe acc, inv;
+            labels_forward(acc, k, labels, g, sc, LB, f_at);
+            scr_store(sc, PEND_Z(PB, g), acc);
+            pend_invert<2 * MULTI_RMAX + 1>(sc, PEND_X(PB, g), 1);
+            scr_load(inv, sc, PEND_ZI(PB, g));
+            if (labels_backward(inv, k, labels, g, sc, LB, f_at, out)) hit = true;
+          }
+        }
+        if (hit) hits |= 1u << j;
+      }
+      stream_emit(ctrl, dev, wn, count, lane, hits);
+    } else if (K == 1) {
 #pragma unroll 1
       for (int j = 0; j < count; j++) {
         gej P;
@@ -1423,13 +1498,13 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
         pend_store(sc, PB, u, F);
       }
     }
-    {  // the new piece becomes P
+    if (!wide) {  // the new piece becomes P
       const int t = pp;
       pp = pn;
       pn = t;
+      count_p = count;
+      if (lane == 0 && count) me.t_p = t_it;
     }
-    count_p = count;
-    if (lane == 0 && count) me.t_p = t_it;
     if (lane == 0) {
       me.busy = me.busy + (wall_clock64() - t_it);
       ST_EV(ST_ITER_END, st_wave, 0ull, 0u, 0u);
@@ -2104,9 +2179,11 @@ static uint64_t stream_grid_blocks(cudasp_scanner* s, uint64_t blocks_req) {
   return grid_blocks_for(s, blocks_req, stream_scratch_words(s->consts.label_count));
 }
 
-// The streaming scan's options: output_count up to MULTI_RMAX (K x rows per
-// piece <= MULTI_RMAX), an HBM fixed-base width, the pipelined schedule.
-static_assert(CUDASP_STREAM_MAX_OUTPUT_COUNT <= MULTI_RMAX, "K x rows of a piece <= MULTI_RMAX");
+// The streaming scan's options: any output_count (K x rows per piece <=
+// MULTI_RMAX in the pipelined schedule, one row per piece and groups of
+// MULTI_RMAX indices above that), an HBM fixed-base width, the pipelined
+// schedule.
+static_assert(CUDASP_STREAM_MAX_OUTPUT_COUNT == CUDASP_MAX_OUTPUT_COUNT, "every output_count streams");
 static bool stream_ok(const cudasp_scanner* s) {
   return s->consts.output_count >= 1 && s->consts.output_count <= (uint32_t)CUDASP_STREAM_MAX_OUTPUT_COUNT &&
          (s->fb_bits == 22 || s->fb_bits == 26) && s->multi_pipe &&
@@ -2939,9 +3016,8 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
   *out = nullptr;
   if (!stream_ok(s))
     return set_error(CUDASP_ERR_INVALID_ARG,
-                     "the streaming scan needs output_count <= %d, an HBM fixed-base width (22 or 26 bits) and the "
-                     "pipelined schedule",
-                     CUDASP_STREAM_MAX_OUTPUT_COUNT);
+                     "the streaming scan needs an HBM fixed-base width (22 or 26 bits), the pipelined schedule and "
+                     "a label count whose scratch fits");
   DeviceGuard g(s->device);
   std::unique_ptr<cudasp_stream> st(new cudasp_stream());
   st->s = s;

@@ -194,17 +194,18 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
  * 64-byte tweak blobs as the table holds them, the outputs CSR) and writing
  * its results back there: one flag per row and/or the indices of the
  * matching rows; the host polls for each batch's completion.  Needs a
- * scanner with output_count <= 6 and an HBM fixed-base width (22 or 26
- * bits); the scanner must not run other launches while a stream on it is
- * open.
+ * scanner with an HBM fixed-base width (22 or 26 bits), any output_count
+ * (up to 6 indices per row ride the pipelined schedule; more are taken one
+ * row per piece, in groups of 6 indices); the scanner must not run other
+ * launches while a stream on it is open.
  *   cudasp_host_alloc   coherent pinned host memory, device-addressable at
  *                       the same address: every host buffer of a published
  *                       batch must lie in such an allocation (checked at
  *                       publish: the kernel's uncached reads and
  *                       system-scope result stores need coherent memory).
  *   cudasp_stream_supported  1 when the scanner's current keys and options
- *                       allow a stream (output_count <= 6, an HBM fixed-base
- *                       width, a label count whose scratch fits), else 0.
+ *                       allow a stream (an HBM fixed-base width, a label
+ *                       count whose scratch fits), else 0.
  *   cudasp_stream_create  blocks = 0: the whole device (3 waves per SIMD).
  *   cudasp_stream_publish_batch  a batch of n >= 1 rows (cudasp_stream_batch):
  *                       d_mirror is a device buffer as large as the batch's
@@ -245,7 +246,7 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
  *                       idle exits, poller polls, workers' busy and lifetime
  *                       ticks (100 MHz). */
 typedef struct cudasp_stream cudasp_stream;
-#define CUDASP_STREAM_MAX_OUTPUT_COUNT 6
+#define CUDASP_STREAM_MAX_OUTPUT_COUNT CUDASP_MAX_OUTPUT_COUNT
 typedef struct {
   const uint8_t* tweak_keys;      /* n x 64 bytes (x then y, little-endian words) */
   const int64_t* outputs;         /* outputs CSR values (4 words per output with full_x) */

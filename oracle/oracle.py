@@ -148,3 +148,42 @@ def fp_mul(a, b):
     out = ctypes.create_string_buffer(32)
     load().cudasp_oracle_fp_mul(a, b, out)
     return out.raw
+
+
+def check_planted_sample(sample, threads=1):
+    """Checker of an end-to-end run's row sample (tools/host_e2e
+    --plant-sample: planted and unplanted rows strided over the table, with
+    the keys and what the run emitted).  Every row is recomputed here:
+    its tweak must be the synthetic generator's T_g = (s0 + g) G, a planted
+    row's planted value (its first output) must be the oracle's value of
+    its column (0 = base, 1 + j = label j) and its oracle flag 1, an
+    unplanted row's oracle flag 0, and the run must have emitted exactly
+    the rows the oracle flags.  Returns {rows, equal, planted, unplanted,
+    mismatches (first few)}; equal == rows means the sample agrees."""
+    scan_key = bytes.fromhex(sample["scan"])
+    spend_key = bytes.fromhex(sample["spend"])
+    labels = [bytes.fromhex(h) for h in sample["labels"]]
+    s0 = bytes.fromhex(sample["s0_le"])
+    rows = sample["rows"]
+    n = len(rows)
+    if n == 0:
+        return dict(rows=0, equal=0, planted=0, unplanted=0, mismatches=[])
+    tw = np.frombuffer(b"".join(bytes.fromhex(r["tweak"]) for r in rows), dtype=np.uint8).reshape(n, 64)
+    lens = np.array([len(r["outputs"]) for r in rows], dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint32)
+    outs = np.array([v for r in rows for v in r["outputs"]], dtype=np.int64)
+    flags, vals = scan(scan_key, spend_key, labels, tw, outs, offs, lens, threads=threads, want_values=True)
+    equal, bad = 0, []
+    for i, r in enumerate(rows):
+        ok = bytes(tw[i]) == synth_tweak(s0, r["g"])
+        if r["column"] >= 0:
+            ok = ok and len(r["outputs"]) > 0 and int(vals[i, r["column"]]) == r["outputs"][0] and flags[i] == 1
+        else:
+            ok = ok and flags[i] == 0
+        ok = ok and int(flags[i]) == int(r["emitted"])
+        equal += ok
+        if not ok and len(bad) < 8:
+            bad.append(dict(g=r["g"], column=r["column"], emitted=r["emitted"], oracle_flag=int(flags[i])))
+    planted = sum(1 for r in rows if r["column"] >= 0)
+    return dict(rows=n, equal=equal, planted=planted, unplanted=n - planted,
+                label_columns=sorted({r["column"] for r in rows if r["column"] > 0}), mismatches=bad)

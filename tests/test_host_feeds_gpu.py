@@ -154,8 +154,11 @@ def test_host_e2e_tool_config5_shape(torch, keys, tmp_path):  # noqa: F811
     executor threads, row chunks and Arrow columns: every query emits exactly
     the planted rows (base values on rows 0 mod 1000, label j = (g / 1000)
     mod 16 on rows 1 mod 1000: all 16 label indices), also for a query started
-    right after a busy kernel (--warm-reps)."""
+    right after a busy kernel (--warm-reps).  A strided sample of planted and
+    unplanted rows, with every label column, is recomputed by the C oracle."""
     import json
+
+    from oracle import oracle
     exe = os.path.join(ROOT, "tools", "host_e2e")
     if not os.path.exists(exe):
         pytest.fail("tools/host_e2e not built (make -C duckdb-cudasp-extension_amd)")
@@ -163,7 +166,8 @@ def test_host_e2e_tool_config5_shape(torch, keys, tmp_path):  # noqa: F811
     lf.write_bytes(b"".join(keys[2]))
     for mode in ("rows", "columns"):
         cmd = [exe, "--rows", "700000", "--threads", "8", "--batch", "300000", "--labels", "16",
-               "--labels-file", str(lf), "--outputs-max", "15", "--input", mode, "--warm-reps", "1"]
+               "--labels-file", str(lf), "--outputs-max", "15", "--input", mode, "--warm-reps", "1",
+               "--plant-sample", str(tmp_path / "sample.json")]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, (mode, r.stdout[-2000:], r.stderr[-2000:])
         res = json.loads(r.stdout.strip().splitlines()[-1])
@@ -173,6 +177,8 @@ def test_host_e2e_tool_config5_shape(torch, keys, tmp_path):  # noqa: F811
         assert res["launches"] >= 3
         # one more query right after a busy kernel on the GPU (bench's e2e_warm_tx_s); exit 0 covers its rows
         assert res["warm_reps"] == 1 and res["warm_tx_per_s"] > 0
+        chk = oracle.check_planted_sample(json.load(open(tmp_path / "sample.json")), threads=16)
+        assert chk["equal"] == chk["rows"] == 512 and chk["label_columns"] == list(range(1, 17)), chk
 
 
 def test_host_error_mid_query_then_pool_reuse(table16, keys):  # noqa: F811

@@ -7,10 +7,10 @@ back into the pinned slot) beyond the default options and single query:
   pooled feeds while the other query's kernel is resident), each compared
   with the C oracle's flags for its own keys (the reference is re-entrant
   per batch, src/cudasp_gpu.cu:474-484);
-* output_count 2 and 6 with label negation on the streaming feed
-  (cudasp_tf_bind_options; K hashes per row, src/cudasp_gpu.cu:278-282 for
-  the index hash they extend) and output_count 8 on per-slot launches,
-  against the oracle's scan_ex;
+* output_count 2, 6, 8 and 13 (with and without label negation) on the
+  streaming feed (cudasp_tf_bind_options; K hashes per row,
+  src/cudasp_gpu.cu:278-282 for the index hash they extend) and 8 on
+  per-slot launches, against the oracle's scan_ex;
 * label keys with every output list NULL or empty (no output words in a
   slot: its device mirror still exists);
 * a wait timeout (CUDASP_STREAM_TIMEOUT_MS): the query fails with an error
@@ -126,21 +126,26 @@ def _variant_rows(torch, n, K, neg, labels, first):  # noqa: F811
     return rows, sorted(np.nonzero(want)[0].tolist())
 
 
-@pytest.mark.parametrize("K,neg,threads,batch", [(2, True, 3, 2500), (2, True, 8, 300000), (6, False, 4, 3000),
-                                                 (8, True, 3, 2500)])
-def test_host_stream_output_count(torch, K, neg, threads, batch):  # noqa: F811
-    """output_count K with one label (and label negation): K <= 6 runs on the
-    streaming feed (the host's default path), K = 8 on per-slot launches;
-    the emitted rows are the oracle's scan_ex flags."""
+@pytest.mark.parametrize("K,neg,threads,batch,mode", [(2, True, 3, 2500, None), (2, True, 8, 300000, None),
+                                                      (6, False, 4, 3000, None), (8, True, 3, 2500, None),
+                                                      (13, False, 4, 3000, None), (8, True, 3, 2500, "launch")])
+def test_host_stream_output_count(torch, monkeypatch, K, neg, threads, batch, mode):  # noqa: F811
+    """output_count K with one label (and label negation) on the streaming
+    feed (the host's default path; K > 6 takes the kernel's one-row pieces
+    with indices in groups of 6) and, for K = 8, on per-slot launches
+    (CUDASP_TF_MODE=launch); the emitted rows are the oracle's scan_ex flags."""
     from cudasp_amd import cudasp_scan, release_pool
     labels = [tm.LABEL]
     rows, want = _variant_rows(torch, 6000, K, neg, labels, 9100 + K)
     assert want
+    if mode:
+        monkeypatch.setenv("CUDASP_TF_MODE", mode)
+    release_pool()
     st = {}
     got = cudasp_scan(rows, tm.SCAN, tm.SPEND, labels, batch_size=batch, threads=threads, output_count=K,
                       label_negation=neg, stats=st)
     assert sorted(h - 800000 for _, h, _ in got) == want
-    assert st["streaming_feeds"] == (1 if K <= 6 else 0)
+    assert st["streaming_feeds"] == (0 if mode == "launch" else 1)
     assert st["rows"] == len(rows)
     release_pool()
 
@@ -271,16 +276,22 @@ def test_host_e2e_eight_logical_gpus_config4():
     over them, src/cudasp_extension.cu:523-529), 8 executor threads per
     logical GPU, one streaming feed each (CUDASP_TF_MODE=stream; each kernel
     gets 1/8 of the wave slots, GPU_MAX_HW_QUEUES=16 so every feed's stream
-    has a hardware queue).  Every query emits exactly the planted rows."""
+    has a hardware queue).  Every query emits exactly the planted rows, and
+    a strided sample of 256 planted and 256 unplanted rows is recomputed by
+    the C oracle (the planted values come from the GPU's values path)."""
     import json
     import os
     import subprocess
+    import tempfile
+
+    from oracle import oracle
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = os.path.join(root, "tools", "host_e2e")
     env = dict(os.environ, CUDASP_TF_DEVICE_MAP=",".join(["0"] * 8), CUDASP_TF_MODE="stream",
                GPU_MAX_HW_QUEUES="16")
+    sample = os.path.join(tempfile.mkdtemp(), "sample.json")
     cmd = [exe, "--rows", "32700000", "--threads", "64", "--batch", "300000", "--labels", "0", "--input", "rows",
-           "--reps", "1", "--outputs", "2"]
+           "--reps", "1", "--outputs", "2", "--plant-sample", sample]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
     res = json.loads(r.stdout.strip().splitlines()[-1])
@@ -288,4 +299,6 @@ def test_host_e2e_eight_logical_gpus_config4():
     assert res["feeds"] == 8 and res["streaming_feeds"] == 8
     assert res["emitted_equal_planted"] is True
     assert res["matches"] == res["planted"] == 32700
+    chk = oracle.check_planted_sample(json.load(open(sample)), threads=16)
+    assert chk["rows"] == 512 and chk["planted"] == 256 and chk["equal"] == chk["rows"], chk
     print("8 logical GPUs, 64 threads, 32.7M rows: %.1f M tx/s on one card" % (res["tx_per_s"] / 1e6))

@@ -331,16 +331,19 @@ def _variant_case(torch, n, K, neg, full_x, labels, first):
     return tw, outs, offs, lens, want
 
 
-@pytest.mark.parametrize("K,neg,full_x", [(2, True, False), (2, False, False), (3, False, True), (6, True, False)])
+@pytest.mark.parametrize("K,neg,full_x", [(2, True, False), (2, False, False), (3, False, True), (6, True, False),
+                                          (7, False, False), (8, True, False), (13, False, True), (64, True, False)])
 def test_stream_variants(torch, K, neg, full_x):
-    """output_count K > 1 (K hashes and fixed-base points per row, K x rows
-    per piece <= 6), label negation and full-x compares through the
-    streaming kernel: flags and compacted matches equal the C oracle's
-    scan_ex over ragged batches in one stream (the reference has none of the
-    variants: parity unpinned against it, pinned to tests/variants.py)."""
+    """output_count K > 1 (K hashes and fixed-base points per row: K x rows
+    per piece <= 6 in the pipelined schedule; K > 6 one row per piece, its
+    indices in groups of 6 with their own inversions, 13 = 6 + 6 + 1), label
+    negation and full-x compares through the streaming kernel: flags and
+    compacted matches equal the C oracle's scan_ex over ragged batches in
+    one stream (the reference has none of the variants: parity unpinned
+    against it, pinned to tests/variants.py)."""
     from cudasp_amd import Scanner, ScanStream, StreamBatch
     labels = [LABEL]
-    n = 700 if full_x else 2200
+    n = 700 if full_x or K > 16 else 2200
     tw, outs, offs, lens, want = _variant_case(torch, n, K, neg, full_x, labels, 4242 + K)
     assert 0 < int(want.sum()) < n
     cuts = [0, 1, 65, n // 2, n]

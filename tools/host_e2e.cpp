@@ -21,14 +21,26 @@
 //
 //   host_e2e [--rows N] [--threads T] [--batch B] [--labels L --labels-file F]
 //            [--outputs K | --outputs-max KMAX] [--input rows|columns]
-//            [--reps R] [--warm-reps W [--warm-ms MS]]
+//            [--reps R] [--warm-reps W [--warm-ms MS]] [--plant-sample FILE]
+//            [--null-device]
 // (W more queries, each started right after MS ms of a busy kernel on every
 // GPU: the rate at full clock, without the ramp from idle; warm_tx_per_s)
+// --plant-sample writes 256 planted rows and 256 unplanted rows, strided over
+// the table (row index, tweak, outputs list, the planted value's column,
+// whether the last timed query emitted it) with the keys, as JSON, for a
+// checker that recomputes them with the C oracle (oracle.check_planted_sample:
+// the planted values above come from the GPU's own values path).
+// --null-device (measurement only) sets CUDASP_TF_NULL_DEVICE=1: the host's
+// feeds mark every slot done at launch, with no device work, so tx_per_s is
+// the executor threads' own ceiling (reserve, copies into the pinned slots,
+// harvest) -- the host's capacity to feed N GPUs; a query then passes when
+// it emits nothing.
 // Label keys: F holds L 64-byte keys (x || y, little-endian, bench.label_keys);
 // without F, L must be 0 or 1 (the SQL test's label, test/sql/cudasp.test:104).
 // Prints one JSON line; exit 0 iff every timed query emitted exactly the
 // planted rows.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -87,6 +99,8 @@ struct Args {
   int reps = 1;
   int warm_reps = 0;    // more queries, each right after a busy kernel on every GPU (clock at speed)
   int warm_ms = 30;
+  std::string plant_sample;  // JSON sample of planted / unplanted rows for the oracle check
+  bool null_device = false;  // measurement only: no device work in the host's feeds
 };
 
 static Args parse(int argc, char** argv) {
@@ -111,6 +125,8 @@ static Args parse(int argc, char** argv) {
     else if (s == "--reps") a.reps = std::max(1, atoi(val()));
     else if (s == "--warm-reps") a.warm_reps = std::max(0, atoi(val()));
     else if (s == "--warm-ms") a.warm_ms = std::max(1, atoi(val()));
+    else if (s == "--plant-sample") a.plant_sample = val();
+    else if (s == "--null-device") a.null_device = true;
     else {
       fprintf(stderr, "unknown argument %s\n", s.c_str());
       exit(1);
@@ -130,6 +146,7 @@ struct Table {
   std::vector<int64_t> outputs;
   std::vector<uint64_t> list_off, list_len;         // list entries (offset into outputs, length)
   std::vector<uint64_t> planted;                    // planted row indices, sorted
+  std::vector<int> planted_col;                     // their values column: 0 = base, 1 + j = label j
   uint32_t labels_planted_mask = 0;                 // label indices planted (bit j)
 };
 
@@ -240,8 +257,9 @@ static void generate(const Args& a, const uint8_t scan[32], const uint8_t spend[
     t.outputs[t.list_off[idx[r]]] = vals[(size_t)v * m + r];
     if (lab[r] >= 0) t.labels_planted_mask |= 1u << (lab[r] & 31);
   }
-  t.planted = idx;
-  std::sort(t.planted.begin(), t.planted.end());
+  t.planted = idx;  // ascending: g, then g + 1 for the label plant
+  t.planted_col.resize(m);
+  for (uint32_t r = 0; r < m; r++) t.planted_col[r] = lab[r] < 0 ? 0 : 1 + lab[r];
   HK(hipFree(dpx));
   HK(hipFree(dpy));
   HK(hipFree(dt));
@@ -255,6 +273,7 @@ struct QueryResult {
   bool exact = false;  // emitted rows == planted rows
   cudasp_tf_stats stats{};
   int logical_gpus = 0;
+  std::vector<uint64_t> got;  // emitted row indices, sorted
   double call_s_mean = 0, final_s_mean = 0, done_min = 0, done_max = 0;
 };
 
@@ -405,7 +424,8 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
   cudasp_tf_bind_free(bd);
   q.emitted = got.size();
   std::sort(got.begin(), got.end());
-  q.exact = got == t.planted;
+  q.exact = a.null_device ? got.empty() : got == t.planted;
+  q.got.swap(got);
   auto mean = [](const std::vector<double>& v) {
     double s = 0;
     for (double x : v) s += x;
@@ -418,8 +438,57 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
   return q;
 }
 
+static std::string hex(const uint8_t* p, size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string s(2 * n, '0');
+  for (size_t i = 0; i < n; i++) {
+    s[2 * i] = d[p[i] >> 4];
+    s[2 * i + 1] = d[p[i] & 15];
+  }
+  return s;
+}
+
+// 256 planted and 256 unplanted rows, strided over the table, as JSON (see
+// the header): what the oracle recomputes to tie the e2e leg to it.
+static bool write_plant_sample(const std::string& path, const Table& t, const uint8_t scan[32],
+                               const uint8_t spend[64], const std::vector<uint8_t>& labels, int L,
+                               const std::vector<uint64_t>& got) {
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) return false;
+  uint8_t s0[32];
+  hex2bin(S0_LE_HEX, s0);
+  fprintf(f, "{\"scan\": \"%s\", \"spend\": \"%s\", \"s0_le\": \"%s\", \"labels\": [", hex(scan, 32).c_str(),
+          hex(spend, 64).c_str(), hex(s0, 32).c_str());
+  for (int j = 0; j < L; j++) fprintf(f, "%s\"%s\"", j ? ", " : "", hex(labels.data() + 64 * j, 64).c_str());
+  fprintf(f, "], \"rows_total\": %llu, \"planted_total\": %zu, \"rows\": [", (unsigned long long)t.rows,
+          t.planted.size());
+  std::vector<std::pair<uint64_t, int>> pick;  // (row, column or -1)
+  const size_t np = t.planted.size(), want = 256;
+  for (size_t i = 0; i < std::min(want, np); i++) {
+    const size_t k = i * np / std::min(want, np);
+    pick.emplace_back(t.planted[k], t.planted_col[k]);
+  }
+  const uint64_t unplanted = t.rows / PLANT_EVERY;  // rows g = 500 mod 1000 (never planted)
+  for (uint64_t i = 0; i < std::min<uint64_t>(want, unplanted); i++) {
+    const uint64_t g = (i * unplanted / std::min<uint64_t>(want, unplanted)) * PLANT_EVERY + PLANT_EVERY / 2;
+    if (g < t.rows) pick.emplace_back(g, -1);
+  }
+  for (size_t i = 0; i < pick.size(); i++) {
+    const uint64_t g = pick[i].first;
+    fprintf(f, "%s{\"g\": %llu, \"tweak\": \"%s\", \"column\": %d, \"emitted\": %d, \"outputs\": [", i ? ", " : "",
+            (unsigned long long)g, hex(t.tweaks.data() + g * 64, 64).c_str(), pick[i].second,
+            std::binary_search(got.begin(), got.end(), g) ? 1 : 0);
+    for (uint64_t k = 0; k < t.list_len[g]; k++)
+      fprintf(f, "%s%lld", k ? ", " : "", (long long)t.outputs[t.list_off[g] + k]);
+    fprintf(f, "]}");
+  }
+  fprintf(f, "]}\n");
+  return fclose(f) == 0;
+}
+
 int main(int argc, char** argv) {
   const Args a = parse(argc, argv);
+  if (a.null_device) setenv("CUDASP_TF_NULL_DEVICE", "1", 1);
   uint8_t scan[32], spend[64];
   hex2bin(SCAN_HEX, scan);
   hex2bin(SPEND_HEX, spend);
@@ -479,6 +548,11 @@ int main(int argc, char** argv) {
   int planted_labels = 0;
   for (int j = 0; j < 32; j++) planted_labels += (t.labels_planted_mask >> j) & 1;
   const char* hq = getenv("GPU_MAX_HW_QUEUES");
+  if (!a.plant_sample.empty() &&
+      !write_plant_sample(a.plant_sample, t, scan, spend, labels, a.labels, qs.back().got)) {
+    fprintf(stderr, "cannot write %s\n", a.plant_sample.c_str());
+    return 1;
+  }
   printf("{\"what\": \"table-function host end-to-end (host memory -> matches, PCIe-inclusive)\", \"input\": \"%s\", "
          "\"rows\": %llu, \"threads\": %d, \"batch_size\": %lld, \"labels\": %d, \"outputs_per_row\": %s, "
          "\"outputs_total\": %llu, \"reps\": %d, \"seconds\": %.5f, \"seconds_all\": %s, \"seconds_min\": %.5f, "
@@ -489,7 +563,8 @@ int main(int argc, char** argv) {
          "\"harvest_wait_s\": %.4f, \"reserve_s\": %.4f, \"copy_s\": %.4f, \"launch_s\": %.4f, "
          "\"thread_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
          "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f, \"streaming_feeds\": %u, \"logical_gpus\": %d, "
-         "\"warm_reps\": %d, \"warm_ms\": %d, \"warm_seconds\": %.5f, \"warm_tx_per_s\": %.1f}\n",
+         "\"warm_reps\": %d, \"warm_ms\": %d, \"warm_seconds\": %.5f, \"warm_tx_per_s\": %.1f, "
+         "\"null_device\": %s, \"host_cpus_online\": %ld}\n",
          a.columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)t.rows, a.threads, (long long)a.batch,
          a.labels,
          a.kmax ? ("\"1.." + std::to_string(a.kmax) + "\"").c_str() : std::to_string(a.k).c_str(),
@@ -500,6 +575,6 @@ int main(int argc, char** argv) {
          (unsigned long long)q.stats.launches, q.stats.launches ? (double)q.stats.rows / q.stats.launches : 0.0,
          q.stats.harvest_wait_s, q.stats.reserve_s, q.stats.copy_s, q.stats.launch_s, q.call_s_mean, q.final_s_mean, q.done_min, q.done_max,
          q.stats.streaming_feeds, q.logical_gpus, a.warm_reps, a.warm_ms, warm_med,
-         warm_med > 0 ? t.rows / warm_med : 0.0);
+         warm_med > 0 ? t.rows / warm_med : 0.0, a.null_device ? "true" : "false", sysconf(_SC_NPROCESSORS_ONLN));
   return all_exact ? 0 : 2;
 }
