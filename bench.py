@@ -523,7 +523,11 @@ def e2e_leg(args, labels, world, fb_bits, mode=None):
     exe = os.path.join(ROOT, "tools", "host_e2e")
     if not os.path.exists(exe):
         return dict(error="tools/host_e2e not built (make -C duckdb-cudasp-extension_amd)")
-    threads = args.e2e_threads or 8 * world
+    # 8 executor threads per GPU, but never more than the host cores this
+    # process is allotted: oversubscribed threads collapse the host feed
+    # (the cgroup's CPU quota throttles them; 64 threads on 16 cores run at
+    # ~0.33 G rows/s against ~0.87 G for 16, profiles/r05_host_ceiling.txt)
+    threads = args.e2e_threads or max(1, min(8 * world, host_cores()[0]))
     reps = args.e2e_reps or (5 if args.rows <= 2_000_000 else 3 if args.rows <= 10_000_000 else 1)
     env = dict(os.environ, CUDASP_FB_BITS=str(fb_bits))
     env.pop("CUDASP_TF_MODE", None)
@@ -894,7 +898,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-e2e-launch", action="store_true",
                     help="skip the second end-to-end leg with the host's per-slot launches (CUDASP_TF_MODE=launch)")
-    ap.add_argument("--e2e-threads", type=int, default=0, help="executor threads of the e2e leg; 0 = 8 per GPU")
+    ap.add_argument("--e2e-threads", type=int, default=0,
+                    help="executor threads of the e2e leg; 0 = 8 per GPU, at most the allotted host cores")
     ap.add_argument("--e2e-reps", type=int, default=0, help="timed e2e queries (median); 0 = by table size")
     ap.add_argument("--e2e-input", choices=["rows", "columns"], default="rows")
     ap.add_argument("--e2e-hw-queues", type=int, default=0,

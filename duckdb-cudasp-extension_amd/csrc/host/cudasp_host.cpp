@@ -56,6 +56,7 @@
 #include <vector>
 
 #include "../../../include/cudasp_abi.h"
+#include "slot_copy.hpp"
 
 namespace {
 
@@ -97,6 +98,16 @@ void write_err(char* err, size_t cap, const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(err, cap, fmt, ap);
   va_end(ap);
+}
+
+// Non-temporal stores for the copies into the slots (slot_copy.hpp);
+// CUDASP_TF_NT=0 selects plain memcpy (A/B).
+bool slot_nt() {
+  static const bool on = [] {
+    const char* e = getenv("CUDASP_TF_NT");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
 }
 
 double now_s() {
@@ -193,6 +204,7 @@ struct FeedSlot {
   size_t outputs_cap = 0;
   uint32_t* h_matches = nullptr;  // streaming feed: the kernel's matching row indices (cap_rows)
   bool coherent = false;          // host buffers from cudasp_host_alloc (streaming feed)
+  bool host_mem = false;          // host buffers from aligned_alloc (null-device measurement feed)
   // emit data of the rows (pageable; only read for matches)
   std::vector<uint8_t> txid_bytes;  // size() is the capacity
   std::vector<uint64_t> txid_off;   // cap_rows
@@ -237,8 +249,12 @@ struct FeedRes {
   cudasp_stream* stream = nullptr;
   uint32_t stream_blocks = 0;
   int stream_slots = FEED_STREAM_SLOTS;  // slots of a streaming feed (feed_stream_slots at creation)
+  // null-device measurement feed (CUDASP_TF_NULL_DEVICE): no scanner, no
+  // stream, no device call at all -- the slots are plain host memory -- so
+  // the host's own ceiling can be measured anywhere, a GPU-less box included
+  bool host_only = false;
   std::vector<void*> stale_host, stale_dev;
-  int nslots() const { return stream ? stream_slots : nstreams + 2; }
+  int nslots() const { return stream || host_only ? stream_slots : nstreams + 2; }
 };
 
 void free_stale(FeedRes& r) {
@@ -252,7 +268,9 @@ void free_slot(FeedSlot& s) {
   void* host[] = {s.h_tweaks, s.h_offs, s.h_lens, s.h_flags, s.h_outputs, s.h_matches};
   for (void* p : host)
     if (p) {
-      if (s.coherent)
+      if (s.host_mem)
+        free(p);
+      else if (s.coherent)
         cudasp_host_free(p);
       else
         (void)hipHostFree(p);
@@ -294,12 +312,12 @@ constexpr size_t POOL_MAX = 64;
 std::mutex g_pool_mu;
 std::vector<FeedRes*> g_pool;
 
-FeedRes* pool_take(int device, uint32_t cap_rows, int nstreams, uint32_t stream_blocks) {
+FeedRes* pool_take(int device, uint32_t cap_rows, int nstreams, uint32_t stream_blocks, bool host_only = false) {
   std::lock_guard<std::mutex> lock(g_pool_mu);
   for (size_t i = 0; i < g_pool.size(); i++) {
     FeedRes* r = g_pool[i];
     if (r->device == device && r->cap_rows == cap_rows && r->nstreams == nstreams &&
-        (r->stream ? r->stream_blocks : 0u) == stream_blocks) {
+        (r->stream ? r->stream_blocks : 0u) == stream_blocks && r->host_only == host_only) {
       g_pool[i] = g_pool.back();
       g_pool.pop_back();
       return r;
@@ -366,6 +384,40 @@ int prepare_slot(FeedSlot& s, int device, uint32_t cap_rows, size_t words, size_
     s.h_outputs = nullptr;
     s.outputs_cap = 0;
     HOST_HIP(hipHostMalloc((void**)&s.h_outputs, cap * sizeof(int64_t), pinned_flags()));
+    s.outputs_cap = cap;
+  }
+  if (txid > s.txid_bytes.size()) s.txid_bytes.resize(txid);
+  return CUDASP_OK;
+}
+
+// A null-device feed's slot (measurement): the same host buffers as a
+// streaming slot, from aligned_alloc, and no device mirror.
+int prepare_slot_host(FeedRes& r, FeedSlot& s, size_t words, size_t txid) {
+  const size_t n = r.cap_rows;
+  auto host = [&](void** p, size_t bytes) -> int {
+    *p = aligned_alloc(4096, (bytes + 4095) / 4096 * 4096);
+    return *p ? CUDASP_OK : host_fail(CUDASP_ERR_CAPACITY, "host slot allocation of %zu bytes failed", bytes);
+  };
+  if (!s.allocated) {
+    s.host_mem = true;
+    int rc = host((void**)&s.h_tweaks, n * 64);
+    if (rc == CUDASP_OK) rc = host((void**)&s.h_offs, n * 4);
+    if (rc == CUDASP_OK) rc = host((void**)&s.h_lens, n * 4);
+    if (rc == CUDASP_OK) rc = host((void**)&s.h_matches, n * 4);
+    if (rc != CUDASP_OK) return rc;
+    s.txid_off.resize(n);
+    s.txid_size.resize(n);
+    s.heights.resize(n);
+    s.allocated = true;
+  }
+  if (words > s.outputs_cap) {
+    size_t cap = s.outputs_cap ? s.outputs_cap : 4096;
+    while (cap < words) cap *= 2;
+    free(s.h_outputs);
+    s.h_outputs = nullptr;
+    s.outputs_cap = 0;
+    const int rc = host((void**)&s.h_outputs, cap * sizeof(int64_t));
+    if (rc != CUDASP_OK) return rc;
     s.outputs_cap = cap;
   }
   if (txid > s.txid_bytes.size()) s.txid_bytes.resize(txid);
@@ -491,6 +543,7 @@ struct cudasp_tf_global {
   // faster end to end); CUDASP_TF_MODE=launch selects the
   // per-slot launches.
   bool streaming = false;
+  bool null_device = false;  // CUDASP_TF_NULL_DEVICE: measurement-only feeds (Feed::null_device)
   std::atomic<bool> streaming_fallback{false};  // this query's keys/options rule the streaming scan out (feed_for)
 };
 
@@ -520,7 +573,7 @@ int feed_error(const Feed& f) { return host_fail(f.error, "%s", f.error_msg.c_st
 int launch_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   FeedRes& r = *f.res;
   s.state = SLOT_BUSY;
-  s.stream = (int)(f.launch_seq++ % (uint32_t)r.nstreams);
+  s.stream = r.nstreams ? (int)(f.launch_seq++ % (uint32_t)r.nstreams) : 0;
   const uint32_t n = s.rows;
   const size_t words = s.words;
   lk.unlock();
@@ -802,8 +855,9 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
         if (!s.allocated || s.outputs_cap < want_words || s.txid_bytes.size() < want_tx) {
           s.state = SLOT_BUSY;
           lk.unlock();
-          const int rc = r.stream ? prepare_slot_streaming(r, s, want_words, want_tx)
-                                  : prepare_slot(s, r.device, r.cap_rows, want_words, want_tx);
+          const int rc = r.host_only ? prepare_slot_host(r, s, want_words, want_tx)
+                         : r.stream  ? prepare_slot_streaming(r, s, want_words, want_tx)
+                                     : prepare_slot(s, r.device, r.cap_rows, want_words, want_tx);
           lk.lock();
           s.state = SLOT_FREE;
           f.cv.notify_all();
@@ -845,8 +899,9 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
           f.txid_per_row = std::max(f.txid_per_row, (double)ntx / r.cap_rows);
           s.state = SLOT_BUSY;
           lk.unlock();
-          const int rc = r.stream ? prepare_slot_streaming(r, s, nwords, ntx)
-                                  : prepare_slot(s, r.device, r.cap_rows, nwords, ntx);
+          const int rc = r.host_only ? prepare_slot_host(r, s, nwords, ntx)
+                         : r.stream  ? prepare_slot_streaming(r, s, nwords, ntx)
+                                     : prepare_slot(s, r.device, r.cap_rows, nwords, ntx);
           lk.lock();
           s.state = SLOT_FILLING;
           f.cv.notify_all();
@@ -972,6 +1027,28 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
   if ((*out = g.feed_ptr[lg].load(std::memory_order_acquire)) != nullptr) return CUDASP_OK;
   const int device = g.device_map[lg];
   const uint32_t cap_rows = (uint32_t)(b.batch_size + CUDASP_TF_VECTOR_SIZE);
+  if (g.null_device) {  // (pooled apart from real feeds: pool_take matches host_only)
+    FeedRes* r = pool_take(device, cap_rows, 0, 0, true);
+    if (!r) {
+      r = new FeedRes();
+      r->device = device;
+      r->cap_rows = cap_rows;
+      r->host_only = true;
+      r->stream_slots = feed_stream_slots();
+    }
+    auto f = std::make_unique<Feed>();
+    f->res = r;
+    f->g = &g;
+    f->batch_size = b.batch_size;
+    f->ow = out_words(b);
+    f->words_per_row = 2.0 * f->ow;
+    f->ramp = 5;
+    f->null_device = true;
+    *out = f.get();
+    g.feeds[lg] = std::move(f);
+    g.feed_ptr[lg].store(*out, std::memory_order_release);
+    return CUDASP_OK;
+  }
   const auto* scan = (const uint8_t*)b.scan_private_key_data.data();
   const auto* spend = (const uint8_t*)b.spend_public_key_data.data();
   const auto* labels = (const uint8_t*)b.label_keys_flat.data();
@@ -1046,7 +1123,6 @@ int feed_for(cudasp_tf_global& g, const cudasp_tf_bind_data& b, int lg, Feed** o
   }
   if (r->stream) (void)cudasp_stream_set_timeout(r->stream, stream_timeout_ms());
   auto f = std::make_unique<Feed>();
-  if (const char* e = getenv("CUDASP_TF_NULL_DEVICE")) f->null_device = atoi(e) != 0;
   if (const char* e = getenv("CUDASP_TF_TEST_LATE_SEQ")) {
     f->late_seq = atoll(e);
     const char* ms = getenv("CUDASP_TF_TEST_LATE_MS");
@@ -1101,24 +1177,46 @@ int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_t
   const double t1 = now_s();
   FeedSlot& s = *res.slot;
   const uint32_t r0 = res.row0;
+  const bool nt = slot_nt();
   memcpy(s.heights.data() + r0, c.height, (size_t)n * sizeof(int32_t));
   uint8_t* tw = s.h_tweaks + (size_t)r0 * TWEAK_KEY_SIZE;
-  for (uint32_t i = 0; i < n; i++) memcpy(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak_data[i], TWEAK_KEY_SIZE);
   size_t tx = res.tx0;
   uint8_t* txb = s.txid_bytes.data();
-  for (uint32_t i = 0; i < n; i++) {
-    const uint32_t sz = c.txid_size[i];
-    s.txid_off[r0 + i] = tx;
-    s.txid_size[r0 + i] = sz;
-    if (sz == 32)
-      memcpy(txb + tx, c.txid_data[i], 32);
-    else if (sz)
-      memcpy(txb + tx, c.txid_data[i], sz);
-    tx += sz;
+  if (nt) {
+    // one pass per row: its 64-byte tweak blob, then its txid (32-byte txids
+    // at 16-byte aligned offsets take non-temporal stores too)
+    for (uint32_t i = 0; i < n; i++) {
+      cudasp_host::nt_copy64(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak_data[i]);
+      const uint32_t sz = c.txid_size[i];
+      s.txid_off[r0 + i] = tx;
+      s.txid_size[r0 + i] = sz;
+      if (sz == 32 && ((uintptr_t)(txb + tx) & 15) == 0)
+        cudasp_host::nt_copy32(txb + tx, c.txid_data[i]);
+      else if (sz)
+        memcpy(txb + tx, c.txid_data[i], sz);
+      tx += sz;
+    }
+  } else {
+    for (uint32_t i = 0; i < n; i++) memcpy(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak_data[i], TWEAK_KEY_SIZE);
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t sz = c.txid_size[i];
+      s.txid_off[r0 + i] = tx;
+      s.txid_size[r0 + i] = sz;
+      if (sz == 32)
+        memcpy(txb + tx, c.txid_data[i], 32);
+      else if (sz)
+        memcpy(txb + tx, c.txid_data[i], sz);
+      tx += sz;
+    }
   }
   size_t o = res.word0;  // one word per output (no full_x here)
   if (lists_contiguous) {
-    if (nouts) memcpy(s.h_outputs + o, c.child_values + first, nouts * sizeof(int64_t));
+    if (nouts) {
+      if (nt)
+        cudasp_host::nt_copy(s.h_outputs + o, c.child_values + first, nouts * sizeof(int64_t));
+      else
+        memcpy(s.h_outputs + o, c.child_values + first, nouts * sizeof(int64_t));
+    }
     for (uint32_t i = 0; i < n; i++) {
       s.h_offs[r0 + i] = (uint32_t)(o + (c.list_offset[i] - first));
       s.h_lens[r0 + i] = (uint32_t)c.list_length[i];
@@ -1132,6 +1230,7 @@ int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_t
       o += len;
     }
   }
+  if (nt) cudasp_host::slot_copy_fence();
   return feed_commit(*f, s, t1 - t0, now_s() - t1);
 }
 
@@ -1285,15 +1384,18 @@ int feed_columns(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_lo
   const size_t obase = res.word0 / ow;
   if (fast) {
     uint32_t sz;
-    memcpy(s.h_tweaks + (size_t)rbase * TWEAK_KEY_SIZE, tweak_ptr(r0, &sz), n * TWEAK_KEY_SIZE);
+    const auto copy = slot_nt() ? cudasp_host::nt_copy : [](void* d, const void* src, size_t bytes) {
+      memcpy(d, src, bytes);
+    };
+    copy(s.h_tweaks + (size_t)rbase * TWEAK_KEY_SIZE, tweak_ptr(r0, &sz), n * TWEAK_KEY_SIZE);
     memcpy(s.heights.data() + rbase, c.height + c.height_offset + r0, n * sizeof(int32_t));
-    if (ntx) memcpy(s.txid_bytes.data() + res.tx0, c.txid_data + txo[r0], ntx);
+    if (ntx) copy(s.txid_bytes.data() + res.tx0, c.txid_data + txo[r0], ntx);
     const uint64_t first = (uint64_t)lo[r0];
     if (nouts) {
       if (b.opt.full_x)
-        memcpy(s.h_outputs + obase * ow, c.child_blob_data + (c.child_offset + first) * XONLY_SIZE, nouts * XONLY_SIZE);
+        copy(s.h_outputs + obase * ow, c.child_blob_data + (c.child_offset + first) * XONLY_SIZE, nouts * XONLY_SIZE);
       else
-        memcpy(s.h_outputs + obase, c.child_values + c.child_offset + first, nouts * sizeof(int64_t));
+        copy(s.h_outputs + obase, c.child_values + c.child_offset + first, nouts * sizeof(int64_t));
     }
     for (uint64_t i = r0; i < r1; i++) {
       const uint32_t row = rbase + (uint32_t)(i - r0);
@@ -1302,6 +1404,7 @@ int feed_columns(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_lo
       s.h_offs[row] = (uint32_t)(obase + ((uint64_t)lo[i] - first));
       s.h_lens[row] = (uint32_t)(lo[i + 1] - lo[i]);
     }
+    if (slot_nt()) cudasp_host::slot_copy_fence();
     return feed_commit(*f, s, t1 - t0, now_s() - t1);
   }
   uint32_t r = rbase;
@@ -1525,6 +1628,7 @@ int cudasp_tf_init(const cudasp_tf_bind_data* b, cudasp_tf_global** out) {
     }
   }
   g->bind = b;
+  if (const char* e = getenv("CUDASP_TF_NULL_DEVICE")) g->null_device = atoi(e) != 0;
   const char* hq = getenv("GPU_MAX_HW_QUEUES");
   g->hw_queues = hq && atoi(hq) > 0 ? atoi(hq) : 4;
   int feeds_per_device = 0;

@@ -1172,7 +1172,10 @@ __device__ __forceinline__ uint32_t stream_unit_rows(uint32_t uh, int K) {
   return r;
 }
 
-template <int FBB>
+// WIDE: output_count K > MULTI_RMAX (one row per piece, its indices in groups
+// of MULTI_RMAX, no pipelining) -- a separate instance, so the default
+// instance's register allocation is the pipelined body's alone.
+template <int FBB, bool WIDE>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtrl* ctrl, StreamDev* dev,
                                                                     const int8_t* __restrict__ naf, ScanConsts k,
                                                                     const uint32_t* __restrict__ fb,
@@ -1199,7 +1202,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
   // units in the pipelined schedule; K > MULTI_RMAX (`wide`): one row per
   // piece, its K indices in groups of MULTI_RMAX, unpipelined (stream_wide)
   const int K = (int)k.output_count;
-  const bool wide = K > MULTI_RMAX;
+  constexpr bool wide = WIDE;
   const bool with_labels = k.label_count != 0;
   const uint32_t ow = k.full_x ? 4u : 1u;
   // pieces of the pipelined schedule: P (F points pending), Q (labels
@@ -1331,7 +1334,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
       scr_load(F.x, sc, QF + 2 * FW * u);
       scr_load(F.y, sc, QF + 2 * FW * u + FW);
     };
-    if (count_q) {  // piece Q: its labels against the mirrored outputs, then its results
+    if (!wide && count_q) {  // piece Q: its labels against the mirrored outputs, then its results
       const StreamWr* wq = wrs[wid][pq];
       const int meta_q = META + 2 * MULTI_RMAX * pq;
       const auto q_out = [&](int u, const int64_t*& o, uint32_t& off, uint32_t& len, int64_t*& vrow,
@@ -1349,7 +1352,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
       stream_emit(ctrl, dev, wq, count_q, lane, hits_q);
       count_q = 0;
     }
-    if (count_p) {  // piece P: affine F, base compare; its labels wait one iteration
+    if (!wide && count_p) {  // piece P: affine F, base compare; its labels wait one iteration
       const StreamWr* wp = wrs[wid][pp];
       const int meta_p = META + 2 * MULTI_RMAX * pp;
       uint32_t hits = 0;
@@ -1386,7 +1389,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
     }
     // t of each new row (K output indices), then stage B's F = t G + B into
     // slots u = j K + kk
-    if (wide) {
+    if constexpr (wide) {
       // K > MULTI_RMAX: the piece (count rows, rmax 1: one) is finished here,
       // its indices in groups of g <= MULTI_RMAX F points with one inversion
       // each (the S points were inverted above, alone: P and Q stay empty)
@@ -1498,7 +1501,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
         pend_store(sc, PB, u, F);
       }
     }
-    if (!wide) {  // the new piece becomes P
+    if constexpr (!wide) {  // the new piece becomes P
       const int t = pp;
       pp = pn;
       pn = t;
@@ -2942,7 +2945,9 @@ static int stream_launch(cudasp_stream* st) {
   const uint32_t rmax = std::max(1u, std::min(st->rmax, (uint32_t)MULTI_RMAX / K));
   hipLaunchKernelGGL(k_stream_start, dim3(1), dim3(64), 0, s->stream, st->dev,
                      (uint32_t)st->blocks * (BLOCK / 64u) - 1u);  // every wave but the poller
-  auto kf = s->fb_bits == 26 ? k_scan_stream<26> : k_scan_stream<22>;
+  const bool wide = K > (uint32_t)MULTI_RMAX;
+  auto kf = s->fb_bits == 26 ? (wide ? k_scan_stream<26, true> : k_scan_stream<26, false>)
+                             : (wide ? k_scan_stream<22, true> : k_scan_stream<22, false>);
   hipLaunchKernelGGL(kf, dim3((uint32_t)st->blocks), dim3(BLOCK), 0, s->stream, st->ctrl, st->dev, s->d_naf,
                      s->consts, s->d_fb, s->d_labels, s->d_mscratch, rmax, st->idle_ticks, st->wstat, st->prio_ticks, st->pf_coal);
   HIP_TRY(hipGetLastError());

@@ -310,7 +310,7 @@ def test_stream_rejects_bad_use(torch):
             q = sb.publish(st)
             st.wait(q)
             st.finish()
-        s.set_options(output_count=7)  # K x rows of a piece must fit the kernel's pending slots
+        s.set_fixed_base_bits(7)  # the LDS-staged width: stage B of the stream reads an HBM table
         with pytest.raises(CudaspError):
             ScanStream(s)
     assert StreamBatch is not None

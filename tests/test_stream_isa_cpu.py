@@ -30,7 +30,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "duckdb-cudasp-extension_amd", "libcudasp_amd.so")
 EMU = os.path.join(ROOT, "tests", "native", "libcudasp_emu29.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
-KERNELS = ("_Z13k_scan_streamILi26E", "_Z13k_scan_streamILi22E")
+KERNELS = ("_Z13k_scan_streamILi26ELb0E", "_Z13k_scan_streamILi22ELb0E", "_Z13k_scan_streamILi26ELb1E",
+           "_Z13k_scan_streamILi22ELb1E")
 
 
 def layout():

@@ -22,7 +22,7 @@
 //   host_e2e [--rows N] [--threads T] [--batch B] [--labels L --labels-file F]
 //            [--outputs K | --outputs-max KMAX] [--input rows|columns]
 //            [--reps R] [--warm-reps W [--warm-ms MS]] [--plant-sample FILE]
-//            [--null-device]
+//            [--null-device [--cpu-table]]
 // (W more queries, each started right after MS ms of a busy kernel on every
 // GPU: the rate at full clock, without the ramp from idle; warm_tx_per_s)
 // --plant-sample writes 256 planted rows and 256 unplanted rows, strided over
@@ -34,7 +34,9 @@
 // feeds mark every slot done at launch, with no device work, so tx_per_s is
 // the executor threads' own ceiling (reserve, copies into the pinned slots,
 // harvest) -- the host's capacity to feed N GPUs; a query then passes when
-// it emits nothing.
+// it emits nothing.  --cpu-table (with --null-device) fills the table on the
+// CPU (pseudo-random tweak bytes, the same splitmix64 outputs, no plants), so
+// the host's ceiling can be measured with no GPU at all.
 // Label keys: F holds L 64-byte keys (x || y, little-endian, bench.label_keys);
 // without F, L must be 0 or 1 (the SQL test's label, test/sql/cudasp.test:104).
 // Prints one JSON line; exit 0 iff every timed query emitted exactly the
@@ -101,6 +103,7 @@ struct Args {
   int warm_ms = 30;
   std::string plant_sample;  // JSON sample of planted / unplanted rows for the oracle check
   bool null_device = false;  // measurement only: no device work in the host's feeds
+  bool cpu_table = false;    // with null_device: table generated on the CPU, no GPU needed
 };
 
 static Args parse(int argc, char** argv) {
@@ -127,12 +130,14 @@ static Args parse(int argc, char** argv) {
     else if (s == "--warm-ms") a.warm_ms = std::max(1, atoi(val()));
     else if (s == "--plant-sample") a.plant_sample = val();
     else if (s == "--null-device") a.null_device = true;
+    else if (s == "--cpu-table") a.cpu_table = true;
     else {
       fprintf(stderr, "unknown argument %s\n", s.c_str());
       exit(1);
     }
   }
-  if (a.threads < 1 || a.rows == 0 || (a.kmax == 0 && a.k < 1) || a.kmax < 0 || a.labels < 0) {
+  if (a.threads < 1 || a.rows == 0 || (a.kmax == 0 && a.k < 1) || a.kmax < 0 || a.labels < 0 ||
+      (a.cpu_table && !a.null_device)) {
     fprintf(stderr, "bad arguments\n");
     exit(1);
   }
@@ -150,8 +155,41 @@ struct Table {
   uint32_t labels_planted_mask = 0;                 // label indices planted (bit j)
 };
 
+static uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// --cpu-table: the table's shape without a GPU (tweak bytes are not curve
+// points; nothing is scanned, --null-device only).
+static void generate_cpu(const Args& a, Table& t) {
+  const uint64_t rows = t.rows = a.rows;
+  t.tweaks.resize(rows * 64);
+  t.txids.assign(rows * 32, 0);
+  t.heights.resize(rows);
+  t.list_off.resize(rows);
+  t.list_len.resize(rows);
+  uint64_t* tw = reinterpret_cast<uint64_t*>(t.tweaks.data());
+  for (uint64_t i = 0; i < rows * 8; i++) tw[i] = splitmix64(i);
+  t.outputs.reserve(a.kmax ? rows * (a.kmax + 1) / 2 : rows * a.k);
+  for (uint64_t g = 0; g < rows; g++) {
+    const uint32_t len = a.kmax ? 1u + (uint32_t)(splitmix64(~OUTPUT_SEED ^ g) % a.kmax) : (uint32_t)a.k;
+    t.list_off[g] = t.outputs.size();
+    t.list_len[g] = len;
+    for (uint32_t j = 0; j < len; j++) t.outputs.push_back((int64_t)splitmix64(OUTPUT_SEED ^ (g * len + j)));
+    for (int b = 0; b < 8; b++) t.txids[g * 32 + 31 - b] = (uint8_t)(g >> (8 * b));
+    t.heights[g] = 800000 + (int32_t)(g / 4000);
+  }
+}
+
 static void generate(const Args& a, const uint8_t scan[32], const uint8_t spend[64],
                      const std::vector<uint8_t>& labels, Table& t) {
+  if (a.cpu_table) {
+    generate_cpu(a, t);
+    return;
+  }
   const uint64_t rows = t.rows = a.rows;
   t.tweaks.resize(rows * 64);
   t.txids.assign(rows * 32, 0);
