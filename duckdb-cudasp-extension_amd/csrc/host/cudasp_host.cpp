@@ -209,6 +209,13 @@ struct FeedSlot {
   std::vector<uint8_t> txid_bytes;  // size() is the capacity
   std::vector<uint64_t> txid_off;   // cap_rows
   std::vector<uint32_t> txid_size;  // cap_rows
+  // runs of rows whose txids are all 32 bytes, back to back from tx0 (a
+  // chunk's rows; txid_off / txid_size are not written for them): r0, n, tx0
+  struct TxRun {
+    uint32_t r0, n;
+    uint64_t tx0;
+  };
+  std::vector<TxRun> tx_runs;  // by r0 (reservations of a slot come in row order)
   std::vector<int32_t> heights;     // cap_rows
   // device buffers
   uint8_t* d_rows = nullptr;
@@ -693,7 +700,14 @@ int harvest_locked(Feed& f, FeedSlot& s, std::unique_lock<std::mutex>& lk) {
   if (e == hipSuccess && !f.null_device) {
     cudasp_tf_global& g = *f.g;
     const auto emit = [&](uint32_t i) {
-      g.output_txids.emplace_back((const char*)s.txid_bytes.data() + s.txid_off[i], s.txid_size[i]);
+      // a row of a 32-byte-txid run, else its own offset and size
+      auto it = std::upper_bound(s.tx_runs.begin(), s.tx_runs.end(), i,
+                                 [](uint32_t r, const FeedSlot::TxRun& t) { return r < t.r0; });
+      if (it != s.tx_runs.begin() && i - (it - 1)->r0 < (it - 1)->n)
+        g.output_txids.emplace_back((const char*)s.txid_bytes.data() + (it - 1)->tx0 + 32ull * (i - (it - 1)->r0),
+                                    32);
+      else
+        g.output_txids.emplace_back((const char*)s.txid_bytes.data() + s.txid_off[i], s.txid_size[i]);
       g.output_heights.push_back(s.heights[i]);
       g.output_tweak_keys.emplace_back((const char*)s.h_tweaks + (size_t)i * TWEAK_KEY_SIZE, TWEAK_KEY_SIZE);
     };
@@ -827,10 +841,14 @@ struct Reservation {
   size_t tx0 = 0;
 };
 
+// Reservation flags: every txid of the chunk is 32 bytes (its rows become a
+// TxRun; the writer skips txid_off / txid_size).
+constexpr int RES_TXID32 = 1;
+
 // Room for a chunk of nrows rows, nwords output words and ntx txid bytes in
 // the feed's open slot.  Blocks while the ring is busy; harvests finished
 // slots on the way (that wait is the executor threads' back-pressure).
-int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation* out) {
+int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation* out, int flags = 0) {
   FeedRes& r = *f.res;
   std::unique_lock<std::mutex> lk(f.mu);
   for (;;) {
@@ -868,6 +886,7 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
         s.words = 0;
         s.txid_used = 0;
         s.writers = 0;
+        s.tx_runs.clear();
         continue;
       }
       case SLOT_FILLING: {
@@ -882,6 +901,7 @@ int feed_reserve(Feed& f, uint32_t nrows, size_t nwords, size_t ntx, Reservation
           out->row0 = s.rows;
           out->word0 = s.words;
           out->tx0 = s.txid_used;
+          if (flags & RES_TXID32) s.tx_runs.push_back(FeedSlot::TxRun{s.rows, nrows, s.txid_used});
           s.rows += nrows;
           s.words += nwords;
           s.txid_used += ntx;
@@ -1159,11 +1179,13 @@ int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_t
   const uint32_t n = c.count;
   size_t nouts = 0, ntx = 0;
   bool lists_contiguous = true;
+  bool txid32 = true;
   const uint64_t first = n ? c.list_offset[0] : 0;
   for (uint32_t i = 0; i < n; i++) {
     if (c.tweak_size[i] != TWEAK_KEY_SIZE)
       return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", c.tweak_size[i]);
     ntx += c.txid_size[i];
+    txid32 &= c.txid_size[i] == 32;
     lists_contiguous &= c.list_offset[i] == first + nouts;
     nouts += c.list_length[i];
   }
@@ -1172,17 +1194,30 @@ int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_t
   if (rc != CUDASP_OK) return rc;
   Reservation res;
   const double t0 = now_s();
-  rc = feed_reserve(*f, n, nouts, ntx, &res);
+  const bool nt = slot_nt();
+  txid32 = txid32 && nt;
+  rc = feed_reserve(*f, n, nouts, ntx, &res, txid32 ? RES_TXID32 : 0);
   if (rc != CUDASP_OK) return rc;
   const double t1 = now_s();
   FeedSlot& s = *res.slot;
   const uint32_t r0 = res.row0;
-  const bool nt = slot_nt();
   memcpy(s.heights.data() + r0, c.height, (size_t)n * sizeof(int32_t));
   uint8_t* tw = s.h_tweaks + (size_t)r0 * TWEAK_KEY_SIZE;
   size_t tx = res.tx0;
   uint8_t* txb = s.txid_bytes.data();
-  if (nt) {
+  if (txid32) {
+    // one pass per row: its 64-byte tweak blob and its 32-byte txid (a TxRun:
+    // no per-row txid offset or size), non-temporal where aligned
+    uint8_t* tb = txb + tx;
+    const bool tb16 = ((uintptr_t)tb & 15) == 0;
+    for (uint32_t i = 0; i < n; i++) {
+      cudasp_host::nt_copy64(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak_data[i]);
+      if (tb16)
+        cudasp_host::nt_copy32(tb + 32 * (size_t)i, c.txid_data[i]);
+      else
+        memcpy(tb + 32 * (size_t)i, c.txid_data[i], 32);
+    }
+  } else if (nt) {
     // one pass per row: its 64-byte tweak blob, then its txid (32-byte txids
     // at 16-byte aligned offsets take non-temporal stores too)
     for (uint32_t i = 0; i < n; i++) {
@@ -1217,9 +1252,21 @@ int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_t
       else
         memcpy(s.h_outputs + o, c.child_values + first, nouts * sizeof(int64_t));
     }
-    for (uint32_t i = 0; i < n; i++) {
-      s.h_offs[r0 + i] = (uint32_t)(o + (c.list_offset[i] - first));
-      s.h_lens[r0 + i] = (uint32_t)c.list_length[i];
+    if (nt) {
+      // through a small buffer, so the slot's offsets and lengths are
+      // written non-temporally too
+      uint32_t bo[CUDASP_TF_VECTOR_SIZE], bl[CUDASP_TF_VECTOR_SIZE];
+      for (uint32_t i = 0; i < n; i++) {
+        bo[i] = (uint32_t)(o + (c.list_offset[i] - first));
+        bl[i] = (uint32_t)c.list_length[i];
+      }
+      cudasp_host::nt_copy(s.h_offs + r0, bo, (size_t)n * 4);
+      cudasp_host::nt_copy(s.h_lens + r0, bl, (size_t)n * 4);
+    } else {
+      for (uint32_t i = 0; i < n; i++) {
+        s.h_offs[r0 + i] = (uint32_t)(o + (c.list_offset[i] - first));
+        s.h_lens[r0 + i] = (uint32_t)c.list_length[i];
+      }
     }
   } else {
     for (uint32_t i = 0; i < n; i++) {
@@ -1376,7 +1423,12 @@ int feed_columns(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_lo
   if (rc != CUDASP_OK) return rc;
   Reservation res;
   const double t0 = now_s();
-  rc = feed_reserve(*f, nrows, nouts * ow, ntx, &res);
+  // every txid 32 bytes (a fixed_size_binary(32) column, or uniform binary):
+  // the rows become a TxRun, no per-row txid offsets
+  bool txid32 = fast && slot_nt() && ntx == 32 * (size_t)n;
+  if (txid32)
+    for (uint64_t i = r0; i < r1 && txid32; i++) txid32 = txo[i + 1] - txo[i] == 32;
+  rc = feed_reserve(*f, nrows, nouts * ow, ntx, &res, txid32 ? RES_TXID32 : 0);
   if (rc != CUDASP_OK) return rc;
   const double t1 = now_s();
   FeedSlot& s = *res.slot;
@@ -1397,14 +1449,28 @@ int feed_columns(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_lo
       else
         copy(s.h_outputs + obase, c.child_values + c.child_offset + first, nouts * sizeof(int64_t));
     }
-    for (uint64_t i = r0; i < r1; i++) {
-      const uint32_t row = rbase + (uint32_t)(i - r0);
-      s.txid_off[row] = res.tx0 + (size_t)(txo[i] - txo[r0]);
-      s.txid_size[row] = (uint32_t)(txo[i + 1] - txo[i]);
-      s.h_offs[row] = (uint32_t)(obase + ((uint64_t)lo[i] - first));
-      s.h_lens[row] = (uint32_t)(lo[i + 1] - lo[i]);
+    if (!txid32)
+      for (uint64_t i = r0; i < r1; i++) {
+        const uint32_t row = rbase + (uint32_t)(i - r0);
+        s.txid_off[row] = res.tx0 + (size_t)(txo[i] - txo[r0]);
+        s.txid_size[row] = (uint32_t)(txo[i + 1] - txo[i]);
+      }
+    if (slot_nt()) {
+      uint32_t bo[CUDASP_TF_VECTOR_SIZE], bl[CUDASP_TF_VECTOR_SIZE];
+      for (uint64_t i = r0; i < r1; i++) {
+        bo[i - r0] = (uint32_t)(obase + ((uint64_t)lo[i] - first));
+        bl[i - r0] = (uint32_t)(lo[i + 1] - lo[i]);
+      }
+      cudasp_host::nt_copy(s.h_offs + rbase, bo, (size_t)n * 4);
+      cudasp_host::nt_copy(s.h_lens + rbase, bl, (size_t)n * 4);
+      cudasp_host::slot_copy_fence();
+    } else {
+      for (uint64_t i = r0; i < r1; i++) {
+        const uint32_t row = rbase + (uint32_t)(i - r0);
+        s.h_offs[row] = (uint32_t)(obase + ((uint64_t)lo[i] - first));
+        s.h_lens[row] = (uint32_t)(lo[i + 1] - lo[i]);
+      }
     }
-    if (slot_nt()) cudasp_host::slot_copy_fence();
     return feed_commit(*f, s, t1 - t0, now_s() - t1);
   }
   uint32_t r = rbase;
