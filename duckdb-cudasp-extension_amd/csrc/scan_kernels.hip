@@ -462,44 +462,14 @@ constexpr uint32_t MULTI_TRACE_WAVES = 8192;
 __device__ uint64_t g_multi_trace[MULTI_TRACE_WAVES * 4];
 #endif
 
-// The ladder hook of k_scan_multi's PRIO instance (CUDASP_MULTI_PRIO_US, an
-// A/B knob): k_scan_stream's issue priority by the age of the wave's oldest
-// unfinished piece (stream_prio), refreshed every 16 ladder steps.
-struct MultiTick {
-  volatile uint64_t* t_old;  // LDS: when the wave claimed its oldest unfinished piece
-  uint64_t step;
-  __device__ __forceinline__ void operator()() const {
-    const uint64_t v = *t_old;
-    const uint64_t t0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
-                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
-    switch (stream_prio(wall_clock64() - t0, step)) {
-      case 0:
-        __builtin_amdgcn_s_setprio(0);
-        break;
-      case 1:
-        __builtin_amdgcn_s_setprio(1);
-        break;
-      case 2:
-        __builtin_amdgcn_s_setprio(2);
-        break;
-      default:
-        __builtin_amdgcn_s_setprio(3);
-        break;
-    }
-  }
-};
-
-// PRIO: the instance with MultiTick in the stage-A ladder (prio_ticks > 0);
-// the default instance has no hook at all.
-template <int FBB, bool PIPE, bool PRIO>
+template <int FBB, bool PIPE>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const MultiBatch* __restrict__ bd, uint32_t nb,
                                                                    uint32_t total_wr, const int8_t* __restrict__ naf,
                                                                    ScanConsts k, const uint32_t* __restrict__ fb,
                                                                    const uint32_t* __restrict__ labels,
                                                                    uint32_t* __restrict__ scr,
                                                                    uint32_t* __restrict__ counter, uint32_t g1,
-                                                                   uint32_t g2, uint32_t rmax, uint32_t adaptive,
-                                                                   uint64_t prio_ticks) {
+                                                                   uint32_t g2, uint32_t rmax, uint32_t adaptive) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = make_scratch(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
@@ -515,9 +485,6 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
   int count_p = 0, count_q = 0;
   bool more = true;
   uint32_t mine = 0;  // wave-rows this wave has claimed (lane 0)
-  __shared__ uint64_t prio_t[PRIO ? BLOCK / 64 : 1];  // per wave: claim time of its oldest unfinished piece
-  uint64_t t_claim_p = 0;  // PRIO: when piece P was claimed
-  const MultiTick tick{&prio_t[PRIO ? threadIdx.x >> 6 : 0], prio_ticks};
 #if CUDASP_MULTI_TRACE
   const uint64_t trace_t0 = wall_clock64();
   uint32_t trace_pieces = 0, trace_rows = 0;
@@ -542,11 +509,6 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
         count = (int)(R < total_wr - base ? R : total_wr - base);
     }
     if (count == 0 && count_p == 0 && count_q == 0) break;
-    uint64_t t_claim = 0;
-    if constexpr (PRIO) {
-      t_claim = wall_clock64();
-      if (lane == 0) prio_t[threadIdx.x >> 6] = count_p ? t_claim_p : t_claim;
-    }
 #if CUDASP_MULTI_TRACE
     trace_pieces += count ? 1u : 0u;
     trace_rows += (uint32_t)count;
@@ -564,10 +526,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
         y[q] = b.ty[(size_t)q * b.n + r];
       }
       gej P;
-      if constexpr (PRIO)
-        row_shared_secret_point_t(P, x, y, naf, k.naf_len, sc, tick);
-      else
-        row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
+      row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
       pend_store(sc, PB, count_p + j, P);
     }
     if constexpr (!PIPE) {
@@ -652,7 +611,6 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
     if constexpr (PIPE) {
       base_p = base;
       count_p = count;
-      if constexpr (PRIO) t_claim_p = t_claim;
     } else {
       pend_invert<MULTI_RMAX>(sc, PB, count);
       multi_finish(bd, nb, base, count, lane, k, labels, sc, PB, LB);
@@ -1940,10 +1898,6 @@ struct cudasp_scanner {
   // k_scan_multi pieces sized by each wave's share of the work done
   // (multi_piece_rows_adaptive); CUDASP_MULTI_ADAPT=0 selects the plain rule
   bool multi_adaptive = true;
-  // A/B knob (round 5): CUDASP_MULTI_PRIO_US > 0 runs k_scan_multi's PRIO
-  // instance, the streaming kernel's wave priority by piece age (100 MHz
-  // ticks per priority level); 0 (default) the instance without the hook
-  uint64_t multi_prio_ticks = 0;
 };
 
 namespace {
@@ -2323,14 +2277,11 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
   HIP_TRY(hipMemsetAsync(s->d_counter, 0, sizeof(uint32_t), st));
   const uint64_t waves = blocks * (BLOCK / 64);
   const uint32_t g1 = (uint32_t)(waves * g1_x100 / 100), g2 = (uint32_t)(waves * g2_x100 / 100);
-  // the PRIO instance only for the CUDASP_MULTI_PRIO_US A/B (pipelined schedule)
-  const bool prio = s->multi_prio_ticks && s->multi_pipe;
-  auto kf = prio ? (s->fb_bits == 26 ? k_scan_multi<26, true, true> : k_scan_multi<22, true, true>)
-        : s->multi_pipe ? (s->fb_bits == 26 ? k_scan_multi<26, true, false> : k_scan_multi<22, true, false>)
-                        : (s->fb_bits == 26 ? k_scan_multi<26, false, false> : k_scan_multi<22, false, false>);
+  auto kf = s->multi_pipe ? (s->fb_bits == 26 ? k_scan_multi<26, true> : k_scan_multi<22, true>)
+                          : (s->fb_bits == 26 ? k_scan_multi<26, false> : k_scan_multi<22, false>);
   hipLaunchKernelGGL(kf, dim3((uint32_t)blocks), dim3(BLOCK), 0, st, s->d_multi, nb, (uint32_t)total_wr, s->d_naf,
                      s->consts, s->d_fb, s->d_labels, s->d_mscratch, s->d_counter, g1, g2, rmax,
-                     s->multi_adaptive ? 1u : 0u, prio ? s->multi_prio_ticks : 0ull);
+                     s->multi_adaptive ? 1u : 0u);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
 }
@@ -2444,10 +2395,6 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
     if (const char* f = getenv("CUDASP_FUSED_SINGLE")) s->fused_single = atoi(f) != 0;
     if (const char* f = getenv("CUDASP_MULTI_PIPE")) s->multi_pipe = atoi(f) != 0;
     if (const char* f = getenv("CUDASP_MULTI_ADAPT")) s->multi_adaptive = atoi(f) != 0;
-    if (const char* f = getenv("CUDASP_MULTI_PRIO_US")) {
-      const long v = atol(f);
-      if (v > 0 && v <= 1000000) s->multi_prio_ticks = (uint64_t)v * 100ull;
-    }
     if (const char* f = getenv("CUDASP_ROWS_A_FORCE")) {
       const int r = atoi(f);
       if (r == 1 || r == 2 || r == ROWS_A) s->rows_a_force = r;

@@ -1,7 +1,8 @@
 # A/B of k_scan_multi's PRIO instance (CUDASP_MULTI_PRIO_US: the streaming
 # kernel's wave priority by piece age in the stage-A ladder) against the
 # default instance, device-resident bench steps at 1M / 3M / 32.7M rows,
-# interleaved, two passes.
+# interleaved, two passes.  (Round 5; the PRIO instance was removed after this
+# A/B, profiles/r05_multi_prio_ab.txt: it needs the round-5 commit that had it.)
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${MEASURE_TAG:-r05}_prio; mkdir -p $O; cd $R
 B="python3 bench.py --no-cpu-baseline --no-e2e --no-layout-probe --idle-samples 0 --exclusive-batches 0"
