@@ -1060,7 +1060,8 @@ def main():
                     rows=args.rows, shard=args.shard, batch_size=args.batch_size, labels=args.labels,
                     output_count=args.output_count, label_negation=args.label_negation,
                     outputs_per_row=round(mean_k, 3), fixed_base_bits=args.fb_bits,
-                    fixed_base_bits_product_default=product_fb_bits, launch=args.launch,
+                    fixed_base_bits_product_default=product_fb_bits, spend_key_folded=scanners[0].spend_folded,
+                    launch=args.launch,
                     streams=1 if multi else args.streams, batches_rank0=tab.nb, parallelism="dp%d" % world),
         roofline=dict(bound="hbm", achieved=achieved_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                       frac=achieved_gbs / HBM_PEAK_GBS, traffic=traffic,

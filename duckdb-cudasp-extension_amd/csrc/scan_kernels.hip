@@ -1541,6 +1541,37 @@ __global__ __launch_bounds__(BLOCK) void k_fb_build(const uint32_t* __restrict__
   for (int q = 0; q < 4; q++) dst[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
 }
 
+// The fixed-base table's top window with the spend key B folded in
+// (ScanConsts::fb_top): entry j of window W - 1 plus B, then minus B, one
+// thread per entry (one inversion for both).  *bad is set if any sum is
+// exceptional (x equal), and the scanner then keeps adding B on its own.
+struct SpendWords {
+  uint32_t w[16];
+};
+template <int BITS>
+__global__ __launch_bounds__(BLOCK) void k_fb_fold(const uint32_t* __restrict__ fb, SpendWords spend,
+                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ bad) {
+  constexpr uint32_t TOP = FbWidth<BITS>::TOP_ENTRIES;
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= TOP) return;
+  ge P, B;
+  ge_from_words(P, fb + ((size_t)(FbWidth<BITS>::WINDOWS - 1) * FbWidth<BITS>::ENTRIES + j) * FB_WORDS);
+  ge_from_words(B, spend.w);
+  uint32_t a[16], b[16];
+  if (!fb_fold_entry(a, b, P, B)) {
+    atomicOr(bad, 1u);
+#pragma unroll
+    for (int q = 0; q < 16; q++) a[q] = b[q] = 0;
+  }
+  uint4* pa = reinterpret_cast<uint4*>(out + (size_t)j * FB_WORDS);
+  uint4* pb = reinterpret_cast<uint4*>(out + ((size_t)TOP + j) * FB_WORDS);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    pa[q] = make_uint4(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
+    pb[q] = make_uint4(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_rows_to_cols(const uint8_t* __restrict__ rows, uint32_t n,
                                                         uint32_t* __restrict__ x, uint32_t* __restrict__ y) {
   const uint32_t stride = gridDim.x * blockDim.x;
@@ -1831,6 +1862,132 @@ int ensure_device_table(int device, int bits, const uint32_t** out) {
   return CUDASP_OK;
 }
 
+// The calling thread's current device switched for a scope.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// --- spend key folded into the top window (ScanConsts::fb_top) -------------
+// One table per (device, width, spend key), shared by every scanner with that
+// key (a query's feeds, a wallet's pooled scanners) and refcounted: 2 x 2^21
+// entries (268 MB) at 26 bits, 2 x 2^13 (1 MB) at 22.  A few unreferenced
+// tables stay cached per device for the next query; beyond that the oldest is
+// freed.  CUDASP_FB_FOLD=0 turns the fold off (A/B; the separate addition).
+struct FoldKey {
+  int device, bits;
+  uint32_t spend[16];
+  bool operator<(const FoldKey& o) const {
+    if (device != o.device) return device < o.device;
+    if (bits != o.bits) return bits < o.bits;
+    return memcmp(spend, o.spend, sizeof(spend)) < 0;
+  }
+};
+struct FoldTable {
+  uint32_t* table = nullptr;  // nullptr: exceptional (or failed) -- no fold for this key
+  int refs = 0;
+  uint64_t last_release = 0;
+};
+std::mutex g_fold_mu;
+std::map<FoldKey, FoldTable> g_folds;
+uint64_t g_fold_clock = 0;
+constexpr int FOLD_CACHED_PER_DEVICE = 4;
+
+bool fold_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CUDASP_FB_FOLD");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+size_t fold_table_bytes(int bits) {
+  const size_t top = bits == 26 ? FbWidth<26>::TOP_ENTRIES : FbWidth<22>::TOP_ENTRIES;
+  return 2 * top * FB_WORDS * 4;
+}
+
+// Caller holds g_fold_mu: free unreferenced tables of `device` beyond the cap,
+// oldest first.
+void fold_trim_locked(int device) {
+  for (;;) {
+    int unref = 0;
+    auto oldest = g_folds.end();
+    for (auto it = g_folds.begin(); it != g_folds.end(); ++it)
+      if (it->first.device == device && it->second.refs == 0) {
+        unref++;
+        if (oldest == g_folds.end() || it->second.last_release < oldest->second.last_release) oldest = it;
+      }
+    if (unref <= FOLD_CACHED_PER_DEVICE) return;
+    if (oldest->second.table) {
+      DeviceGuard g(device);
+      (void)hipFree(oldest->second.table);
+    }
+    g_folds.erase(oldest);
+  }
+}
+
+// A reference to the fold table of (device, bits, spend), built on first use
+// (synchronously, on a stream of its own).  *table = nullptr when the key
+// cannot be folded (exceptional sums) or the allocation failed.
+int fold_acquire(const FoldKey& key, const uint32_t* d_fb, const uint32_t** table) {
+  std::lock_guard<std::mutex> lk(g_fold_mu);
+  auto it = g_folds.find(key);
+  if (it != g_folds.end()) {
+    it->second.refs++;
+    *table = it->second.table;
+    return CUDASP_OK;
+  }
+  FoldTable ft;
+  DeviceGuard g(key.device);
+  uint32_t* d = nullptr;
+  uint32_t* d_bad = nullptr;
+  if (hipMalloc(&d, fold_table_bytes(key.bits)) != hipSuccess || hipMalloc(&d_bad, 4) != hipSuccess) {
+    (void)hipGetLastError();
+    if (d) (void)hipFree(d);
+    d = nullptr;
+  } else {
+    hipStream_t st = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HIP_TRY(hipMemsetAsync(d_bad, 0, 4, st));
+    SpendWords sw;
+    memcpy(sw.w, key.spend, sizeof(sw.w));
+    const uint32_t top = key.bits == 26 ? FbWidth<26>::TOP_ENTRIES : FbWidth<22>::TOP_ENTRIES;
+    auto kf = key.bits == 26 ? k_fb_fold<26> : k_fb_fold<22>;
+    hipLaunchKernelGGL(kf, dim3((top + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, d_fb, sw, d, d_bad);
+    HIP_TRY(hipGetLastError());
+    uint32_t bad = 1;
+    HIP_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipStreamDestroy(st));
+    if (bad) {
+      (void)hipFree(d);
+      d = nullptr;
+    }
+  }
+  if (d_bad) (void)hipFree(d_bad);
+  ft.table = d;
+  ft.refs = 1;
+  g_folds[key] = ft;
+  *table = d;
+  return CUDASP_OK;
+}
+
+void fold_release(const FoldKey& key) {
+  std::lock_guard<std::mutex> lk(g_fold_mu);
+  auto it = g_folds.find(key);
+  if (it == g_folds.end()) return;
+  if (--it->second.refs == 0) {
+    it->second.last_release = ++g_fold_clock;
+    fold_trim_locked(key.device);
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ scanner
@@ -1846,6 +2003,10 @@ struct cudasp_scanner {
   uint32_t label_cap = 0;  // label keys the label buffers are sized for
   uint32_t capacity = 0;
   cudasp_scan_options opt{1, 0, 0};
+  bool fold_allowed = true;        // cudasp_scanner_set_spend_fold (and CUDASP_FB_FOLD)
+  bool fold_held = false;          // holds a reference to g_folds[fold_key]
+  FoldKey fold_key{};
+  const uint32_t* fold_table = nullptr;  // its table (nullptr: not foldable)
   uint32_t t_cap_k = 1;            // output indices d_t / d_vflags are sized for
   std::vector<uint8_t> keys;       // scan key || spend key || label keys (set_options re-prepares)
   bool prepared = false;           // consts / d_naf / d_labels hold `keys` under prepared_opt (set_keys)
@@ -1959,17 +2120,6 @@ int rows_b_for(const cudasp_scanner* s, uint32_t n) {
   return (n + ROWS_B - 1) / ROWS_B >= s->fill_threads_b ? ROWS_B : 2;
 }
 
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
-
 // Stream arguments (include/cudasp_abi.h): NULL = the scanner's own stream
 // (the stateless entry points: the null stream), CUDASP_STREAM_DEFAULT = the
 // device's null stream -- torch's default stream, whose handle is 0 and so
@@ -1981,8 +2131,46 @@ hipStream_t scanner_stream(const cudasp_scanner* s, void* stream) {
   return stream == nullptr ? s->stream : plain_stream(stream);
 }
 
+// The scanner's fold of its spend key into the top window (ScanConsts::fb_top)
+// after its keys or fixed-base width changed: an on-curve key at an HBM width
+// takes (or shares) a fold table; anything else adds B on its own.  Caller:
+// no work of the scanner in flight.
+int scanner_update_fold(cudasp_scanner* s) {
+  FoldKey key{};
+  const bool want = s->fold_allowed && fold_enabled() && (s->fb_bits == 22 || s->fb_bits == 26) &&
+                    s->d_fb != nullptr && on_curve_words(s->consts.spend);
+  if (want) {
+    key.device = s->device;
+    key.bits = s->fb_bits;
+    memcpy(key.spend, s->consts.spend, sizeof(key.spend));
+    if (s->fold_held && !(key < s->fold_key) && !(s->fold_key < key)) {
+      s->consts.fb_top = s->fold_table;
+      return CUDASP_OK;
+    }
+  }
+  if (s->fold_held) {
+    fold_release(s->fold_key);
+    s->fold_held = false;
+    s->fold_table = nullptr;
+  }
+  s->consts.fb_top = nullptr;
+  if (!want) return CUDASP_OK;
+  const uint32_t* t = nullptr;
+  const int rc = fold_acquire(key, s->d_fb, &t);
+  if (rc != CUDASP_OK) return rc;
+  s->fold_held = true;
+  s->fold_key = key;
+  s->fold_table = t;
+  s->consts.fb_top = t;
+  return CUDASP_OK;
+}
+
 void free_scanner(cudasp_scanner* s) {
   if (!s) return;
+  if (s->fold_held) {
+    fold_release(s->fold_key);
+    s->fold_held = false;
+  }
   DeviceGuard g(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   void* ptrs[] = {s->d_naf,  s->d_labels, s->d_t,       s->d_vscratch, s->d_lscratch, s->d_rows,
@@ -2431,6 +2619,11 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
     free_scanner(s);
     return set_error(CUDASP_ERR_HIP, "hipMemcpy failed: %s", hipGetErrorString(e));
   }
+  rc = scanner_update_fold(s);
+  if (rc != CUDASP_OK) {
+    free_scanner(s);
+    return rc;
+  }
   s->prepared = true;  // prepare_scan above used the default options (s->opt)
   *out = s;
   return CUDASP_OK;
@@ -2488,6 +2681,10 @@ int cudasp_scanner_set_keys(cudasp_scanner* s, const uint8_t scan_private_key[32
   HIP_TRY(hipMemcpy(s->d_labels, labels.data(), labels.size() * 4, hipMemcpyHostToDevice));
   s->consts = consts;
   s->label_count = label_count;
+  {
+    const int rc = scanner_update_fold(s);
+    if (rc != CUDASP_OK) return rc;
+  }
   s->prepared = true;
   s->prepared_opt = s->opt;
   if (s->keys.data() != scan_private_key) {
@@ -2558,10 +2755,22 @@ int cudasp_scanner_set_fixed_base_bits(cudasp_scanner* s, int bits) {
   if (rc != CUDASP_OK) return rc;
   s->d_fb = fb;
   s->fb_bits = bits;
-  return CUDASP_OK;
+  return scanner_update_fold(s);
 }
 
 int cudasp_scanner_fixed_base_bits(const cudasp_scanner* s) { return s ? s->fb_bits : 0; }
+
+int cudasp_scanner_set_spend_fold(cudasp_scanner* s, int on) {
+  g_last_error.clear();
+  if (!s) return set_error(CUDASP_ERR_INVALID_ARG, "null scanner");
+  if (s->fold_allowed == (on != 0)) return CUDASP_OK;
+  DeviceGuard g(s->device);
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  s->fold_allowed = on != 0;
+  return scanner_update_fold(s);
+}
+
+int cudasp_scanner_spend_folded(const cudasp_scanner* s) { return s && s->consts.fb_top ? 1 : 0; }
 
 int cudasp_scanner_set_rows_per_thread(cudasp_scanner* s, int rows_a, int rows_b) {
   g_last_error.clear();

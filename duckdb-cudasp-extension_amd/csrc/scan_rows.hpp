@@ -36,6 +36,9 @@ struct FbWidth {
   static_assert(BITS >= 4 && BITS <= 27, "fixed-base window width");
   static constexpr int WINDOWS = (256 + BITS - 1) / BITS;
   static constexpr uint32_t ENTRIES = 1u << (BITS - 1);
+  // entries of the top window a scalar below 2^256 can reach: its digit is
+  // 2 b + 1 with b = t' >> (BITS (WINDOWS - 1) + 1) < 2^(255 - BITS (WINDOWS - 1))
+  static constexpr uint32_t TOP_ENTRIES = 1u << (255 - BITS * (WINDOWS - 1));
 };
 constexpr int FB_BITS = CUDASP_FB_BITS;
 static_assert(FB_BITS == 22 || FB_BITS == 26, "default fixed-base width must be a prebuilt one (22 or 26)");
@@ -53,6 +56,11 @@ struct ScanConsts {
   // is output_count 1, full_x 0):
   uint32_t output_count;  // K: output indices k = 0..K-1 hashed per row
   uint32_t full_x;        // outputs are 32-byte big-endian x-only keys
+  // The spend key folded into the fixed-base table's top window (nullptr:
+  // added on its own): TOP_ENTRIES entries (2j+1) 2^(w (W-1)) G + B, then as
+  // many with - B (fixed_base_mul, fb_fold_entry).  Set by the scanner for an
+  // on-curve B and an HBM width only; never by prepare_scan.
+  const uint32_t* fb_top;
 };
 
 // beta, a primitive cube root of unity mod p: (beta*x, y) = lambda*(x, y).
@@ -549,8 +557,13 @@ CUDASP_HD bool scalar_odd_rep(uint32_t t[8], const uint32_t in[8]) {
 // value (not reduced mod n, like the reference, src/cudasp_gpu.cu:862-877;
 // n*G = O makes that irrelevant).  W gathers and W - 1 mixed additions (W the
 // windows of the BITS-bit table), no constant term.
+// fb_top (optional): the top window with a point B folded in (ScanConsts::
+// fb_top): the result is then t G + B.  A lane whose odd representative
+// stands for -t (negated at the end) reads the - B half, so the final
+// negation gives -(t' G - B) = t G + B as well.
 template <int BITS = FB_BITS>
-CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb_table) {
+CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb_table,
+                              const uint32_t* fb_top = nullptr) {
   constexpr int WINDOWS = FbWidth<BITS>::WINDOWS;
   constexpr uint32_t ENTRIES = FbWidth<BITS>::ENTRIES;
   uint32_t t[9];
@@ -575,6 +588,8 @@ CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb
     ge P;
     if (i < WINDOWS - 1)
       fb_entry<BITS>(P, fb_table, i, bits);
+    else if (fb_top)  // positive digit, entry bits of the folded top window (+ B or - B)
+      fb_entry<BITS>(P, fb_top + (negate ? (size_t)FbWidth<BITS>::TOP_ENTRIES * FB_WORDS : 0), 0, bits | ENTRIES);
     else
       fb_entry<BITS>(P, fb_table, i, bits | ENTRIES);  // positive digit 2 bits + 1: entry bits
     if (i == 0) {
@@ -594,10 +609,16 @@ CUDASP_HD void fixed_base_mul(gej& R, const uint32_t t_in[8], const uint32_t* fb
 // Stage B, first half: F = t G + B as a Jacobian point.
 template <int BITS = FB_BITS>
 CUDASP_HD void row_match_point(gej& R, const uint32_t t_in[8], const uint32_t* fb_table, const ScanConsts& k) {
+  if (k.fb_top) {
+    // an on-curve B folded into the top window: F = t G + B with one mixed
+    // addition fewer (the group law makes it the same point as the chord
+    // addition below)
+    fixed_base_mul<BITS>(R, t_in, fb_table, k.fb_top);
+    return;
+  }
   fixed_base_mul<BITS>(R, t_in, fb_table);  // P0 = t*G
-  // B is added on its own (not folded into the table), so F = P0 + B is the same
-  // single chord addition as the reference's even for a spend key that is not
-  // on the curve.
+  // B added on its own: F = P0 + B is the same single chord addition as the
+  // reference's, also for a spend key that is not on the curve.
   ge B;
   ge_from_words(B, k.spend);
   gej_add_ge(R, R, B);  // F = P0 + B (Jacobian)
@@ -825,6 +846,62 @@ CUDASP_HD bool row_match(const uint32_t t_in[8], const uint32_t* fb_table, const
 }
 
 // Fixed-base table entry (2j+1) Q of a window with base Q = 2^(w window) G.
+// Affine P + Q (normalized words) given inv = 1 / (Q.x - P.x).
+CUDASP_HD void affine_add_inv(uint32_t out[16], const ge& P, const ge& Q, const fe& inv) {
+  fe num, lam, x3, y3, t;
+  fe_sub<1>(num, Q.y, P.y);
+  fe_mul(lam, num, inv);
+  fe_sqr(x3, lam);
+  fe_sub<1>(x3, x3, P.x);
+  fe_sub<1>(x3, x3, Q.x);
+  fe_normalize(x3);
+  fe_sub<1>(t, P.x, x3);
+  fe_mul(y3, lam, t);
+  fe_sub<1>(y3, y3, P.y);
+  fe_normalize(y3);
+  fe_to_u32x8(out, x3);
+  fe_to_u32x8(out + 8, y3);
+}
+
+// One entry P of the fixed-base table's top window with the spend key folded
+// in (ScanConsts::fb_top): out_pos = P + B, out_neg = P - B, both affine and
+// normalized, from one inversion (the two denominators are the same).
+// P, B normalized.  False when x(P) = x(B): a sum would be a doubling or the
+// point at infinity (probability ~2^-230 for a real key); the scanner then
+// adds B on its own.
+CUDASP_HD bool fb_fold_entry(uint32_t out_pos[16], uint32_t out_neg[16], const ge& P, const ge& B) {
+  fe den, dn, inv;
+  fe_sub<1>(den, B.x, P.x);
+  dn = den;
+  fe_normalize(dn);
+  if (fe_is_zero_norm(dn)) return false;
+  fe_inv(inv, dn);
+  affine_add_inv(out_pos, P, B, inv);
+  ge nB;
+  nB.x = B.x;
+  fe_negate<1>(nB.y, B.y);
+  fe_normalize(nB.y);
+  affine_add_inv(out_neg, P, nB, inv);
+  return true;
+}
+
+// y^2 = x^3 + 7 for normalized words (the fold needs the group law, so only
+// an on-curve spend key is folded).
+CUDASP_HD bool on_curve_words(const uint32_t w[16]) {
+  fe x, y, y2, x3;
+  fe_from_u32x8(x, w);
+  fe_from_u32x8(y, w + 8);
+  fe_sqr(y2, y);
+  fe_sqr(x3, x);
+  fe_mul(x3, x3, x);
+  fe seven;
+  fe_set_int(seven, 7);
+  fe_add(x3, x3, seven);
+  fe_normalize(y2);
+  fe_normalize(x3);
+  return fe_equal_norm(y2, x3);
+}
+
 CUDASP_HD void fb_build_entry(uint32_t out[16], const ge& Q, uint32_t j) {
   uint32_t m = 2 * j + 1;  // 1 .. 2^w - 1
   int top = 31 - __builtin_clz(m);

@@ -33,6 +33,8 @@ SIGNATURES = {
     "cudasp_fixed_base_table_bytes": (ctypes.c_uint64, [_I32]),
     "cudasp_scanner_set_fixed_base_bits": (_I32, [_P, _I32]),
     "cudasp_scanner_fixed_base_bits": (_I32, [_P]),
+    "cudasp_scanner_set_spend_fold": (_I32, [_P, _I32]),
+    "cudasp_scanner_spend_folded": (_I32, [_P]),
     "cudasp_scanner_set_rows_per_thread": (_I32, [_P, _I32, _I32]),
     "cudasp_scan_device": (_I32, [_P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "cudasp_scan_host": (_I32, [_P, _P, _P, ctypes.c_size_t, _P, _P, _U32, _P]),

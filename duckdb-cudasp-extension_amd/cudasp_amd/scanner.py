@@ -72,6 +72,17 @@ class Scanner:
         width; builds the device's table for that width on first use."""
         _native.check(self._lib.cudasp_scanner_set_fixed_base_bits(self._h, int(bits)))
 
+    def set_spend_fold(self, on=True):
+        """The spend key folded into the fixed-base table's top window
+        (cudasp_scanner_set_spend_fold; on by default for an on-curve key at an
+        HBM width).  Same results either way."""
+        _native.check(self._lib.cudasp_scanner_set_spend_fold(self._h, int(bool(on))))
+
+    @property
+    def spend_folded(self):
+        """Whether this scanner's launches use the folded top window."""
+        return bool(self._lib.cudasp_scanner_spend_folded(self._h))
+
     def set_rows_per_thread(self, rows_a=0, rows_b=0):
         """Launch shape of the next launches (cudasp_scanner_set_rows_per_thread):
         rows per thread of stage A (1, 2, 4) and stage B (2, 6); 0 = automatic."""

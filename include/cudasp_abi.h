@@ -97,6 +97,19 @@ uint64_t cudasp_fixed_base_table_bytes(int bits);
 int cudasp_scanner_set_fixed_base_bits(cudasp_scanner* s, int bits);
 int cudasp_scanner_fixed_base_bits(const cudasp_scanner* s);
 
+/* The spend key folded into the fixed-base table's top window: the table's
+ * reachable top-window entries P become P + B and P - B (a per-(device,
+ * width, key) table shared by the scanners holding that key: 268 MB at 26
+ * bits, 1 MB at 22), so stage B's F = t*G + B costs one mixed addition fewer.
+ * Used only for a spend key on the curve (the group law makes the result the
+ * reference's chord addition P0 + B; an off-curve key, which the reference's
+ * formulas also take, is added on its own) and an HBM width.  On by default;
+ * CUDASP_FB_FOLD=0 turns it off process-wide, set_spend_fold(s, 0) for one
+ * scanner (not concurrent with work in flight on it).  spend_folded returns 1
+ * when the scanner's launches use the fold.  Results never depend on it. */
+int cudasp_scanner_set_spend_fold(cudasp_scanner* s, int on);
+int cudasp_scanner_spend_folded(const cudasp_scanner* s);
+
 /* Launch shape of the scanner's next launches: rows per thread of stage A
  * (1, 2 or 4) and stage B (2 or 6); 0 = automatic (the default: 4 and 6, or
  * fewer for launches too small to fill the device).  Rows of a thread run in

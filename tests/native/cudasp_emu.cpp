@@ -231,6 +231,47 @@ int emu_pend_invert(const uint8_t* zs, int count, uint8_t* out) {
   return 0;
 }
 
+// The spend key folded into the top window (ScanConsts::fb_top): one entry's
+// P + B and P - B (fb_fold_entry; 1, or 0 when exceptional), y^2 = x^3 + 7.
+int emu_fb_fold_entry(const uint32_t P[16], const uint32_t B[16], uint32_t pos[16], uint32_t neg[16]) {
+  ge p, b;
+  ge_from_words(p, P);
+  ge_from_words(b, B);
+  return fb_fold_entry(pos, neg, p, b) ? 1 : 0;
+}
+
+int emu_on_curve(const uint32_t w[16]) { return on_curve_words(w) ? 1 : 0; }
+
+// t G + B through fixed_base_mul with B folded into the top window (only the
+// top entry t needs is folded; the rest of the fold table stays zero):
+// affine x, y as 8 LE words.  Returns 0, or 1 if the fold was exceptional.
+int emu_fixed_base_mul_folded(const uint32_t t[8], const uint32_t B[16], uint32_t out[16]) {
+  LazyTable& tab = lazy_table();
+  tab.ensure_for(t);
+  constexpr uint32_t TOP = FbWidth<FB_BITS>::TOP_ENTRIES;
+  std::vector<uint32_t> fold((size_t)2 * TOP * FB_WORDS, 0);
+  uint32_t to[8];
+  (void)scalar_odd_rep(to, t);
+  // j = t' >> (w (W - 1) + 1), the top window's entry index
+  const int sh = FB_BITS * (FB_WINDOWS - 1) + 1;
+  const uint32_t j = (to[sh / 32] >> (sh % 32)) | (sh % 32 && sh / 32 < 7 ? to[sh / 32 + 1] << (32 - sh % 32) : 0u);
+  ge P, b;
+  ge_from_words(P, tab.table + ((size_t)(FB_WINDOWS - 1) * FB_ENTRIES + (j & (TOP - 1))) * FB_WORDS);
+  ge_from_words(b, B);
+  if (!fb_fold_entry(&fold[(size_t)(j & (TOP - 1)) * FB_WORDS], &fold[((size_t)TOP + (j & (TOP - 1))) * FB_WORDS], P,
+                     b))
+    return 1;
+  gej R;
+  fixed_base_mul(R, t, tab.table, fold.data());
+  fe zi;
+  fe_inv(zi, R.z);
+  ge A;
+  gej_to_ge_zinv(A, R, zi);
+  fe_to_u32x8(out, A.x);
+  fe_to_u32x8(out + 8, A.y);
+  return 0;
+}
+
 int emu_fb_layout(int* bits, int* windows, uint32_t* entries) {
   *bits = FB_BITS;
   *windows = FB_WINDOWS;

@@ -111,3 +111,53 @@ def test_lds_width_small_scanner(torch, max_rows):
     assert sorted(np.nonzero(res[0])[0].tolist()) == planted.cpu().tolist()
     for r in res[1:]:
         assert (r == res[0]).all()
+
+
+def test_spend_fold_equals_separate_addition(torch):
+    """The spend key folded into the top window (cudasp_scanner_set_spend_fold,
+    on by default for an on-curve key at an HBM width): compare values and
+    flags through the stage kernels, the fused single-batch kernel and the
+    multi-batch kernel equal the oracle's with the fold and without it, at 22
+    and 26 bits; an off-curve spend key (the SQL test's "wrong keys" query
+    passes one) is never folded."""
+    from test_labels16_gpu import rows_of, synth_var
+    from cudasp_amd import Scanner
+    from oracle import oracle
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    labels = bench.label_keys(2)
+    n = 4099
+    x, y, outs, offs, lens = synth_var(torch, 987654, n)
+    rows = rows_of(x, y)
+    _, ov = oracle.scan(bench.SCAN_KEY, bench.SPEND_KEY, labels, rows, threads=16, want_values=True)
+    o = outs.cpu().numpy()
+    of = offs.cpu().numpy().view(np.uint32)
+    for i in range(0, n, 3):
+        o[of[i]] = ov[i, (i // 3) % 3]
+    od = torch.from_numpy(o).cuda()
+    want, _ = oracle.scan(bench.SCAN_KEY, bench.SPEND_KEY, labels, rows, o, of, lens.cpu().numpy().view(np.uint32),
+                          threads=16)
+    with Scanner(bench.SCAN_KEY, bench.SPEND_KEY, labels, max_rows=n) as s:
+        for bits in (22, 26):
+            s.set_fixed_base_bits(bits)
+            for fold in (True, False):
+                s.set_spend_fold(fold)
+                assert s.spend_folded == fold, (bits, fold)
+                t = torch.empty((8, n), dtype=torch.int32, device="cuda")
+                v = torch.empty((3, n), dtype=torch.int64, device="cuda")
+                s.row_values_device(x, y, t, v)
+                f1 = torch.zeros(n, dtype=torch.uint8, device="cuda")
+                s.scan_device(x, y, od, offs, lens, f1)
+                f2 = torch.zeros(n, dtype=torch.uint8, device="cuda")
+                s.scan_device_batches([dict(tweak_x=x, tweak_y=y, outputs=od, offsets=offs, lengths=lens, flags=f2)])
+                s.sync()
+                assert (v.cpu().numpy().T == ov).all(), (bits, fold)
+                assert (f1.cpu().numpy() == want).all(), (bits, fold)
+                assert (f2.cpu().numpy() == want).all(), (bits, fold)
+        s.set_spend_fold(True)
+        off_curve = bench.SPEND_KEY[:32] + bytes([bench.SPEND_KEY[32] ^ 1]) + bench.SPEND_KEY[33:]
+        s.set_keys(bench.SCAN_KEY, off_curve, labels)
+        assert not s.spend_folded
+        s.set_keys(bench.SCAN_KEY, bench.SPEND_KEY, labels)
+        assert s.spend_folded

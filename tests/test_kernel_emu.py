@@ -223,6 +223,42 @@ def test_fixed_base_mul_recoding(emu):
         assert (x, y) == _mul(t % N), hex(t)
 
 
+def _w16(pt):
+    return (ctypes.c_uint32 * 16)(*[(pt[0] >> (32 * i)) & 0xFFFFFFFF for i in range(8)],
+                                  *[(pt[1] >> (32 * i)) & 0xFFFFFFFF for i in range(8)])
+
+
+def _pt(out):
+    return (sum(out[i] << (32 * i) for i in range(8)), sum(out[8 + i] << (32 * i) for i in range(8)))
+
+
+def test_spend_key_folded_into_top_window(emu):
+    """The spend key folded into the fixed-base table's top window
+    (ScanConsts::fb_top, round 5): fb_fold_entry gives P + B and P - B; with
+    it fixed_base_mul returns t G + B directly -- for odd t and for even t
+    (whose lanes read the - B half and negate at the end), t >= n, and the
+    scalar extremes -- equal to the separate chord addition of the
+    reference; x(P) = x(B) is refused (the scanner then adds B on its own);
+    the on-curve check accepts B and rejects (x, y + 1)."""
+    rng = random.Random(352)
+    ts = [1, 2, 3, N - 1, N - 2, N + 1, (1 << 256) - 1, (1 << 256) - 2, 1 << 255]
+    ts += [rng.getrandbits(256) for _ in range(24)]
+    out = (ctypes.c_uint32 * 16)()
+    for i, t in enumerate(ts):
+        B = _mul(rng.randrange(1, N))
+        assert emu.emu_on_curve(_w16(B)) == 1
+        tw = (ctypes.c_uint32 * 8)(*[(t >> (32 * q)) & 0xFFFFFFFF for q in range(8)])
+        assert emu.emu_fixed_base_mul_folded(tw, _w16(B), out) == 0
+        assert _pt(out) == _add(_mul(t % N), B), hex(t)
+    B = _mul(12345)
+    assert emu.emu_on_curve(_w16((B[0], (B[1] + 1) % P))) == 0
+    P0 = _mul(777)
+    pos, neg = (ctypes.c_uint32 * 16)(), (ctypes.c_uint32 * 16)()
+    assert emu.emu_fb_fold_entry(_w16(P0), _w16(B), pos, neg) == 1
+    assert _pt(pos) == _add(P0, B) and _pt(neg) == _add(P0, (B[0], P - B[1]))
+    assert emu.emu_fb_fold_entry(_w16(P0), _w16(P0), pos, neg) == 0  # x(P) = x(B): doubling / infinity
+
+
 def _values(emu, scan, spend, labels, tweaks, outs=None, offs=None, lens=None):
     n = len(tweaks) // 64
     L = len(labels)
