@@ -36,7 +36,10 @@
 // harvest) -- the host's capacity to feed N GPUs; a query then passes when
 // it emits nothing.  --cpu-table (with --null-device) fills the table on the
 // CPU (pseudo-random tweak bytes, the same splitmix64 outputs, no plants), so
-// the host's ceiling can be measured with no GPU at all.
+// the host's ceiling can be measured with no GPU at all.  host_call_tx_per_s
+// in the output = rows / the threads' mean time inside the host's calls
+// (cudasp_tf_function*): the host's own rate, without this driver's chunk
+// building (DuckDB's side of the vectors).
 // Label keys: F holds L 64-byte keys (x || y, little-endian, bench.label_keys);
 // without F, L must be 0 or 1 (the SQL test's label, test/sql/cudasp.test:104).
 // Prints one JSON line; exit 0 iff every timed query emitted exactly the
@@ -602,7 +605,7 @@ int main(int argc, char** argv) {
          "\"thread_call_s_mean\": %.4f, \"thread_final_s_mean\": %.4f, "
          "\"thread_done_s_min\": %.4f, \"thread_done_s_max\": %.4f, \"streaming_feeds\": %u, \"logical_gpus\": %d, "
          "\"warm_reps\": %d, \"warm_ms\": %d, \"warm_seconds\": %.5f, \"warm_tx_per_s\": %.1f, "
-         "\"null_device\": %s, \"host_cpus_online\": %ld}\n",
+         "\"null_device\": %s, \"host_cpus_online\": %ld, \"host_call_tx_per_s\": %.1f}\n",
          a.columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)t.rows, a.threads, (long long)a.batch,
          a.labels,
          a.kmax ? ("\"1.." + std::to_string(a.kmax) + "\"").c_str() : std::to_string(a.k).c_str(),
@@ -613,6 +616,7 @@ int main(int argc, char** argv) {
          (unsigned long long)q.stats.launches, q.stats.launches ? (double)q.stats.rows / q.stats.launches : 0.0,
          q.stats.harvest_wait_s, q.stats.reserve_s, q.stats.copy_s, q.stats.launch_s, q.call_s_mean, q.final_s_mean, q.done_min, q.done_max,
          q.stats.streaming_feeds, q.logical_gpus, a.warm_reps, a.warm_ms, warm_med,
-         warm_med > 0 ? t.rows / warm_med : 0.0, a.null_device ? "true" : "false", sysconf(_SC_NPROCESSORS_ONLN));
+         warm_med > 0 ? t.rows / warm_med : 0.0, a.null_device ? "true" : "false", sysconf(_SC_NPROCESSORS_ONLN),
+         q.call_s_mean > 0 ? t.rows / q.call_s_mean : 0.0);
   return all_exact ? 0 : 2;
 }
