@@ -354,10 +354,13 @@ def run_step(tab, scanners, streams, events=None, tail_rows=(0, 0)):
 
 
 def multi_descs(tab):
-    """The rank's batches as cudasp_scan_device_batches descriptors."""
-    return [dict(tweak_x=tab.cols(tab.tx, b), tweak_y=tab.cols(tab.ty, b), outputs=tab.outs[b], offsets=tab.offs[b],
+    """The rank's batches as cudasp_scan_device_batches descriptors, built
+    once as the C array the call takes (Scanner.device_batches), so that a
+    step spends no host time converting them."""
+    from cudasp_amd import Scanner
+    return Scanner.device_batches([dict(tweak_x=tab.cols(tab.tx, b), tweak_y=tab.cols(tab.ty, b), outputs=tab.outs[b], offsets=tab.offs[b],
                  lengths=tab.lens[b], flags=tab.flags[b][:tab.sizes[b]], match_rows=tab.match_rows[b],
-                 match_count=tab.match_count[b:b + 1]) for b in range(tab.nb)]
+                 match_count=tab.match_count[b:b + 1]) for b in range(tab.nb)])
 
 
 def run_step_multi(tab, scanner, stream, descs, events=None):

@@ -453,14 +453,70 @@ __device__ __forceinline__ void multi_finish(const MultiBatch* __restrict__ bd, 
 
 // Measurement builds only (-DCUDASP_MULTI_TRACE=1, tools/multi_trace.py): per
 // wave of the last k_scan_multi launch, its start and end (s_memrealtime
-// ticks), pieces and wave-rows, read back by cudasp_debug_multi_trace.
+// ticks), pieces and wave-rows, its placement (HW_ID | XCC_ID << 32), when it
+// first found the counter exhausted, shader-clock ticks (s_memtime) over its
+// life and when its last stage-A row ended, read back by
+// cudasp_debug_multi_trace.
 #ifndef CUDASP_MULTI_TRACE
 #define CUDASP_MULTI_TRACE 0
 #endif
 #if CUDASP_MULTI_TRACE
 constexpr uint32_t MULTI_TRACE_WAVES = 8192;
-__device__ uint64_t g_multi_trace[MULTI_TRACE_WAVES * 4];
+constexpr uint32_t MULTI_TRACE_WORDS = 8;
+__device__ uint64_t g_multi_trace[MULTI_TRACE_WAVES * MULTI_TRACE_WORDS];
+__device__ __forceinline__ uint64_t trace_placement() {
+  uint32_t hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  return (uint64_t)hw | ((uint64_t)xcc << 32);
+}
 #endif
+
+// The wave's issue priority, 0 .. 3 (s_setprio takes an immediate).
+__device__ __forceinline__ void set_wave_prio(uint32_t level) {
+  switch (level) {
+    case 0:
+      __builtin_amdgcn_s_setprio(0);
+      break;
+    case 1:
+      __builtin_amdgcn_s_setprio(1);
+      break;
+    case 2:
+      __builtin_amdgcn_s_setprio(2);
+      break;
+    default:
+      __builtin_amdgcn_s_setprio(3);
+      break;
+  }
+}
+
+// The ladder hook of k_scan_multi (the drain): once the work counter has run
+// out, the SIMDs' waves issue youngest first.  Until then the oldest wave of a
+// SIMD issues first and the youngest gets ~4% of it, so the youngest's last
+// piece is the SIMD's last work and runs alone (1 wave on the SIMD) after the
+// others have left: tools/multi_trace.py finds the youngest wave ending last
+// on 77-100% of the SIMDs, its stage A ending ~0.6 ms after the counter ran
+// out at 4M rows.  Reversed, it finishes while the older waves fill its
+// stalls, and the older ones (whose last pieces are short: they claim most
+// often) finish after it.  The wave's tier comes from its block (the
+// dispatcher places a CU-count of blocks at a time: `young_from` = 2 x CUs on
+// the full grid, ~0 otherwise); the priority is set once, at the first ladder
+// tick or claim that finds the counter out.  Claims and piece sizes are
+// untouched.
+struct MultiTick {
+  const uint32_t* counter;
+  uint32_t total_wr;
+  bool* out;       // the counter has run out (sticky, wave-uniform)
+  uint32_t level;  // the priority to take then (0: none)
+  __device__ __forceinline__ void ladder(int, uint32_t) const {
+    if (level == 0 || *out) return;
+    const uint32_t c = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)c) < total_wr) return;
+    *out = true;
+    set_wave_prio(level);
+  }
+};
+
 
 template <int FBB, bool PIPE>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const MultiBatch* __restrict__ bd, uint32_t nb,
@@ -469,7 +525,8 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
                                                                    const uint32_t* __restrict__ labels,
                                                                    uint32_t* __restrict__ scr,
                                                                    uint32_t* __restrict__ counter, uint32_t g1,
-                                                                   uint32_t g2, uint32_t rmax, uint32_t adaptive) {
+                                                                   uint32_t g2, uint32_t rmax, uint32_t adaptive,
+                                                                   uint32_t young_from, uint32_t tier_blocks) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = make_scratch(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
@@ -485,8 +542,16 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
   int count_p = 0, count_q = 0;
   bool more = true;
   uint32_t mine = 0;  // wave-rows this wave has claimed (lane 0)
+  bool out = false;   // MultiTick: the counter has run out
+  // MultiTick's priority: youngest first (blocks from 2 x tier_blocks), then
+  // the middle tier (from tier_blocks); the oldest keep 0; tier_blocks = 0: off
+  const uint32_t drain_level = tier_blocks == 0u                  ? 0u
+                               : blockIdx.x >= 2u * tier_blocks   ? 3u
+                               : blockIdx.x >= tier_blocks        ? 2u
+                                                                  : 0u;
 #if CUDASP_MULTI_TRACE
-  const uint64_t trace_t0 = wall_clock64();
+  const uint64_t trace_t0 = wall_clock64(), trace_c0 = __builtin_amdgcn_s_memtime();
+  uint64_t trace_tx = 0, trace_ta = 0;
   uint32_t trace_pieces = 0, trace_rows = 0;
 #endif
   for (;;) {
@@ -497,16 +562,25 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
       if (lane == 0) {
         const uint32_t prev = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t rem = prev < total_wr ? total_wr - prev : 0u;
-        R = adaptive ? multi_piece_rows_adaptive(rem, prev, mine, g1, g2, rmax) : multi_piece_rows(rem, g1, g2, rmax);
-        base = atomicAdd(counter, R);
+        R = adaptive ? multi_piece_rows_adaptive(rem, prev, mine, g1, g2, rmax, blockIdx.x >= young_from)
+                     : multi_piece_rows(rem, g1, g2, rmax);
+        base = R ? atomicAdd(counter, R) : total_wr;  // R = 0: this wave leaves
         mine += R;
       }
       base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
       R = (uint32_t)__builtin_amdgcn_readfirstlane((int)R);
-      if (base >= total_wr)
+      if (base >= total_wr) {
         more = false;
-      else
+        if (drain_level && !out) {  // MultiTick's drain priority
+          out = true;
+          set_wave_prio(drain_level);
+        }
+      } else {
         count = (int)(R < total_wr - base ? R : total_wr - base);
+      }
+#if CUDASP_MULTI_TRACE
+      if (!more) trace_tx = wall_clock64();
+#endif
     }
     if (count == 0 && count_p == 0 && count_q == 0) break;
 #if CUDASP_MULTI_TRACE
@@ -526,9 +600,13 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
         y[q] = b.ty[(size_t)q * b.n + r];
       }
       gej P;
-      row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
+      row_shared_secret_point_t(P, x, y, naf, k.naf_len, sc,
+                                MultiTick{counter, total_wr, &out, drain_level});
       pend_store(sc, PB, count_p + j, P);
     }
+#if CUDASP_MULTI_TRACE
+    if (count) trace_ta = wall_clock64();
+#endif
     if constexpr (!PIPE) {
       pend_invert<MULTI_RMAX>(sc, PB, count);
     } else {
@@ -618,11 +696,17 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
   }
 #if CUDASP_MULTI_TRACE
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
+  const uint64_t trace_c1 = __builtin_amdgcn_s_memtime(), trace_t1 = wall_clock64();
   if (lane == 0 && wave < MULTI_TRACE_WAVES) {
-    g_multi_trace[wave * 4 + 0] = trace_t0;
-    g_multi_trace[wave * 4 + 1] = wall_clock64();
-    g_multi_trace[wave * 4 + 2] = trace_pieces;
-    g_multi_trace[wave * 4 + 3] = trace_rows;
+    uint64_t* rec = g_multi_trace + (size_t)wave * MULTI_TRACE_WORDS;
+    rec[0] = trace_t0;
+    rec[1] = trace_t1;
+    rec[2] = trace_pieces;
+    rec[3] = trace_rows;
+    rec[4] = trace_placement();
+    rec[5] = trace_tx;
+    rec[6] = trace_c1 - trace_c0;
+    rec[7] = trace_ta;
   }
 #endif
 }
@@ -1145,21 +1229,9 @@ struct StreamTick {
 #endif
     if (step == 0) return;
     const uint64_t t_old = uniform_u64(me->t_old);
-    switch (stream_prio(wall_clock64() - t_old, step)) {
-      case 0:
-        __builtin_amdgcn_s_setprio(0);
-        break;
-      case 1:
-        __builtin_amdgcn_s_setprio(1);
-        break;
-      case 2:
-        __builtin_amdgcn_s_setprio(2);
-        break;
-      default:
-        __builtin_amdgcn_s_setprio(3);
-        break;
-    }
+    set_wave_prio(stream_prio(wall_clock64() - t_old, step));
   }
+  __device__ __forceinline__ void ladder(int, uint32_t) const { (*this)(); }
 };
 
 // Row bits of a label pass's unit bits (unit u = row u / K, index u % K).
@@ -2059,6 +2131,12 @@ struct cudasp_scanner {
   // k_scan_multi pieces sized by each wave's share of the work done
   // (multi_piece_rows_adaptive); CUDASP_MULTI_ADAPT=0 selects the plain rule
   bool multi_adaptive = true;
+  // k_scan_multi's drain: youngest waves first once the counter has run out
+  // (MultiTick); CUDASP_MULTI_ENDGAME=0 turns it off (A/B)
+  bool multi_endgame = true;
+  // k_scan_multi: the SIMDs' youngest waves take no piece they would finish
+  // last (multi_piece_rows_adaptive); CUDASP_MULTI_YOUNG=0 turns it off (A/B)
+  bool multi_young = true;
 };
 
 namespace {
@@ -2465,11 +2543,17 @@ static int launch_multi(cudasp_scanner* s, const std::vector<MultiBatch>& md, ui
   HIP_TRY(hipMemsetAsync(s->d_counter, 0, sizeof(uint32_t), st));
   const uint64_t waves = blocks * (BLOCK / 64);
   const uint32_t g1 = (uint32_t)(waves * g1_x100 / 100), g2 = (uint32_t)(waves * g2_x100 / 100);
+  // the SIMDs' wave tiers by age on a grid of every wave slot (3 blocks per
+  // CU, dispatched a CU-count at a time): the youngest third's claim rule
+  // (multi_piece_rows_adaptive) and the drain priority (MultiTick)
+  const bool tiers = CUDASP_WAVES_A == 3 && blocks == (uint64_t)s->cus * 3;
+  const uint32_t young_from = tiers && s->multi_young ? (uint32_t)(2 * s->cus) : 0xFFFFFFFFu;
+  const uint32_t tier_blocks = tiers && s->multi_endgame ? (uint32_t)s->cus : 0u;
   auto kf = s->multi_pipe ? (s->fb_bits == 26 ? k_scan_multi<26, true> : k_scan_multi<22, true>)
                           : (s->fb_bits == 26 ? k_scan_multi<26, false> : k_scan_multi<22, false>);
   hipLaunchKernelGGL(kf, dim3((uint32_t)blocks), dim3(BLOCK), 0, st, s->d_multi, nb, (uint32_t)total_wr, s->d_naf,
                      s->consts, s->d_fb, s->d_labels, s->d_mscratch, s->d_counter, g1, g2, rmax,
-                     s->multi_adaptive ? 1u : 0u);
+                     s->multi_adaptive ? 1u : 0u, young_from, tier_blocks);
   HIP_TRY(hipGetLastError());
   return CUDASP_OK;
 }
@@ -2583,6 +2667,8 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
     if (const char* f = getenv("CUDASP_FUSED_SINGLE")) s->fused_single = atoi(f) != 0;
     if (const char* f = getenv("CUDASP_MULTI_PIPE")) s->multi_pipe = atoi(f) != 0;
     if (const char* f = getenv("CUDASP_MULTI_ADAPT")) s->multi_adaptive = atoi(f) != 0;
+    if (const char* f = getenv("CUDASP_MULTI_ENDGAME")) s->multi_endgame = atoi(f) != 0;
+    if (const char* f = getenv("CUDASP_MULTI_YOUNG")) s->multi_young = atoi(f) != 0;
     if (const char* f = getenv("CUDASP_ROWS_A_FORCE")) {
       const int r = atoi(f);
       if (r == 1 || r == 2 || r == ROWS_A) s->rows_a_force = r;
@@ -2844,18 +2930,25 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
     const long v = atol(e);
     if (v >= 2 && v <= MULTI_RMAX) rmax = (uint32_t)v;
   }
+  // CUDASP_MULTI_BLOCKS = a grid of that many blocks instead of every wave slot (tuning)
+  uint64_t blocks = 0;
+  if (const char* e = getenv("CUDASP_MULTI_BLOCKS")) {
+    const long v = atol(e);
+    if (v >= 1 && v <= MAX_BLOCKS) blocks = (uint64_t)v;
+  }
   return launch_multi(s, md, total_wr, st, rmax, multi_threshold_x100("CUDASP_MULTI_G1", 100),
-                      multi_threshold_x100("CUDASP_MULTI_G2", 0), 0);
+                      multi_threshold_x100("CUDASP_MULTI_G2", 0), blocks);
 }
 
 #if CUDASP_MULTI_TRACE
 // Measurement builds only (not in include/cudasp_abi.h): copies up to
-// max_waves records (start, end, pieces, wave-rows) of the last k_scan_multi
-// launch; returns the number of records and the realtime clock in *hz.
+// max_waves records (8 words: start, end, pieces, wave-rows, placement,
+// exhausted, shader ticks, last stage A) of the last k_scan_multi launch; returns the
+// number of records and the realtime clock in *hz.
 extern "C" int cudasp_debug_multi_trace(uint64_t* out, uint32_t max_waves, int* hz) {
   const uint32_t n = max_waves < MULTI_TRACE_WAVES ? max_waves : MULTI_TRACE_WAVES;
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_multi_trace), (size_t)n * 4 * sizeof(uint64_t)));
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_multi_trace), (size_t)n * MULTI_TRACE_WORDS * sizeof(uint64_t)));
   int dev = 0, rate_khz = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev));

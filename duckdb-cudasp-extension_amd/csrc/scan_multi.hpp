@@ -66,10 +66,23 @@ CUDASP_HD uint32_t multi_piece_rows(uint32_t rem, uint32_t g1, uint32_t g2, uint
 // first: on gfx950 the three waves of a SIMD progress at ~1 : 0.3 : 0.05).
 // A wave's first piece is one wave-row (its speed is not known yet); g1 = 0
 // (a fused single-batch launch) keeps rmax throughout.
+//
+// `young`: the wave is its SIMD's youngest (the persistent grid's last third
+// of blocks: the dispatcher places blocks 0 .. cus - 1 first on every CU,
+// then the next cus, then the last; tools/multi_trace.py finds the last third
+// the slowest on all 1024 SIMDs).  It issues last, at ~4% of its SIMD while the
+// older two work, so a wave-row it claims late is the last work of its SIMD
+// and runs alone there in the drain.  In a launch of fewer than 10 x g1
+// wave-rows (~2M rows on the full grid: while a young wave does one wave-row
+// at ~4% of its SIMD, the GPU does ~25 per SIMD) it takes no piece at all: 0
+// (= leave).  Leaving later as well, once its share of the rows left drops
+// under one wave-row, costs more than the straggler it saves (its issue share
+// lost for the second half of a 4M-row launch: -0.5%).
+// The older waves keep the rules above, so every row is still claimed.
 CUDASP_HD uint32_t multi_piece_rows_adaptive(uint32_t rem, uint32_t prev, uint32_t mine, uint32_t g1, uint32_t g2,
-                                             uint32_t rmax) {
+                                             uint32_t rmax, bool young = false) {
   if (g1 == 0) return rmax;
-  if (mine == 0 || prev == 0) return 1u;
+  if (mine == 0 || prev == 0) return young && rem < 10ull * g1 ? 0u : 1u;
   const uint64_t r = (uint64_t)rem * mine / prev;
   return r < 1u ? 1u : (r > rmax ? rmax : (uint32_t)r);
 }

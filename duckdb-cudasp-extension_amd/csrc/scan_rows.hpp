@@ -158,14 +158,14 @@ CUDASP_HD int8_t uniform_digit(const int8_t* p, int i) {
 
 // A ladder hook that does nothing (row_shared_secret_point_t).
 struct NoTick {
-  CUDASP_HD void operator()() const {}
+  CUDASP_HD void ladder(int, uint32_t) const {}
 };
 
 // Stage A, first half: S = d T as a Jacobian point of the original curve.
 // tx, ty: the tweak point, 8 LE u32 words each (normal form, the reference's
 // layout).  naf: 2 * NAF_MAX digits (GLV half 1, then half 2, signs folded in).
-// tick() runs every 16 ladder steps (the streaming kernel re-prioritises its
-// waves there).
+// tick.ladder(i, naf_len) runs every 16 ladder steps, i the digits still to
+// go (the persistent kernels re-prioritise their waves there).
 template <class Tick>
 CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uint32_t ty[8], const int8_t* naf,
                                          uint32_t naf_len, const Scratch& sc, const Tick& tick) {
@@ -250,7 +250,7 @@ CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uin
   // doubling, so the load's latency runs under the doubling's ~900
   // instructions (the digits are wave-uniform, so is the choice).
   for (int i = (int)naf_len - 1; i >= 0; --i) {
-    if ((i & 15) == 0) tick();
+    if ((i & 15) == 0) tick.ladder(i, naf_len);
     const int d0 = uniform_digit(naf, i), d1 = uniform_digit(naf, NAF_MAX + i);
     const int hf = d0 != 0 ? 0 : (d1 != 0 ? 1 : -1);
     ge Pn;
@@ -289,7 +289,7 @@ CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uin
   }
 #else
   for (int i = (int)naf_len - 1; i >= 0; --i) {
-    if ((i & 15) == 0) tick();
+    if ((i & 15) == 0) tick.ladder(i, naf_len);
 #if LADDER_YH
     if (!inf) {
       gej_double_neg_yh(R, R);

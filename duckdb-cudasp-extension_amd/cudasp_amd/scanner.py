@@ -14,6 +14,23 @@ import numpy as np
 from . import _native
 
 
+class DeviceBatches:
+    """A prepared cudasp_device_batch array (Scanner.device_batches): the
+    descriptors of include/cudasp_abi.h, plus references that keep the
+    tensors they point into alive."""
+
+    def __init__(self, batches):
+        batches = list(batches)
+        self.count = len(batches)
+        self.array = (_native.DeviceBatch * max(1, self.count))()
+        for i, b in enumerate(batches):
+            self.array[i] = _native.DeviceBatch(
+                _ptr(b["tweak_x"]), _ptr(b["tweak_y"]), _ptr(b.get("outputs")), _ptr(b["offsets"]),
+                _ptr(b["lengths"]), int(b["flags"].numel()), _ptr(b["flags"]), _ptr(b.get("match_rows")),
+                _ptr(b.get("match_count")))
+        self._refs = batches
+
+
 def _ptr(t):
     """Raw pointer of a torch tensor or numpy array (None -> NULL)."""
     if t is None:
@@ -146,15 +163,19 @@ class Scanner:
         (cudasp_scan_device_batches: one persistent kernel for both stages).
         batches: sequence of dicts with the keys of scan_device (tweak_x,
         tweak_y, outputs, offsets, lengths, flags, optional match_rows /
-        match_count); n is flags.numel()."""
-        arr = (_native.DeviceBatch * max(1, len(batches)))()
-        for i, b in enumerate(batches):
-            arr[i] = _native.DeviceBatch(
-                _ptr(b["tweak_x"]), _ptr(b["tweak_y"]), _ptr(b.get("outputs")), _ptr(b["offsets"]),
-                _ptr(b["lengths"]), int(b["flags"].numel()), _ptr(b["flags"]), _ptr(b.get("match_rows")),
-                _ptr(b.get("match_count")))
+        match_count); n is flags.numel().  Or the DeviceBatches of
+        device_batches(...), for a set scanned repeatedly: the C array is then
+        built once, not on every call."""
+        if not isinstance(batches, DeviceBatches):
+            batches = DeviceBatches(batches)
         st = self._stream(stream)
-        _native.check(self._lib.cudasp_scan_device_batches(self._h, arr, len(batches), st))
+        _native.check(self._lib.cudasp_scan_device_batches(self._h, batches.array, batches.count, st))
+
+    @staticmethod
+    def device_batches(batches):
+        """The cudasp_device_batch array of `batches` (as for
+        scan_device_batches), built once; it holds references to the tensors."""
+        return DeviceBatches(batches)
 
     def row_values_device(self, tweak_x, tweak_y, t_out, values, stream=None):
         n = int(tweak_x.numel() // 8)

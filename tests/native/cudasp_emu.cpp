@@ -426,9 +426,11 @@ int emu_row_values_grouped(const uint8_t scan[32], const uint8_t spend[64], cons
 // from a fresh wave-row).  cover[sum(sizes)] counts how often each batch row
 // was scanned by an active lane; stats[r - 1] (r = 1..16) = pieces of r rows,
 // stats[16] = pieces in total, stats[17] = pieces whose rows ran past the last
-// wave-row.
+// wave-row, stats[18] = waves that left without claiming (young_from: waves
+// v >= young_from are their SIMDs' youngest).
 int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, uint32_t g1, uint32_t g2,
-                       uint32_t rmax, uint32_t adaptive, uint64_t seed, uint32_t* cover, uint64_t* stats) {
+                       uint32_t rmax, uint32_t adaptive, uint32_t young_from, uint64_t seed, uint32_t* cover,
+                       uint64_t* stats) {
   if (waves == 0 || rmax < 1 || rmax > 16) return CUDASP_ERR_INVALID_ARG;
   std::vector<MultiBatch> md;
   std::vector<uint64_t> row0;  // index of each descriptor's row 0 in cover
@@ -445,7 +447,7 @@ int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, ui
     at += sizes[i];
   }
   for (uint64_t i = 0; i < at; i++) cover[i] = 0;
-  for (int i = 0; i < 18; i++) stats[i] = 0;
+  for (int i = 0; i < 19; i++) stats[i] = 0;
   if (md.empty()) return 0;
   const uint32_t nb = (uint32_t)md.size(), twr = (uint32_t)total_wr;
   uint32_t counter = 0;
@@ -462,11 +464,17 @@ int emu_multi_schedule(const uint32_t* sizes, uint32_t count, uint32_t waves, ui
     while (done[v]) v = (v + 1) % waves;
     if (sized[v] < 0) {  // lane 0 reads the counter and sizes its piece
       const uint32_t rem = counter < twr ? twr - counter : 0u;
-      sized[v] = (int32_t)(adaptive ? multi_piece_rows_adaptive(rem, counter, mine[v], g1, g2, rmax)
+      sized[v] = (int32_t)(adaptive ? multi_piece_rows_adaptive(rem, counter, mine[v], g1, g2, rmax, v >= young_from)
                                     : multi_piece_rows(rem, g1, g2, rmax));
       continue;
     }
     const uint32_t R = (uint32_t)sized[v];
+    if (R == 0) {  // a young wave leaves without claiming
+      done[v] = 1;
+      live--;
+      stats[18]++;
+      continue;
+    }
     const uint32_t base = counter;  // atomicAdd
     counter += R;
     mine[v] += R;

@@ -108,6 +108,29 @@ def test_record_batch_stream(gpu):
     assert _rows(cudasp_scan_arrow(iter(batches), *keys)) == sorted(cudasp_scan(rows, *keys))
 
 
+def test_parquet_file(gpu, tmp_path):
+    """The reference's README shape, cudasp_scan(read_parquet(...), ...)
+    (README.md:109 there): a Parquet file written and read back by pyarrow
+    (several row groups, fixed_size_binary tweaks, NULLs), streamed as the
+    reader's record batches and read whole, equals the row path."""
+    pq = pytest.importorskip("pyarrow.parquet")
+    from cudasp_amd import cudasp_scan, cudasp_scan_arrow
+    rr = golden_io.load("random_rows.json")
+    rows = [(i.to_bytes(32, "big"), 900000 + i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
+    rows = rows * 8
+    rows[5] = (rows[5][0], rows[5][1], rows[5][2], None)
+    rows[9] = (None,) + rows[9][1:]
+    keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
+    want = sorted(cudasp_scan(rows, *keys))
+    assert want
+    path = str(tmp_path / "tweaks.parquet")
+    pq.write_table(_arrow(rows, pa.binary(64)), path, row_group_size=300)
+    f = pq.ParquetFile(path)
+    assert f.metadata.num_row_groups > 1
+    assert _rows(cudasp_scan_arrow(f.iter_batches(batch_size=250), *keys, batch_size=700, threads=2)) == want
+    assert _rows(cudasp_scan_arrow(pq.read_table(path), *keys)) == want
+
+
 def test_bad_tweak_length(gpu):
     from cudasp_amd import CudaspError, cudasp_scan_arrow
     rr = golden_io.load("random_rows.json")

@@ -19,16 +19,21 @@ def emu():
     subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])
     lib = ctypes.CDLL(os.path.join(HERE, "native", "libcudasp_emu29.so"))
     V, U = ctypes.c_void_p, ctypes.c_uint32
-    lib.emu_multi_schedule.argtypes = [V, U, U, U, U, U, U, ctypes.c_uint64, V, V]
+    lib.emu_multi_schedule.argtypes = [V, U, U, U, U, U, U, U, ctypes.c_uint64, V, V]
     return lib
 
 
-def schedule(emu, sizes, waves, g1, g2, rmax=RMAX, seed=1, adaptive=0):
-    """cover per row; stats: pieces by size (index r - 1), total, past the end."""
+NO_YOUNG = 0xFFFFFFFF
+
+
+def schedule(emu, sizes, waves, g1, g2, rmax=RMAX, seed=1, adaptive=0, young_from=NO_YOUNG):
+    """cover per row; stats: pieces by size (index r - 1), total, past the end,
+    waves that left without claiming (waves >= young_from are the SIMDs'
+    youngest)."""
     sizes = np.asarray(sizes, dtype=np.uint32)
     cover = np.zeros(max(1, int(sizes.sum())), dtype=np.uint32)
-    stats = np.zeros(18, dtype=np.uint64)
-    rc = emu.emu_multi_schedule(sizes.ctypes.data, len(sizes), waves, g1, g2, rmax, adaptive, seed,
+    stats = np.zeros(19, dtype=np.uint64)
+    rc = emu.emu_multi_schedule(sizes.ctypes.data, len(sizes), waves, g1, g2, rmax, adaptive, young_from, seed,
                                 cover.ctypes.data, stats.ctypes.data)
     assert rc == 0
     return cover[: int(sizes.sum())], stats
@@ -87,7 +92,7 @@ def test_piece_rows_rule(emu):
     waves, g1 = 1, 10
     sizes = [64 * 100]
     _, stats = schedule(emu, sizes, waves, g1, 0)
-    rem, want = 100, np.zeros(18, dtype=np.uint64)
+    rem, want = 100, np.zeros(19, dtype=np.uint64)
     while rem > 0:
         r = min(RMAX, max(1, rem // g1))
         want[r - 1] += 1
@@ -116,7 +121,7 @@ def test_adaptive_rule(emu):
     first piece is one wave-row; then the wave's share of the claimed work is
     all of it, so pieces are min(rmax, rem) rows: 100 = 1 + 16 x 6 + 3."""
     _, stats = schedule(emu, [64 * 100], 1, 1, 0, adaptive=1)
-    want = np.zeros(18, dtype=np.uint64)
+    want = np.zeros(19, dtype=np.uint64)
     want[0] = 1
     want[RMAX - 1] = 16
     want[2] = 1
@@ -132,3 +137,22 @@ def test_adaptive_long_step(emu):
     cover, stats = schedule(emu, sizes, waves, waves, 0, adaptive=1)
     assert np.all(cover == 1)
     assert RMAX * int(stats[RMAX - 1]) >= 0.8 * wave_rows(sizes)
+
+
+@pytest.mark.parametrize("rows,young_idle", [(1_000_000, True), (4_087_500, False), (300_000 * 20, False)])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_young_waves(emu, rows, young_idle, seed):
+    """The persistent grid's youngest third (waves >= 2048 of 3072) claims
+    nothing in a launch under 10 x 3072 wave-rows (1M rows), and works as the
+    others do in a larger one.  Every row is still claimed exactly once."""
+    waves = 3072
+    sizes = [300000] * (rows // 300000) + ([rows % 300000] if rows % 300000 else [])
+    cover, stats = schedule(emu, sizes, waves, waves, 0, seed=seed, adaptive=1, young_from=2048)
+    assert np.all(cover == 1)
+    assert stats[16] == stats[:16].sum()
+    if young_idle:
+        assert stats[18] == waves - 2048  # every young wave left at once
+    else:
+        # young waves work; only one whose first read comes late (under 10 x g1
+        # wave-rows left by then, in this random interleaving) leaves at once
+        assert stats[18] < (waves - 2048) // 10

@@ -53,3 +53,26 @@ def test_no_device_fails_loudly():
 def test_version_string():
     from cudasp_amd import _native
     assert b"gfx950" in _native.load().cudasp_version()
+
+
+def test_prepared_device_batches_match_the_abi_struct():
+    """Scanner.device_batches builds the cudasp_device_batch array once (the
+    bench's step reuses it): field order and values as scan_device_batches
+    would pass them, references to the tensors held."""
+    import torch
+    from cudasp_amd import Scanner, _native
+    n = 100
+    t = {k: torch.zeros(s, dtype=d) for k, s, d in (("tweak_x", 8 * n, torch.int32), ("tweak_y", 8 * n, torch.int32),
+                                                   ("outputs", 2 * n, torch.int64), ("offsets", n, torch.int32),
+                                                   ("lengths", n, torch.int32), ("flags", n, torch.uint8),
+                                                   ("match_rows", n, torch.int32), ("match_count", 1, torch.int32))}
+    prep = Scanner.device_batches([t, dict(t, flags=t["flags"][:7])])
+    assert prep.count == 2 and isinstance(prep.array[0], _native.DeviceBatch)
+    names = [f[0] for f in _native.DeviceBatch._fields_]
+    b0 = prep.array[0]
+    want = dict(zip(names, (t["tweak_x"].data_ptr(), t["tweak_y"].data_ptr(), t["outputs"].data_ptr(),
+                            t["offsets"].data_ptr(), t["lengths"].data_ptr(), n, t["flags"].data_ptr(),
+                            t["match_rows"].data_ptr(), t["match_count"].data_ptr())))
+    assert {k: getattr(b0, k) for k in names} == want
+    assert getattr(prep.array[1], names[5]) == 7
+    assert len(Scanner.device_batches([]).array) == 1 and Scanner.device_batches([]).count == 0
