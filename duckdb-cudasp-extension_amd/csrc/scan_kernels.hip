@@ -1020,6 +1020,16 @@ __device__ __forceinline__ void stream_copy_range(int64_t* mirror, const int64_t
 __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, uint64_t base, int count,
                                                 uint32_t lane, StreamWr* wr, StreamPf* pf, const Scratch& sc,
                                                 int stg, int meta, uint32_t ow, bool coal, uint4* tr) {
+  // A system-scope acquire (buffer_inv sc0 sc1) before the piece's reads of
+  // host memory: the pinned slots' lines can stay in the GPU's caches, and a
+  // slot the host has rewritten for a newer batch was otherwise read stale --
+  // rows scanned with another batch's tweaks, matches lost (a streaming feed
+  // with 4 slots lost 8-25% of its planted matches; tools/soak_host.py,
+  // test_host_stream_slot_reuse_reads_fresh_rows).  The descriptor that
+  // published the batch was read before this (pub_wr, then the mirrored ring).
+#ifndef CUDASP_AB_PF_NO_ACQUIRE
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
 #pragma unroll 1
   for (int j = 0; j < count; j++) {
     if (j > 0 && wr[j - 1].r0 / 64u + 1u < wr[j - 1].nwr) {

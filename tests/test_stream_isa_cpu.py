@@ -141,6 +141,23 @@ def test_done_word_follows_system_release(disasm, prefix):
     check_done(kernel(disasm, prefix), layout())
 
 
+def check_prefetch_acquire(code):
+    """The piece prefetch's system-scope acquire: one `buffer_inv sc0 sc1` in
+    the kernel, with the piece's 16-byte loads of the row blobs after it."""
+    inv = [i for i, ins in enumerate(code) if ins == "buffer_inv sc0 sc1"]
+    assert len(inv) == 1, inv
+    assert any(re.match(r"(global|flat)_load_dwordx4", ins) for ins in code[inv[0]:inv[0] + 800]), "no blob loads after it"
+
+
+@pytest.mark.parametrize("prefix", KERNELS)
+def test_piece_prefetch_acquires_host_memory(disasm, prefix):
+    """Before a piece's reads of the pinned slots, a system-scope acquire: a
+    slot rewritten by the host for a newer batch must not be read from lines
+    the GPU still caches (the stale reads lost matches with 4 slots;
+    test_host_stream_slot_reuse_reads_fresh_rows)."""
+    check_prefetch_acquire(kernel(disasm, prefix))
+
+
 def test_checks_reject_reordered_code(disasm):
     """Controls: the same code with one wait, fence or cache-policy bit
     removed fails the checks."""
@@ -159,6 +176,9 @@ def test_checks_reject_reordered_code(disasm):
     no_fence = [c for c in code if not c.startswith("buffer_wbl2")]
     with pytest.raises(AssertionError):
         check_done(no_fence, L)
+    no_acquire = [c for c in code if c != "buffer_inv sc0 sc1"]
+    with pytest.raises(AssertionError):
+        check_prefetch_acquire(no_acquire)
 
 
 def test_device_code_is_gfx950_only():
