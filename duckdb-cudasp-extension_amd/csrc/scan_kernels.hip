@@ -990,6 +990,17 @@ struct StreamPf {
 
 // Outputs words [q0, q1) of one batch into its device mirror, the whole wave
 // copying (lane-strided, 4 loads in flight per lane).
+// A store into a batch's device mirror of its outputs: written through to
+// memory (agent scope: global_store sc1, the line not kept in this XCD's L2).
+// A mirror is rewritten whenever its slot carries a newer batch, by waves on
+// any XCD; a plain store leaves the line dirty in its XCD's L2, and a
+// write-back of such a line after the slot's next batch had rewritten it
+// undid that batch's outputs (matches lost with 4 slots even behind the
+// per-iteration acquire; profiles/r05_stream_acquire.txt).
+__device__ __forceinline__ void mirror_store(int64_t* p, int64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void stream_copy_range(int64_t* mirror, const int64_t* outputs, uint32_t q0, uint32_t q1,
                                                   uint32_t lane) {
 #pragma unroll 1
@@ -1000,7 +1011,7 @@ __device__ __forceinline__ void stream_copy_range(int64_t* mirror, const int64_t
       if (q + 64u * i < q1) v[i] = outputs[q + 64u * i];
 #pragma unroll
     for (int i = 0; i < 4; i++)
-      if (q + 64u * i < q1) mirror[q + 64u * i] = v[i];
+      if (q + 64u * i < q1) mirror_store(mirror + q + 64u * i, v[i]);
   }
 }
 
@@ -1020,16 +1031,6 @@ __device__ __forceinline__ void stream_copy_range(int64_t* mirror, const int64_t
 __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, uint64_t base, int count,
                                                 uint32_t lane, StreamWr* wr, StreamPf* pf, const Scratch& sc,
                                                 int stg, int meta, uint32_t ow, bool coal, uint4* tr) {
-  // A system-scope acquire (buffer_inv sc0 sc1) before the piece's reads of
-  // host memory: the pinned slots' lines can stay in the GPU's caches, and a
-  // slot the host has rewritten for a newer batch was otherwise read stale --
-  // rows scanned with another batch's tweaks, matches lost (a streaming feed
-  // with 4 slots lost 8-25% of its planted matches; tools/soak_host.py,
-  // test_host_stream_slot_reuse_reads_fresh_rows).  The descriptor that
-  // published the batch was read before this (pub_wr, then the mirrored ring).
-#ifndef CUDASP_AB_PF_NO_ACQUIRE
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-#endif
 #pragma unroll 1
   for (int j = 0; j < count; j++) {
     if (j > 0 && wr[j - 1].r0 / 64u + 1u < wr[j - 1].nwr) {
@@ -1146,7 +1147,7 @@ __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, 
           for (int t = 0; t < 3; t++)
             if (t >= i0 && t < i) {
 #pragma unroll 1
-              for (uint32_t q = of[t] * ow; q < (of[t] + ln[t]) * ow; q++) mir[q] = out[q];
+              for (uint32_t q = of[t] * ow; q < (of[t] + ln[t]) * ow; q++) mirror_store(mir + q, out[q]);
             }
         }
         lo = ~0u;
@@ -1389,6 +1390,18 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
       me.t_old = count_q ? me.t_q : (count_p ? me.t_p : t_it);
     }
     tick();
+    // A system-scope acquire (buffer_inv sc0 sc1: this CU's L1 and this XCD's
+    // L2) before the iteration's reads of the new piece's pinned slots and of
+    // the pending pieces' output mirrors.  A slot the host rewrote for a newer
+    // batch, or a mirror rewritten for one (slot reuse), was otherwise read
+    // from stale cached lines: rows scanned with another batch's tweaks or
+    // compared against its outputs, matches lost (a streaming feed of 4 slots
+    // lost 8-25% of its planted matches; tools/soak_host.py,
+    // profiles/r05_stream_acquire.txt).  The batch's publication was observed
+    // before this (pub_wr, then the mirrored ring).
+#ifndef CUDASP_AB_PF_NO_ACQUIRE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
     StreamWr* const wn = wrs[wid][pn];
     const int meta_n = META + 2 * MULTI_RMAX * pn;
     if (count) stream_prefetch(dev, hint, base, count, lane, wn, pfs[wid], sc, STG, meta_n, ow, pf_coal != 0, pftr[wid]);

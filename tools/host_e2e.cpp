@@ -373,6 +373,7 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
   for (int i = 0; i < T; i++) CK(cudasp_tf_local_init(gs, &ls[i]));
   std::atomic<uint64_t> next{0};
   std::vector<uint64_t> got;  // emitted row indices (from the txids)
+  size_t torn = 0;            // emitted rows whose tweak or height is not their txid's row
   std::vector<double> t_calls(T, 0.0), t_final(T, 0.0), t_done(T, 0.0);
   if (warm_ms) busy_all_gpus(warm_ms);
   const auto t0 = std::chrono::steady_clock::now();
@@ -387,6 +388,10 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
         uint64_t g = 0;
         for (int b = 0; b < 8; b++) g |= (uint64_t)out->txid_data[i][31 - b] << (8 * b);
         got.push_back(g);  // only the output thread gets here
+        // the emitted row's other columns belong to the row its txid names
+        if (g >= rows || out->txid_size[i] != 32 || out->tweak_size[i] != 64 || out->height[i] != t.heights[g] ||
+            memcmp(out->tweak_data[i], t.tweaks.data() + g * 64, 64) != 0)
+          torn++;
       }
       if (rc != CUDASP_TF_HAVE_MORE_OUTPUT) break;
     }
@@ -466,6 +471,18 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
   q.emitted = got.size();
   std::sort(got.begin(), got.end());
   q.exact = a.null_device ? got.empty() : got == t.planted;
+  if (!q.exact || torn) {  // which rows differ (stderr; the JSON keeps the verdict)
+    std::vector<uint64_t> extra, missing;
+    std::set_difference(got.begin(), got.end(), t.planted.begin(), t.planted.end(), std::back_inserter(extra));
+    std::set_difference(t.planted.begin(), t.planted.end(), got.begin(), got.end(), std::back_inserter(missing));
+    fprintf(stderr, "query not exact: %zu emitted, %zu planted, %zu extra, %zu missing, %zu torn rows (txid and "
+            "tweak/height of different rows)\n", got.size(), t.planted.size(), extra.size(), missing.size(),
+            (size_t)torn);
+    for (size_t k = 0; k < extra.size() && k < 8; k++) fprintf(stderr, "  extra g=%llu\n", (unsigned long long)extra[k]);
+    for (size_t k = 0; k < missing.size() && k < 8; k++)
+      fprintf(stderr, "  missing g=%llu\n", (unsigned long long)missing[k]);
+  }
+  q.exact = q.exact && torn == 0;
   q.got.swap(got);
   auto mean = [](const std::vector<double>& v) {
     double s = 0;

@@ -37,7 +37,7 @@ def shape(rng):
         labels=labels,
         outputs=rng.choice([["--outputs", "1"], ["--outputs", "2"], ["--outputs", "8"], ["--outputs-max", "15"]]),
         device_map=rng.choice(["0", "0", "0,0,0", ",".join(["0"] * 8)]),
-        mode=rng.choice(["", "", "launch"]),
+        mode=rng.choice(["", "stream", "launch"]),  # "": streaming for one feed per device, else per-slot
         slots=rng.choice(["", "", "4", "48"]),
         nt=rng.choice(["", "0"]),
         fold=rng.choice(["", "0"]),
@@ -65,6 +65,8 @@ def main():
         if sh["batch"] < 2048 and sh["rows"] > 65536:
             sh["rows"] = 65536
         env = dict(os.environ, CUDASP_TF_DEVICE_MAP=sh["device_map"])
+        if sh["mode"] == "stream" and "," in sh["device_map"]:
+            env["GPU_MAX_HW_QUEUES"] = "16"  # a hardware queue per feed's persistent kernel (as the 8-feed test)
         for k, v in (("CUDASP_TF_MODE", sh["mode"]), ("CUDASP_TF_STREAM_SLOTS", sh["slots"]),
                      ("CUDASP_TF_NT", sh["nt"]), ("CUDASP_FB_FOLD", sh["fold"])):
             env.pop(k, None)
