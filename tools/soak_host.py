@@ -6,7 +6,8 @@ table size, executor threads, batch_size (down to a few rows: many slots and
 ring wraps), row chunks or Arrow columns, 0 / 1 / 2 / 16 label keys, fixed or
 ragged output lists, 1 / 3 / 8 logical GPUs on the one card, streaming feeds or
 per-slot launches, the streaming slot count, plain or non-temporal slot copies,
-the spend-key fold on or off.  Every query must emit exactly the planted rows
+the spend-key fold on or off, streaming kernels that leave after 1-3 ms idle
+(relaunched by the next publish).  Every query must emit exactly the planted rows
 (host_e2e's own check), and each run's 512-row sample is recomputed by the C
 oracle (oracle.check_planted_sample, checker use of oracle/).  Prints one line
 per run and a JSON summary; exit 1 on the first failure.
@@ -42,6 +43,7 @@ def shape(rng):
         nt=rng.choice(["", "0"]),
         fold=rng.choice(["", "0"]),
         reps=rng.choice([1, 2]),
+        idle_ms=rng.choice(["", "", "1", "3"]),  # streaming kernels leave when idle this long: many relaunches
     )
 
 
@@ -68,7 +70,8 @@ def main():
         if sh["mode"] == "stream" and "," in sh["device_map"]:
             env["GPU_MAX_HW_QUEUES"] = "16"  # a hardware queue per feed's persistent kernel (as the 8-feed test)
         for k, v in (("CUDASP_TF_MODE", sh["mode"]), ("CUDASP_TF_STREAM_SLOTS", sh["slots"]),
-                     ("CUDASP_TF_NT", sh["nt"]), ("CUDASP_FB_FOLD", sh["fold"])):
+                     ("CUDASP_TF_NT", sh["nt"]), ("CUDASP_FB_FOLD", sh["fold"]),
+                     ("CUDASP_STREAM_IDLE_MS", sh["idle_ms"])):
             env.pop(k, None)
             if v:
                 env[k] = v
