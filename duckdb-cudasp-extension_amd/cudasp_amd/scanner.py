@@ -387,6 +387,23 @@ class StreamBatch:
                                   self.mirror, self.match_rows)
         return self.seq
 
+    def refill(self, tweak_keys, outputs, offsets, lengths):
+        """Another batch into the same pinned buffers and device mirror (a
+        host's slot reused once its previous batch is done): at most the rows
+        and output bytes the buffers were made for (int64 outputs)."""
+        tk = np.ascontiguousarray(tweak_keys, dtype=np.uint8).reshape(-1)
+        outs = np.ascontiguousarray(outputs, dtype=np.int64).view(np.uint8).reshape(-1)
+        n = tk.size // 64
+        if n == 0 or tk.size > self.rows.nbytes or outs.nbytes > self.outputs.nbytes or 4 * n > self.offsets.nbytes:
+            raise ValueError("refill: %d rows / %d output bytes exceed the batch's buffers" % (n, outs.nbytes))
+        self.rows.array[:tk.size] = tk
+        self.outputs.array[:outs.nbytes] = outs
+        self.offsets.view(np.uint32)[:n] = np.asarray(offsets, dtype=np.uint32)
+        self.lengths.view(np.uint32)[:n] = np.asarray(lengths, dtype=np.uint32)
+        self.n = n
+        self.output_words = outs.nbytes // 8
+        self.reset()
+
     def reset(self):
         if self.flags is not None:
             self.flags.array[:] = 0xEE
@@ -394,7 +411,7 @@ class StreamBatch:
             self.match_rows.array[:] = 0xEE
 
     def result(self):
-        return self.flags.array.copy()
+        return self.flags.array[:self.n].copy()
 
     def matches(self, stream):
         """The matching rows (sorted) of this batch once it is done."""

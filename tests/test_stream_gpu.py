@@ -121,6 +121,45 @@ def test_stream_ring_wraps(torch):
     flags_equal(got, want)
 
 
+def test_stream_reused_buffers(torch):
+    """Four StreamBatch buffers carry 48 different batches in one query, each
+    refilled (rows, outputs, offsets, lengths and the same device mirror)
+    as soon as its previous batch is done -- a host's slot ring.  The kernel
+    reads every refill fresh: flags equal the per-batch path's for every
+    batch.  (Paced by Python, this does not reproduce the stale reads of
+    profiles/r05_stream_acquire.txt -- it passes on the build without the
+    acquire too; test_host_stream_slot_reuse_reads_fresh_rows does.)"""
+    from cudasp_amd import Scanner, ScanStream
+    rng = np.random.default_rng(48)
+    sizes = [int(x) for x in rng.integers(500, 2049, 48)]
+    labels = [LABEL]
+    batches = [tm.make_batch(torch, 5 + 2048 * i, n, kmax=8) for i, n in enumerate(sizes)]
+    tm.plant(torch, batches, labels, every=3)
+    want = tm.run_per_batch(torch, batches, labels)
+    assert sum(c for _, _, c in want) > 0
+    ring = [staged(tm.make_batch(torch, 10**9 + i, 2048, kmax=15), len(labels)) for i in range(4)]
+    got = [None] * len(batches)
+    with Scanner(SCAN, SPEND, labels, max_rows=1000) as s, ScanStream(s) as st:
+        held = [None] * len(ring)  # batch index each buffer carries
+        for i, b in enumerate(batches):
+            k = i % len(ring)
+            sb = ring[k]
+            if held[k] is not None:
+                st.wait(sb.seq)
+                got[held[k]] = sb.result()
+            n = b["n"]
+            sb.refill(host_rows(b), b["outputs"].cpu().numpy(), b["offsets"][:n].cpu().numpy().view(np.uint32),
+                      b["lengths"][:n].cpu().numpy().view(np.uint32))
+            sb.publish(st)
+            held[k] = i
+        st.close_input()
+        for k, sb in enumerate(ring):
+            st.wait(sb.seq)
+            got[held[k]] = sb.result()
+        st.finish()
+    flags_equal(got, want)
+
+
 def test_stream_concurrent_publishers_16_labels(torch):
     """Three publisher threads into one stream, 2500-row batches, 16 labels,
     1..15 outputs per row (the host's feed shape whose DMA-staged variant
