@@ -214,8 +214,11 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
  *   cudasp_host_alloc   coherent pinned host memory, device-addressable at
  *                       the same address: every host buffer of a published
  *                       batch must lie in such an allocation (checked at
- *                       publish: the kernel's uncached reads and
- *                       system-scope result stores need coherent memory).
+ *                       publish: the kernel's system-scope result stores
+ *                       need coherent memory).  The GPU may still cache
+ *                       lines of it: the kernel acquires at system scope
+ *                       before each piece's reads, so a buffer rewritten for
+ *                       a later batch is read fresh.
  *   cudasp_stream_supported  1 when the scanner's current keys and options
  *                       allow a stream (an HBM fixed-base width, a label
  *                       count whose scratch fits), else 0.
@@ -225,7 +228,9 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
  *                       outputs (>= 1 word; the kernel copies each row's
  *                       outputs there once); match_flags (n bytes) and/or
  *                       match_rows (room for n indices).  The buffers must
- *                       stay untouched until the batch is done.  *seq
+ *                       stay untouched until the batch is done; then any of
+ *                       them, d_mirror included, may carry a later batch
+ *                       (the kernel writes mirrors through).  *seq
  *                       receives the batch's sequence number.  At most 64
  *                       batches may be published and not yet done
  *                       (CUDASP_ERR_CAPACITY otherwise).  Launches the kernel
