@@ -22,7 +22,7 @@
 //   host_e2e [--rows N] [--threads T] [--batch B] [--labels L --labels-file F]
 //            [--outputs K | --outputs-max KMAX] [--input rows|columns]
 //            [--reps R] [--warm-reps W [--warm-ms MS]] [--plant-sample FILE]
-//            [--null-device [--cpu-table]]
+//            [--null-device [--cpu-table]] [--output-count K] [--label-negation]
 // (W more queries, each started right after MS ms of a busy kernel on every
 // GPU: the rate at full clock, without the ramp from idle; warm_tx_per_s)
 // --plant-sample writes 256 planted rows and 256 unplanted rows, strided over
@@ -40,6 +40,9 @@
 // in the output = rows / the threads' mean time inside the host's calls
 // (cudasp_tf_function*): the host's own rate, without this driver's chunk
 // building (DuckDB's side of the vectors).
+// --output-count / --label-negation bind the protocol variants (DESIGN.md
+// section 6b); the planted values stay the reference's (output index 0, labels
+// added), which every variant still matches, and no other row may match.
 // Label keys: F holds L 64-byte keys (x || y, little-endian, bench.label_keys);
 // without F, L must be 0 or 1 (the SQL test's label, test/sql/cudasp.test:104).
 // Prints one JSON line; exit 0 iff every timed query emitted exactly the
@@ -107,6 +110,8 @@ struct Args {
   std::string plant_sample;  // JSON sample of planted / unplanted rows for the oracle check
   bool null_device = false;  // measurement only: no device work in the host's feeds
   bool cpu_table = false;    // with null_device: table generated on the CPU, no GPU needed
+  int output_count = 1;        // protocol variant: output indices per row (bind option output_count)
+  bool label_negation = false;  // protocol variant: labels also negated (bind option label_negation)
 };
 
 static Args parse(int argc, char** argv) {
@@ -134,6 +139,8 @@ static Args parse(int argc, char** argv) {
     else if (s == "--plant-sample") a.plant_sample = val();
     else if (s == "--null-device") a.null_device = true;
     else if (s == "--cpu-table") a.cpu_table = true;
+    else if (s == "--output-count") a.output_count = atoi(val());
+    else if (s == "--label-negation") a.label_negation = true;
     else {
       fprintf(stderr, "unknown argument %s\n", s.c_str());
       exit(1);
@@ -365,6 +372,11 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
   char err[512];
   if (cudasp_tf_bind(4, a_scan, a_spend, 1, a_lab.data(), (uint32_t)L, 1, 1, a.batch, &bd, err, sizeof(err)) != 0) {
     fprintf(stderr, "bind: %s\n", err);
+    exit(1);
+  }
+  if ((a.output_count != 1 || a.label_negation) &&
+      cudasp_tf_bind_options(bd, 1, a.output_count, 1, a.label_negation ? 1 : 0, 0, 0, err, sizeof(err)) != 0) {
+    fprintf(stderr, "bind options: %s\n", err);
     exit(1);
   }
   cudasp_tf_global* gs;

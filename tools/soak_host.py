@@ -7,7 +7,8 @@ ring wraps), row chunks or Arrow columns, 0 / 1 / 2 / 16 label keys, fixed or
 ragged output lists, 1 / 3 / 8 logical GPUs on the one card, streaming feeds or
 per-slot launches, the streaming slot count, plain or non-temporal slot copies,
 the spend-key fold on or off, streaming kernels that leave after 1-3 ms idle
-(relaunched by the next publish).  Every query must emit exactly the planted rows
+(relaunched by the next publish), output_count 1..13 and label negation (the
+planted values, index 0 and added labels, match under every variant).  Every query must emit exactly the planted rows
 (host_e2e's own check), and each run's 512-row sample is recomputed by the C
 oracle (oracle.check_planted_sample, checker use of oracle/).  Prints one line
 per run and a JSON summary; exit 1 on the first failure.
@@ -44,6 +45,8 @@ def shape(rng):
         fold=rng.choice(["", "0"]),
         reps=rng.choice([1, 2]),
         idle_ms=rng.choice(["", "", "1", "3"]),  # streaming kernels leave when idle this long: many relaunches
+        output_count=rng.choice([1, 1, 1, 2, 6, 7, 13]),  # protocol variants: > 6 = WIDE
+        label_negation=rng.choice([False, False, False, True]),
     )
 
 
@@ -63,9 +66,12 @@ def main():
     out = open(a.out, "w") if a.out else None
     while time.time() < t_end:
         sh = shape(rng)
-        # tiny batches on big tables take many slot cycles: keep a run bounded
+        # tiny batches on big tables take many slot cycles, K indices K x stage B:
+        # keep a run bounded
         if sh["batch"] < 2048 and sh["rows"] > 65536:
             sh["rows"] = 65536
+        if sh["output_count"] > 2 and sh["rows"] > 300001:
+            sh["rows"] = 300001
         env = dict(os.environ, CUDASP_TF_DEVICE_MAP=sh["device_map"])
         if sh["mode"] == "stream" and "," in sh["device_map"]:
             env["GPU_MAX_HW_QUEUES"] = "16"  # a hardware queue per feed's persistent kernel (as the 8-feed test)
@@ -79,7 +85,9 @@ def main():
         smp.close()
         cmd = [exe, "--rows", str(sh["rows"]), "--threads", str(sh["threads"]), "--batch", str(sh["batch"]),
                "--input", sh["input"], "--labels", str(sh["labels"]), "--reps", str(sh["reps"]),
-               "--plant-sample", smp.name] + sh["outputs"]
+               "--plant-sample", smp.name, "--output-count", str(sh["output_count"])] + sh["outputs"]
+        if sh["label_negation"]:
+            cmd.append("--label-negation")
         lf = None
         if sh["labels"]:
             lf = tempfile.NamedTemporaryFile(prefix="soak_labels_", suffix=".bin", delete=False)
