@@ -53,6 +53,7 @@ end-to-end leg's planted and unplanted rows, `e2e.planted_oracle_check`).
 host) where it covers the options, else the oracle port.
 """
 import argparse
+import ctypes
 import hashlib
 import json
 import os
@@ -987,6 +988,14 @@ def main():
         # Diagnostic only: the reported `matches` are the timed steps' counts above.
         print("rank %d: %d found, %d flagged, %d planted; found per step %s; batches (index, found, planted) "
               "that differ: %s" % (rank, found, flagged, tab.expected, step_found, bad[:16]), file=sys.stderr, flush=True)
+    # the shader clock of the last timed launch (the grid's first wave's
+    # s_memtime over s_memrealtime; boxes of the pool differ by a few percent)
+    clock = None
+    if multi:
+        mhz, secs = ctypes.c_double(0), ctypes.c_double(0)
+        if lib.cudasp_debug_multi_clock(device, ctypes.byref(mhz), ctypes.byref(secs)) == 0:
+            clock = dict(shader_mhz=round(mhz.value, 1), wave_s=round(secs.value, 4),
+                         note="last timed k_scan_multi launch: its first wave's s_memtime ticks over s_memrealtime")
     total_s, found, flagged, expected = aggregate(world, args.dist_backend, total_s, found, flagged, tab.expected)
     after_idle = None
     if multi and world == 1 and args.idle_samples:
@@ -1089,6 +1098,8 @@ def main():
     )
     if after_idle:
         result["device_after_idle"] = after_idle
+    if clock:
+        result["clock"] = clock
     if not args.no_layout_probe:
         result["layout_probe"] = layout_probe(lib, tab)
         if os.path.exists(args.pmc_summary) and not args.outputs_max and args.outputs_per_row == 2:

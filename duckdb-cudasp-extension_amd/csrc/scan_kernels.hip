@@ -518,6 +518,12 @@ struct MultiTick {
 };
 
 
+// The shader clock of the last k_scan_multi launch (cudasp_debug_multi_clock,
+// measurement only: the bench line's clock, which differs by a few percent
+// between boxes): the grid's first wave's s_memtime and s_memrealtime at its
+// start and end (it is its SIMD's oldest wave and runs until the drain).
+__device__ uint64_t g_multi_clock[4];
+
 template <int FBB, bool PIPE>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const MultiBatch* __restrict__ bd, uint32_t nb,
                                                                    uint32_t total_wr, const int8_t* __restrict__ naf,
@@ -543,6 +549,11 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
   bool more = true;
   uint32_t mine = 0;  // wave-rows this wave has claimed (lane 0)
   bool out = false;   // MultiTick: the counter has run out
+  const bool clock_wave = blockIdx.x == 0 && threadIdx.x == 0u;  // (nothing held across the loop)
+  if (clock_wave) {
+    g_multi_clock[0] = __builtin_amdgcn_s_memtime();
+    g_multi_clock[1] = wall_clock64();
+  }
   // MultiTick's priority: youngest first (blocks from 2 x tier_blocks), then
   // the middle tier (from tier_blocks); the oldest keep 0; tier_blocks = 0: off
   const uint32_t drain_level = tier_blocks == 0u                  ? 0u
@@ -693,6 +704,10 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
       pend_invert<MULTI_RMAX>(sc, PB, count);
       multi_finish(bd, nb, base, count, lane, k, labels, sc, PB, LB);
     }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0u) {
+    g_multi_clock[2] = __builtin_amdgcn_s_memtime();
+    g_multi_clock[3] = wall_clock64();
   }
 #if CUDASP_MULTI_TRACE
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
@@ -2961,6 +2976,21 @@ int cudasp_scan_device_batches(cudasp_scanner* s, const cudasp_device_batch* bat
   }
   return launch_multi(s, md, total_wr, st, rmax, multi_threshold_x100("CUDASP_MULTI_G1", 100),
                       multi_threshold_x100("CUDASP_MULTI_G2", 0), blocks);
+}
+
+int cudasp_debug_multi_clock(int device, double* mhz, double* seconds) {
+  if (!mhz) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
+  DeviceGuard g(device);
+  uint64_t c[4] = {};
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_multi_clock), sizeof(c)));
+  int rate_khz = 0;
+  HIP_TRY(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device));
+  if (c[3] <= c[1] || rate_khz <= 0) return set_error(CUDASP_ERR_INVALID_ARG, "no k_scan_multi launch recorded");
+  const double secs = (double)(c[3] - c[1]) / (rate_khz * 1e3);
+  *mhz = (double)(c[2] - c[0]) / secs / 1e6;
+  if (seconds) *seconds = secs;
+  return CUDASP_OK;
 }
 
 #if CUDASP_MULTI_TRACE

@@ -323,6 +323,12 @@ int cudasp_stage_match_device(cudasp_scanner* s, const uint32_t* d_t, const int6
                               const uint32_t* d_output_offsets, const uint32_t* d_output_lengths, uint32_t n,
                               uint8_t* d_match_flags, uint32_t* d_match_rows, uint32_t* d_match_count, void* stream);
 
+/* Shader clock of the last k_scan_multi launch on `device` (measurement
+ * only): s_memtime ticks over s_memrealtime time of the grid's first wave,
+ * in MHz, and that wave's life in seconds (may be NULL).  Synchronizes the
+ * device.  Boxes of one pool differ by a few percent in this clock. */
+int cudasp_debug_multi_clock(int device, double* mhz, double* seconds);
+
 /* Layout probe (measurement only): reads the algorithmic bytes of n rows
  * (tweak columns, offsets, lengths, outputs) and writes a flag per row, with
  * stage A's thread-to-row mapping and no arithmetic, so rocprof / HIP events
