@@ -33,7 +33,7 @@ def shape(rng):
     labels = rng.choice([0, 0, 1, 2, 16])
     return dict(
         rows=rows,
-        threads=rng.choice([1, 2, 3, 8, 16]),
+        threads=rng.choice([1, 2, 3, 8, 16, 32]),
         batch=rng.choice([1, 7, 2048, 5000, 65536, 300000]),
         input=rng.choice(["rows", "columns"]),
         labels=labels,
