@@ -1102,8 +1102,11 @@ __device__ __forceinline__ void stream_prefetch(StreamDev* dev, uint32_t& hint, 
 #pragma unroll
           for (int q = 0; q < 4; q++) v[i][q] = src[q];
         }
+        // lengths, or none: Arrow list offsets (n + 1 of them, a row's list
+        // from offs[r] to offs[r + 1]; cudasp_stream_batch)
+        const uint32_t* lp = pf[g + i].lens;
         of[i] = pf[g + i].offs[r];
-        ln[i] = pf[g + i].lens[r];
+        ln[i] = lp != nullptr ? lp[r] : pf[g + i].offs[r + 1] - of[i];
       }
     }
 #pragma unroll
@@ -3432,8 +3435,10 @@ int cudasp_stream_create(cudasp_scanner* s, uint32_t blocks, cudasp_stream** out
 int cudasp_stream_publish_batch(cudasp_stream* st, const cudasp_stream_batch* bt, uint64_t* seq) {
   if (!st || !bt) return set_error(CUDASP_ERR_INVALID_ARG, "null argument");
   const uint32_t n = bt->n;
-  if (n == 0 || !bt->tweak_keys || !bt->output_offsets || !bt->output_lengths || !bt->d_mirror)
+  if (n == 0 || !bt->tweak_keys || !bt->output_offsets || !bt->d_mirror)
     return set_error(CUDASP_ERR_INVALID_ARG, "empty batch or null buffer (the outputs mirror included)");
+  // no lengths: the offsets are Arrow list offsets, n + 1 of them
+  const size_t noffs = bt->output_lengths ? n : (size_t)n + 1;
   if (!bt->match_flags && !bt->match_rows)
     return set_error(CUDASP_ERR_INVALID_ARG, "a streamed batch needs match_flags and/or match_rows");
   // every host buffer the kernel touches must be coherent pinned memory
@@ -3442,8 +3447,8 @@ int cudasp_stream_publish_batch(cudasp_stream* st, const cudasp_stream_batch* bt
   // takes, are the caller's)
   if ((bt->match_flags && !host_range_coherent(bt->match_flags, n)) ||
       (bt->match_rows && !host_range_coherent(bt->match_rows, (size_t)n * 4)) ||
-      !host_range_coherent(bt->output_offsets, (size_t)n * 4) ||
-      !host_range_coherent(bt->output_lengths, (size_t)n * 4) ||
+      !host_range_coherent(bt->output_offsets, noffs * 4) ||
+      (bt->output_lengths && !host_range_coherent(bt->output_lengths, (size_t)n * 4)) ||
       !host_range_coherent(bt->tweak_keys, (size_t)n * 64) || (bt->outputs && !host_range_coherent(bt->outputs, 8)))
     return set_error(CUDASP_ERR_INVALID_ARG, "streamed batch buffers must come from cudasp_host_alloc");
   std::lock_guard<std::mutex> lk(st->mu);

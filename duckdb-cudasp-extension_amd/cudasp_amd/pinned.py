@@ -1,0 +1,210 @@
+"""A tweak table held in coherent pinned host memory and scanned in place.
+
+The reference copies every row of every query into per-thread strings and
+managed buffers (src/cudasp_extension.cu:188-223, 327-337); the table-function
+host (include/cudasp_host.h) still copies each chunk into its batch slots,
+which is the host's cost per row.  A tweak table is
+static while wallets (scan keys) come and go, so PinnedTable copies it ONCE
+into pinned memory (cudasp_host_alloc), laid out as the streaming kernel reads
+it -- 64-byte tweak blobs, the outputs list's int64 values and Arrow-style
+offsets (n + 1 per batch: cudasp_stream_batch with output_lengths NULL) -- and
+every scan() publishes those buffers to one persistent k_scan_stream as they
+are: no host copy per query, the GPU reads the rows over PCIe in place.
+
+Same inputs and semantics as cudasp_scan_arrow (columns by position: txid
+BLOB, height INTEGER, tweak_key BLOB(64), outputs BIGINT[]; rows with a NULL
+txid, height or tweak are skipped, a NULL list scans as empty, NULL list
+elements are dropped, a tweak of another size is an error), output_count and
+label_negation included (not full_x); results as a pyarrow Table (txid,
+height, tweak_key), row order unspecified like the reference's.
+"""
+import time
+
+import numpy as np
+
+from ._native import CudaspError
+from .scanner import HostBuffer, Scanner, ScanStream
+from .table_function import BoundScan, InvalidInputException
+
+STREAM_RING = 64  # batches in flight at most (include/cudasp_abi.h)
+ERR_INVALID_ARG, ERR_CAPACITY = -2, -5  # CUDASP_ERR_* (include/cudasp_abi.h)
+
+
+def _table(data):
+    import pyarrow as pa
+    if isinstance(data, pa.Table):
+        return data.combine_chunks()
+    if isinstance(data, pa.RecordBatch):
+        return pa.Table.from_batches([data])
+    return pa.Table.from_batches(list(data)).combine_chunks()
+
+
+def _blob64(arr):
+    """The 64-byte blobs of a binary / large_binary / fixed_size_binary(64)
+    array without nulls, as an (n, 64) uint8 array."""
+    import pyarrow as pa
+    n = len(arr)
+    if pa.types.is_fixed_size_binary(arr.type):
+        if arr.type.byte_width != 64:
+            raise CudaspError(ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %d bytes" % arr.type.byte_width)
+        data = np.frombuffer(arr.buffers()[1], dtype=np.uint8)
+        return data[arr.offset * 64:(arr.offset + n) * 64].reshape(n, 64)
+    ot = np.int64 if pa.types.is_large_binary(arr.type) else np.int32
+    offs = np.frombuffer(arr.buffers()[1], dtype=ot)[arr.offset:arr.offset + n + 1]
+    lens = np.diff(offs)
+    bad = np.nonzero(lens != 64)[0]
+    if bad.size:
+        raise CudaspError(ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %d bytes" % int(lens[bad[0]]))
+    data = np.frombuffer(arr.buffers()[2], dtype=np.uint8)
+    return data[int(offs[0]):int(offs[0]) + 64 * n].reshape(n, 64)
+
+
+def _lists(arr):
+    """(per-row start offsets (n + 1, int64, from 0), int64 values) of a
+    list<int64> / large_list<int64> array: a NULL list is empty, NULL elements
+    are dropped (src/cudasp_extension.cu:195-221)."""
+    import pyarrow as pa
+    n = len(arr)
+    ot = np.int64 if pa.types.is_large_list(arr.type) else np.int32
+    offs = np.frombuffer(arr.buffers()[1], dtype=ot)[arr.offset:arr.offset + n + 1].astype(np.int64)
+    if arr.null_count:
+        valid = np.asarray(arr.is_valid())
+        lens = np.where(valid, np.diff(offs), 0)
+    else:
+        lens = np.diff(offs)
+    child = arr.values  # the whole child array (offsets index into it)
+    vals = np.asarray(child.fill_null(0) if child.null_count else child).astype(np.int64, copy=False)
+    starts = offs[:-1]
+    # mark the child elements every (non-NULL) list covers
+    cover = np.zeros(len(child) + 1, dtype=np.int64)
+    np.add.at(cover, starts[lens > 0], 1)
+    np.add.at(cover, (starts + lens)[lens > 0], -1)
+    keep = np.cumsum(cover[:-1]) > 0
+    if child.null_count:
+        cvalid = np.asarray(child.is_valid())
+        elem_ok = keep & cvalid
+        # per-row counts of the valid elements
+        pref = np.concatenate([[0], np.cumsum(elem_ok.astype(np.int64))])
+        lens = pref[starts + lens] - pref[starts]
+        keep = elem_ok
+    out_offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    return out_offs, vals[keep]
+
+
+class PinnedTable:
+    """A tweak table in pinned host memory, batched for the streaming scan.
+
+        pt = PinnedTable(arrow_table)           # batch_size as cudasp_scan's (300000)
+        matches = pt.scan(scan_private_key, spend_public_key, label_keys)
+
+    batch_size as cudasp_scan's (rows per streamed batch); device: the GPU.
+    Holds ~64 + 8 k + 4 bytes of pinned memory per row (k outputs) plus a
+    device mirror of the outputs; close() (or the garbage collector) frees
+    it."""
+
+    def __init__(self, data, batch_size=None, device=0):
+        import pyarrow as pa
+        import torch
+        # the bind's batch_size rules and messages (CudaspScanBind :474-487)
+        if batch_size is None:
+            batch_size = 300000
+        elif not isinstance(batch_size, int) or isinstance(batch_size, bool):
+            raise InvalidInputException("batch_size parameter must be an INTEGER")
+        elif batch_size <= 0:
+            raise InvalidInputException("batch_size must be positive, got %d" % batch_size)
+        elif batch_size > 10_000_000:
+            raise InvalidInputException("batch_size too large (max 10,000,000), got %d" % batch_size)
+        t = _table(data)
+        if t.num_columns < 4:
+            raise InvalidInputException("cudasp_scan needs the columns (txid, height, tweak_key, outputs)")
+        txid, height, tweak, outputs = (t.column(i).combine_chunks() if t.column(i).num_chunks != 1
+                                        else t.column(i).chunk(0) for i in range(4))
+        valid = np.ones(t.num_rows, dtype=bool)
+        for col in (txid, height, tweak):
+            if col.null_count:
+                valid &= np.asarray(col.is_valid())
+        if not valid.all():
+            idx = pa.array(np.nonzero(valid)[0])
+            txid, height, tweak, outputs = (c.take(idx) for c in (txid, height, tweak, outputs))
+        self.n = len(txid)
+        self.txid, self.height = txid, height
+        tw = _blob64(tweak) if self.n else np.zeros((0, 64), dtype=np.uint8)
+        self.tweak = tweak
+        offs, vals = _lists(outputs) if self.n else (np.zeros(1, dtype=np.int64), np.zeros(0, dtype=np.int64))
+        self.device = device
+        self.batch_size = batch_size
+        dev = torch.device("cuda", device)
+        self.batches = []
+        for r0 in range(0, self.n, batch_size):
+            r1 = min(self.n, r0 + batch_size)
+            m = r1 - r0
+            o0, o1 = int(offs[r0]), int(offs[r1])
+            if o1 - o0 >= 2 ** 32:
+                raise CudaspError(ERR_CAPACITY, "a batch's outputs exceed u32 offsets: use a smaller batch_size")
+            b = dict(r0=r0, n=m)
+            b["rows"] = HostBuffer(64 * m)
+            b["rows"].array[:] = tw[r0:r1].reshape(-1)
+            b["outputs"] = HostBuffer(max(8, 8 * (o1 - o0)))
+            b["outputs"].view(np.int64)[:o1 - o0] = vals[o0:o1]
+            b["offsets"] = HostBuffer(4 * (m + 1))
+            b["offsets"].view(np.uint32)[:] = (offs[r0:r1 + 1] - o0).astype(np.uint32)
+            b["matches"] = HostBuffer(4 * m)
+            b["mirror"] = torch.empty((max(1, o1 - o0),), dtype=torch.int64, device=dev)
+            self.batches.append(b)
+        self.last_stats = None
+
+    def scan(self, scan_private_key, spend_public_key, label_keys, output_count=None, label_negation=None):
+        """cudasp_scan over the pinned table with these keys: every batch
+        published in place to one streaming kernel (at most 64 in flight),
+        then the matching rows gathered.  Returns a pyarrow Table (txid,
+        height, tweak_key); last_stats gets the scan's timing."""
+        import pyarrow as pa
+        bound = BoundScan(scan_private_key, spend_public_key, label_keys, self.batch_size,
+                          output_count=output_count, label_negation=label_negation)
+        del bound  # the reference's argument checks and errors
+        t0 = time.perf_counter()
+        hits = []
+
+        def collect(st, b, q):
+            # a done batch's matches: its count is readable until 64 more
+            # batches are published, its row indices stay in its buffer
+            st.wait(q)
+            c = st.matches(q)
+            if c:
+                hits.append(b["r0"] + b["matches"].view(np.uint32)[:c].astype(np.int64))
+
+        with Scanner(scan_private_key, spend_public_key, list(label_keys), max_rows=max(1, min(self.batch_size, 300000)),
+                     device=self.device) as s:
+            s.set_options(output_count=output_count or 1, label_negation=bool(label_negation))
+            with ScanStream(s) as st:
+                seqs = []
+                for i, b in enumerate(self.batches):
+                    if i >= STREAM_RING:
+                        collect(st, self.batches[i - STREAM_RING], seqs[i - STREAM_RING])
+                    seqs.append(st.publish(b["rows"], b["outputs"], b["offsets"], None, b["n"], None,
+                                           b["mirror"], b["matches"]))
+                st.close_input()
+                t_pub = time.perf_counter()
+                for i in range(max(0, len(seqs) - STREAM_RING), len(seqs)):
+                    collect(st, self.batches[i], seqs[i])
+                st.finish()
+        idx = np.sort(np.concatenate(hits)) if hits else np.zeros(0, dtype=np.int64)
+        t1 = time.perf_counter()
+        ia = pa.array(idx, type=pa.int64())
+        out = pa.table({"txid": self.txid.take(ia).cast(pa.binary()), "height": self.height.take(ia),
+                        "tweak_key": self.tweak.take(ia).cast(pa.binary())})
+        self.last_stats = dict(rows=self.n, batches=len(self.batches), matches=int(idx.size),
+                               scan_s=t1 - t0, publish_s=t_pub - t0, tx_per_s=self.n / (t1 - t0) if t1 > t0 else 0.0)
+        return out
+
+    def close(self):
+        for b in self.batches:
+            for k in ("rows", "outputs", "offsets", "matches"):
+                b[k].close()
+        self.batches = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -268,8 +268,9 @@ typedef struct cudasp_stream cudasp_stream;
 typedef struct {
   const uint8_t* tweak_keys;      /* n x 64 bytes (x then y, little-endian words) */
   const int64_t* outputs;         /* outputs CSR values (4 words per output with full_x) */
-  const uint32_t* output_offsets; /* n, in outputs */
-  const uint32_t* output_lengths; /* n */
+  const uint32_t* output_offsets; /* n, in outputs; n + 1 when output_lengths is NULL */
+  const uint32_t* output_lengths; /* n, or NULL: output_offsets are Arrow list offsets (row r's list is
+                                     outputs[offsets[r] .. offsets[r + 1]), e.g. a pinned Arrow column's) */
   uint32_t n;
   uint8_t* match_flags;           /* n flags, or NULL */
   uint32_t* match_rows;           /* room for n row indices, or NULL */

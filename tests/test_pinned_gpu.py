@@ -1,0 +1,104 @@
+"""GPU: PinnedTable (cudasp_amd/pinned.py) -- a tweak table copied once into
+pinned host memory and scanned in place by the streaming kernel, with Arrow
+list offsets (cudasp_stream_batch.output_lengths NULL) -- gives exactly
+cudasp_scan_arrow's rows: the SQL file's queries, NULL rules and slices,
+batch sizes that wrap the 64-entry descriptor ring, repeated scans of one
+pinned table with different keys, the protocol variants, and the reference's
+tweak-length error."""
+import pytest
+
+import golden_io
+from test_arrow_gpu import _arrow, _rows, _sql_table
+
+pytestmark = pytest.mark.gpu
+pa = pytest.importorskip("pyarrow")
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _keys(q):
+    return bytes.fromhex(q["scan_key"]), bytes.fromhex(q["spend_key"]), [bytes.fromhex(l) for l in q["label_keys"]]
+
+
+def test_sql_file_pinned(gpu):
+    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+    sc = golden_io.load("sql_cases.json")
+    for q in sc["queries"]:
+        tbl = _arrow(_sql_table(sc, q))
+        with PinnedTable(tbl, batch_size=q["batch_size"]) as pt:
+            out = pt.scan(*_keys(q))
+        assert _rows(out) == _rows(cudasp_scan_arrow(tbl, *_keys(q), batch_size=q["batch_size"])), q["line"]
+        got = [out.num_rows] if q["select"] == "count" else sorted(out.column("height").to_pylist())
+        assert got == q["expected"], (q["line"], got)
+
+
+def test_nulls_slices_types(gpu):
+    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+    sc = golden_io.load("sql_cases.json")
+    q = sc["queries"][2]
+    r = [x for x in sc["tables"]["test_data"] if x["height"] == 200][0]
+    tw, txid, v = bytes.fromhex(r["tweak"]), bytes.fromhex(r["txid"]), r["outputs"][0]
+    keys = (bytes.fromhex(q["scan_key"]), bytes.fromhex(q["spend_key"]), [])
+    rows = [
+        (txid, 1, tw, [v]), (None, 2, tw, [v]), (txid, None, tw, [v]), (txid, 4, None, [v]),
+        (txid, 5, tw, None), (txid, 6, tw, [None, v]), (txid, 7, tw, []), (b"", 8, tw, [v, v]),
+    ] * 50
+    for tweak_type in (None, pa.binary(64)):
+        for large in (False, True):
+            if large and tweak_type is not None:
+                continue
+            tbl = _arrow(rows, tweak_type, large)
+            for t in (tbl, tbl.slice(37, 250)):
+                with PinnedTable(t, batch_size=64) as pt:
+                    assert _rows(pt.scan(*keys)) == _rows(cudasp_scan_arrow(t, *keys))
+    with PinnedTable(_arrow([]), batch_size=10) as pt:
+        assert pt.scan(*keys).num_rows == 0
+
+
+@pytest.mark.parametrize("batch_size", [1, 37, 2048, 300000])
+def test_batches_ring_and_repeated_scans(gpu, batch_size):
+    """5120 random rows with planted base and label matches: at batch_size 1
+    and 37 more than 64 batches pass the descriptor ring; one pinned table is
+    scanned again with other keys and again with the first ones."""
+    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+    rr = golden_io.load("random_rows.json")
+    rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
+    tbl = _arrow(rows * 40 if batch_size > 1 else rows * 2)
+    k1 = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
+    k2 = (k1[0], k1[1], [])
+    want1 = _rows(cudasp_scan_arrow(tbl, *k1))
+    want2 = _rows(cudasp_scan_arrow(tbl, *k2))
+    assert want1 and want1 != want2
+    with PinnedTable(tbl, batch_size=batch_size) as pt:
+        assert _rows(pt.scan(*k1)) == want1
+        assert _rows(pt.scan(*k2)) == want2
+        assert _rows(pt.scan(*k1)) == want1
+        assert pt.last_stats["matches"] == len(want1) and pt.last_stats["batches"] == len(pt.batches)
+
+
+def test_variants(gpu):
+    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+    rr = golden_io.load("random_rows.json")
+    rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
+    tbl = _arrow(rows * 4)
+    keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
+    with PinnedTable(tbl, batch_size=100) as pt:
+        for oc, neg in ((2, None), (8, True), (None, True)):
+            want = _rows(cudasp_scan_arrow(tbl, *keys, batch_size=100, output_count=oc, label_negation=neg))
+            assert _rows(pt.scan(*keys, output_count=oc, label_negation=neg)) == want, (oc, neg)
+
+
+def test_errors(gpu):
+    from cudasp_amd import CudaspError, InvalidInputException, PinnedTable
+    rr = golden_io.load("random_rows.json")
+    with pytest.raises(CudaspError, match="64 bytes"):
+        PinnedTable(_arrow([(b"t", 1, bytes.fromhex(rr["rows"][0]["tweak"]), [1]), (b"u", 2, b"\x01" * 63, [1])]))
+    rows = [(b"t", 1, bytes.fromhex(rr["rows"][0]["tweak"]), [1])]
+    with PinnedTable(_arrow(rows)) as pt:
+        with pytest.raises(InvalidInputException):
+            pt.scan(b"\x01" * 31, bytes.fromhex(rr["spend_key"]), [])
