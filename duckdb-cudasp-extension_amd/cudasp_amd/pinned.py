@@ -152,6 +152,9 @@ class PinnedTable:
             b["mirror"] = torch.empty((max(1, o1 - o0),), dtype=torch.int64, device=dev)
             self.batches.append(b)
         self.last_stats = None
+        self._scanner = self._stream = None
+        self._stream_ok = False
+        self._stream_shape = None
 
     def scan(self, scan_private_key, spend_public_key, label_keys, output_count=None, label_negation=None):
         """cudasp_scan over the pinned table with these keys: every batch
@@ -173,21 +176,38 @@ class PinnedTable:
             if c:
                 hits.append(b["r0"] + b["matches"].view(np.uint32)[:c].astype(np.int64))
 
-        with Scanner(scan_private_key, spend_public_key, list(label_keys), max_rows=max(1, min(self.batch_size, 300000)),
-                     device=self.device) as s:
-            s.set_options(output_count=output_count or 1, label_negation=bool(label_negation))
-            with ScanStream(s) as st:
-                seqs = []
-                for i, b in enumerate(self.batches):
-                    if i >= STREAM_RING:
-                        collect(st, self.batches[i - STREAM_RING], seqs[i - STREAM_RING])
-                    seqs.append(st.publish(b["rows"], b["outputs"], b["offsets"], None, b["n"], None,
-                                           b["mirror"], b["matches"]))
-                st.close_input()
-                t_pub = time.perf_counter()
-                for i in range(max(0, len(seqs) - STREAM_RING), len(seqs)):
-                    collect(st, self.batches[i], seqs[i])
-                st.finish()
+        # one scanner and stream per pinned table, rebound to each scan's keys
+        # (a scanner's creation, its stream's and their allocations cost
+        # milliseconds: a 1M-row scan takes ~6 ms on the device)
+        if self._scanner is None:
+            self._scanner = Scanner(scan_private_key, spend_public_key, list(label_keys),
+                                    max_rows=max(1, min(self.batch_size, 300000)), device=self.device)
+        else:
+            self._scanner.set_keys(scan_private_key, spend_public_key, list(label_keys))
+        s = self._scanner
+        s.set_options(output_count=output_count or 1, label_negation=bool(label_negation))
+        # a stream is sized (scratch, grid) for its scanner's label count and
+        # output indices when created: a new one when they change
+        shape = (len(list(label_keys)), output_count or 1, bool(label_negation))
+        if self._stream is None or not self._stream_ok or shape != self._stream_shape:
+            if self._stream is not None:
+                self._stream.close()
+            self._stream = ScanStream(s)
+            self._stream_shape = shape
+        st = self._stream
+        self._stream_ok = False  # until this scan finishes
+        seqs = []
+        for i, b in enumerate(self.batches):
+            if i >= STREAM_RING:
+                collect(st, self.batches[i - STREAM_RING], seqs[i - STREAM_RING])
+            seqs.append(st.publish(b["rows"], b["outputs"], b["offsets"], None, b["n"], None,
+                                   b["mirror"], b["matches"]))
+        st.close_input()
+        t_pub = time.perf_counter()
+        for i in range(max(0, len(seqs) - STREAM_RING), len(seqs)):
+            collect(st, self.batches[i], seqs[i])
+        st.finish()  # the stream is reset for the next scan
+        self._stream_ok = True
         idx = np.sort(np.concatenate(hits)) if hits else np.zeros(0, dtype=np.int64)
         t1 = time.perf_counter()
         ia = pa.array(idx, type=pa.int64())
@@ -198,6 +218,12 @@ class PinnedTable:
         return out
 
     def close(self):
+        if self._stream is not None:
+            self._stream.close()
+            self._stream = None
+        if self._scanner is not None:
+            self._scanner.close()
+            self._scanner = None
         for b in self.batches:
             for k in ("rows", "outputs", "offsets", "matches"):
                 b[k].close()
