@@ -97,12 +97,16 @@ class PinnedTable:
         pt = PinnedTable(arrow_table)           # batch_size as cudasp_scan's (300000)
         matches = pt.scan(scan_private_key, spend_public_key, label_keys)
 
-    batch_size as cudasp_scan's (rows per streamed batch); device: the GPU.
-    Holds ~64 + 8 k + 4 bytes of pinned memory per row (k outputs) plus a
-    device mirror of the outputs; close() (or the garbage collector) frees
-    it."""
+    batch_size as cudasp_scan's (rows per streamed batch).  devices: the GPUs
+    (default [device]); batch b goes to devices[b % len(devices)], round-robin
+    like the reference's threads over its GPUs (src/cudasp_extension.cu:523-529),
+    each GPU with its own streaming kernel; a device listed k times runs k
+    kernels on 1/k of its wave slots each (logical GPUs, as
+    CUDASP_TF_DEVICE_MAP).  Holds ~64 + 8 k + 4 bytes of pinned memory per row
+    (k outputs) plus a device mirror of each batch's outputs on its GPU;
+    close() (or the garbage collector) frees it."""
 
-    def __init__(self, data, batch_size=None, device=0):
+    def __init__(self, data, batch_size=None, device=0, devices=None):
         import pyarrow as pa
         import torch
         # the bind's batch_size rules and messages (CudaspScanBind :474-487)
@@ -131,9 +135,8 @@ class PinnedTable:
         tw = _blob64(tweak) if self.n else np.zeros((0, 64), dtype=np.uint8)
         self.tweak = tweak
         offs, vals = _lists(outputs) if self.n else (np.zeros(1, dtype=np.int64), np.zeros(0, dtype=np.int64))
-        self.device = device
+        self.devices = [int(d) for d in (devices if devices else [device])]
         self.batch_size = batch_size
-        dev = torch.device("cuda", device)
         self.batches = []
         for r0 in range(0, self.n, batch_size):
             r1 = min(self.n, r0 + batch_size)
@@ -141,7 +144,9 @@ class PinnedTable:
             o0, o1 = int(offs[r0]), int(offs[r1])
             if o1 - o0 >= 2 ** 32:
                 raise CudaspError(ERR_CAPACITY, "a batch's outputs exceed u32 offsets: use a smaller batch_size")
-            b = dict(r0=r0, n=m)
+            lg = len(self.batches) % len(self.devices)  # logical GPU of this batch
+            dev = torch.device("cuda", self.devices[lg])
+            b = dict(r0=r0, n=m, lg=lg)
             b["rows"] = HostBuffer(64 * m)
             b["rows"].array[:] = tw[r0:r1].reshape(-1)
             b["outputs"] = HostBuffer(max(8, 8 * (o1 - o0)))
@@ -152,7 +157,8 @@ class PinnedTable:
             b["mirror"] = torch.empty((max(1, o1 - o0),), dtype=torch.int64, device=dev)
             self.batches.append(b)
         self.last_stats = None
-        self._scanner = self._stream = None
+        nl = len(self.devices)
+        self._scanners, self._streams = [None] * nl, [None] * nl
         self._stream_ok = False
         self._stream_shape = None
 
@@ -176,37 +182,42 @@ class PinnedTable:
             if c:
                 hits.append(b["r0"] + b["matches"].view(np.uint32)[:c].astype(np.int64))
 
-        # one scanner and stream per pinned table, rebound to each scan's keys
-        # (a scanner's creation, its stream's and their allocations cost
-        # milliseconds: a 1M-row scan takes ~6 ms on the device)
-        if self._scanner is None:
-            self._scanner = Scanner(scan_private_key, spend_public_key, list(label_keys),
-                                    max_rows=max(1, min(self.batch_size, 300000)), device=self.device)
-        else:
-            self._scanner.set_keys(scan_private_key, spend_public_key, list(label_keys))
-        s = self._scanner
-        s.set_options(output_count=output_count or 1, label_negation=bool(label_negation))
-        # a stream is sized (scratch, grid) for its scanner's label count and
-        # output indices when created: a new one when they change
-        shape = (len(list(label_keys)), output_count or 1, bool(label_negation))
-        if self._stream is None or not self._stream_ok or shape != self._stream_shape:
-            if self._stream is not None:
-                self._stream.close()
-            self._stream = ScanStream(s)
-            self._stream_shape = shape
-        st = self._stream
+        # one scanner and stream per logical GPU, kept and rebound to each
+        # scan's keys (a scanner's creation, its stream's and their
+        # allocations cost milliseconds: a 1M-row scan takes ~6 ms on the GPU)
+        labels = list(label_keys)
+        shape = (len(labels), output_count or 1, bool(label_negation))
+        fresh = not self._stream_ok or shape != self._stream_shape
+        for lg, d in enumerate(self.devices):
+            if self._scanners[lg] is None:
+                self._scanners[lg] = Scanner(scan_private_key, spend_public_key, labels,
+                                             max_rows=max(1, min(self.batch_size, 300000)), device=d)
+            else:
+                self._scanners[lg].set_keys(scan_private_key, spend_public_key, labels)
+            self._scanners[lg].set_options(output_count=output_count or 1, label_negation=bool(label_negation))
+            # a stream is sized (scratch, grid) for its scanner's label count
+            # and output indices when created: a new one when they change
+            if fresh or self._streams[lg] is None:
+                if self._streams[lg] is not None:
+                    self._streams[lg].close()
+                self._streams[lg] = ScanStream(self._scanners[lg], self._blocks(d))
+        self._stream_shape = shape
         self._stream_ok = False  # until this scan finishes
-        seqs = []
+        seqs = [[] for _ in self.devices]  # per logical GPU: (batch index, seq) in publish order
         for i, b in enumerate(self.batches):
-            if i >= STREAM_RING:
-                collect(st, self.batches[i - STREAM_RING], seqs[i - STREAM_RING])
-            seqs.append(st.publish(b["rows"], b["outputs"], b["offsets"], None, b["n"], None,
-                                   b["mirror"], b["matches"]))
-        st.close_input()
+            lg, st = b["lg"], self._streams[b["lg"]]
+            if len(seqs[lg]) >= STREAM_RING:
+                j, q = seqs[lg][-STREAM_RING]
+                collect(st, self.batches[j], q)
+            seqs[lg].append((i, st.publish(b["rows"], b["outputs"], b["offsets"], None, b["n"], None,
+                                           b["mirror"], b["matches"])))
+        for st in self._streams:
+            st.close_input()
         t_pub = time.perf_counter()
-        for i in range(max(0, len(seqs) - STREAM_RING), len(seqs)):
-            collect(st, self.batches[i], seqs[i])
-        st.finish()  # the stream is reset for the next scan
+        for lg, st in enumerate(self._streams):
+            for j, q in seqs[lg][-STREAM_RING:]:
+                collect(st, self.batches[j], q)
+            st.finish()  # the stream is reset for the next scan
         self._stream_ok = True
         idx = np.sort(np.concatenate(hits)) if hits else np.zeros(0, dtype=np.int64)
         t1 = time.perf_counter()
@@ -217,13 +228,23 @@ class PinnedTable:
                                scan_s=t1 - t0, publish_s=t_pub - t0, tx_per_s=self.n / (t1 - t0) if t1 > t0 else 0.0)
         return out
 
+    def _blocks(self, d):
+        """A logical GPU's grid: its device's wave slots shared by the logical
+        GPUs on it (0 = the whole device)."""
+        k = self.devices.count(d)
+        if k == 1:
+            return 0
+        import torch
+        return torch.cuda.get_device_properties(d).multi_processor_count * 3 // k
+
     def close(self):
-        if self._stream is not None:
-            self._stream.close()
-            self._stream = None
-        if self._scanner is not None:
-            self._scanner.close()
-            self._scanner = None
+        for lg in range(len(self.devices)):
+            if self._streams[lg] is not None:
+                self._streams[lg].close()
+                self._streams[lg] = None
+            if self._scanners[lg] is not None:
+                self._scanners[lg].close()
+                self._scanners[lg] = None
         for b in self.batches:
             for k in ("rows", "outputs", "offsets", "matches"):
                 b[k].close()

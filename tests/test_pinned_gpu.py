@@ -102,3 +102,20 @@ def test_errors(gpu):
     with PinnedTable(_arrow(rows)) as pt:
         with pytest.raises(InvalidInputException):
             pt.scan(b"\x01" * 31, bytes.fromhex(rr["spend_key"]), [])
+
+
+@pytest.mark.parametrize("devices,batch_size", [([0, 0], 37), ([0, 0, 0], 2048)])
+def test_logical_gpus(gpu, devices, batch_size):
+    """Batches round-robin over 2 or 3 logical GPUs on the one card (each its
+    own scanner and streaming kernel on a share of the wave slots; at
+    batch_size 37 each stream's 64-entry ring wraps): the rows of one GPU."""
+    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+    rr = golden_io.load("random_rows.json")
+    rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
+    tbl = _arrow(rows * 40)
+    keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
+    want = _rows(cudasp_scan_arrow(tbl, *keys))
+    with PinnedTable(tbl, batch_size=batch_size, devices=devices) as pt:
+        assert {b["lg"] for b in pt.batches} == set(range(len(devices)))
+        assert _rows(pt.scan(*keys)) == want
+        assert _rows(pt.scan(*keys[:2], [])) == _rows(cudasp_scan_arrow(tbl, *keys[:2], []))
