@@ -48,6 +48,9 @@ on this box's host cores as `cpu_baseline_port` and checked against the GPU
 flags; it also recomputes the planted values of 256 planted rows spread over
 the whole rank table, `planted_oracle_check`, and of a 256-row sample of the
 end-to-end leg's planted and unplanted rows, `e2e.planted_oracle_check`).
+The `pinned` leg scans the same table pinned once in host memory, in place
+(cudasp_amd.PinnedTable over all N GPUs, no host copy per query; DESIGN.md
+section 7e).
 `cpu_baseline` itself is the strongest CPU stand-in the image allows:
 `port-optimized` (tools/cpu_port, the product's row pipeline compiled for the
 host) where it covers the options, else the oracle port.
@@ -504,6 +507,32 @@ def host_cores():
     return visible, visible, "sched_getaffinity"
 
 
+def pinned_leg(args, labels, world):
+    """Zero-copy scans of the same table (cudasp_amd.PinnedTable, DESIGN.md
+    section 7e): tools/pinned_bench.py as a child process builds the table,
+    copies it ONCE into pinned host memory and scans it 3 times in place over
+    all `world` GPUs (batches round-robin, one streaming kernel per GPU, no
+    host copy per query); every scan must emit exactly the planted rows."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "pinned_bench.py"), "--rows", str(args.rows), "--batch-size",
+           str(args.batch_size), "--labels", str(len(labels)), "--reps", "3",
+           "--devices", ",".join(str(d) for d in range(world))]
+    if args.outputs_max:
+        cmd += ["--outputs-max", str(args.outputs_max)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.e2e_timeout)
+    except subprocess.TimeoutExpired:
+        return dict(error="timed out after %d s" % args.e2e_timeout)
+    line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else ""
+    try:
+        res = json.loads(line)
+    except ValueError:
+        return dict(error="exit %d: %s" % (r.returncode, (r.stderr or r.stdout)[-400:]))
+    if not res.get("diffs"):
+        res.pop("diffs", None)
+    return res
+
+
 def e2e_leg(args, labels, world, fb_bits, mode=None):
     """PCIe-inclusive end-to-end rate through the table-function host
     (include/cudasp_host.h, the calls DuckDB's executor makes) over all
@@ -900,6 +929,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layout-probe", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-pinned", action="store_true", help="skip the pinned-table leg (cudasp_amd.PinnedTable)")
     ap.add_argument("--no-e2e-launch", action="store_true",
                     help="skip the second end-to-end leg with the host's per-slot launches (CUDASP_TF_MODE=launch)")
     ap.add_argument("--e2e-threads", type=int, default=0,
@@ -1186,6 +1216,11 @@ def main():
                 el = e2e_leg(args, labels, world, args.fb_bits, mode="launch")
                 result["e2e_launch"] = el
                 result["e2e_launch_tx_s"] = el.get("tx_per_s")
+            if not args.no_pinned and args.fb_bits in (0, 26):
+                # the table pinned once and scanned in place: no host copy per query
+                pn = pinned_leg(args, labels, world)
+                result["pinned"] = pn
+                result["pinned_tx_s"] = pn.get("tx_per_s")
         if world > 1:
             dist.barrier(group=cpu_group)
     if rank == 0:

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--outputs-max", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--probe", action="store_true", help="diagnosis: scan the last batch alone two ways")
+    ap.add_argument("--devices", default="0", help="GPUs of the scans, e.g. 0,1,2,3 (batches round-robin)")
     a = ap.parse_args()
     import pyarrow as pa
     import torch
@@ -79,7 +80,8 @@ def main():
     })
     t_build = time.perf_counter() - t0
     t0 = time.perf_counter()
-    pt = PinnedTable(table, batch_size=a.batch_size)
+    devices = [int(x) for x in a.devices.split(",")]
+    pt = PinnedTable(table, batch_size=a.batch_size, devices=devices)
     t_pin = time.perf_counter() - t0
     scans = []
     for r in range(a.reps + 1):  # the first scan warms the process (tables, scratch)
@@ -107,7 +109,7 @@ def main():
     timed = scans[1:]
     med = float(np.median([s["scan_s"] for s in timed]))
     res = dict(what="PinnedTable.scan: pinned host table scanned in place (one streaming kernel, no host copies)",
-               rows=a.rows, batch_size=a.batch_size, labels=a.labels, outputs_max=a.outputs_max,
+               rows=a.rows, batch_size=a.batch_size, labels=a.labels, outputs_max=a.outputs_max, devices=devices,
                expected=expected, exact=all(s["exact"] for s in scans), build_s=round(t_build, 2),
                pin_s=round(t_pin, 2), scans=[dict(s=round(s["scan_s"], 4), tx_per_s=round(s["tx_per_s"])) for s in timed],
                tx_per_s=a.rows / med, warmup_s=round(scans[0]["scan_s"], 4),
