@@ -1216,7 +1216,8 @@ def main():
                 el = e2e_leg(args, labels, world, args.fb_bits, mode="launch")
                 result["e2e_launch"] = el
                 result["e2e_launch_tx_s"] = el.get("tx_per_s")
-            if not args.no_pinned and args.fb_bits in (0, 26):
+            if not args.no_pinned and args.fb_bits in (0, 26) and args.rows <= 40_000_000:
+                # (the child rebuilds the table in host memory: bounded to config-4 sizes)
                 # the table pinned once and scanned in place: no host copy per query
                 pn = pinned_leg(args, labels, world)
                 result["pinned"] = pn
