@@ -516,7 +516,7 @@ def pinned_leg(args, labels, world):
     import subprocess
     cmd = [sys.executable, os.path.join(ROOT, "tools", "pinned_bench.py"), "--rows", str(args.rows), "--batch-size",
            str(args.batch_size), "--labels", str(len(labels)), "--reps", "3",
-           "--devices", ",".join(str(d) for d in range(world))]
+           "--devices", ",".join(str(r % max(1, torch.cuda.device_count())) for r in range(world))]
     if args.outputs_max:
         cmd += ["--outputs-max", str(args.outputs_max)]
     try:
