@@ -203,21 +203,25 @@ class PinnedTable:
                 self._streams[lg] = ScanStream(self._scanners[lg], self._blocks(d))
         self._stream_shape = shape
         self._stream_ok = False  # until this scan finishes
+        import torch
         seqs = [[] for _ in self.devices]  # per logical GPU: (batch index, seq) in publish order
         for i, b in enumerate(self.batches):
             lg, st = b["lg"], self._streams[b["lg"]]
-            if len(seqs[lg]) >= STREAM_RING:
-                j, q = seqs[lg][-STREAM_RING]
-                collect(st, self.batches[j], q)
-            seqs[lg].append((i, st.publish(b["rows"], b["outputs"], b["offsets"], None, b["n"], None,
-                                           b["mirror"], b["matches"])))
-        for st in self._streams:
-            st.close_input()
+            with torch.cuda.device(self.devices[lg]):  # (the library sets it too; cheap insurance)
+                if len(seqs[lg]) >= STREAM_RING:
+                    j, q = seqs[lg][-STREAM_RING]
+                    collect(st, self.batches[j], q)
+                seqs[lg].append((i, st.publish(b["rows"], b["outputs"], b["offsets"], None, b["n"], None,
+                                               b["mirror"], b["matches"])))
+        for lg, st in enumerate(self._streams):
+            with torch.cuda.device(self.devices[lg]):
+                st.close_input()
         t_pub = time.perf_counter()
         for lg, st in enumerate(self._streams):
-            for j, q in seqs[lg][-STREAM_RING:]:
-                collect(st, self.batches[j], q)
-            st.finish()  # the stream is reset for the next scan
+            with torch.cuda.device(self.devices[lg]):
+                for j, q in seqs[lg][-STREAM_RING:]:
+                    collect(st, self.batches[j], q)
+                st.finish()  # the stream is reset for the next scan
         self._stream_ok = True
         idx = np.sort(np.concatenate(hits)) if hits else np.zeros(0, dtype=np.int64)
         t1 = time.perf_counter()
