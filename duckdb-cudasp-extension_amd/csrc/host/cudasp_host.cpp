@@ -56,6 +56,7 @@
 #include <vector>
 
 #include "../../../include/cudasp_abi.h"
+#include "bind_data.hpp"
 #include "slot_copy.hpp"
 
 namespace {
@@ -125,15 +126,6 @@ extern "C" void cudasp_internal_trace_host(uint32_t kind, uint64_t a, uint32_t b
 #else
 #define ST_HOST(...) ((void)0)
 #endif
-
-struct cudasp_tf_bind_data {
-  uint64_t batch_size = CUDASP_TF_DEFAULT_BATCH;
-  cudasp_scan_options opt{1, 0, 0};  // named parameters output_count / label_negation / full_x
-  std::string scan_private_key_data;
-  std::string spend_public_key_data;
-  std::vector<std::string> label_keys_data;
-  std::string label_keys_flat;  // label_count x 64, back to back
-};
 
 namespace {
 

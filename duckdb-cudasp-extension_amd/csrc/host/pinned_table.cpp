@@ -1,0 +1,458 @@
+// Pinned tables (include/cudasp_host.h, cudasp_pinned_*): a tweak table copied
+// once into coherent pinned host memory and scanned in place by the streaming
+// kernel (cudasp_stream_*, include/cudasp_abi.h) for every query.
+//
+// The reference re-reads every row of every query into per-thread strings
+// (src/cudasp_extension.cu:188-223) and copies each batch into managed buffers
+// (:327-337, src/cudasp_gpu.cu:705-761); the table-function host of this
+// library (cudasp_host.cpp) still copies each chunk into its batch slots, the
+// host's cost per row.  Here a scan only publishes the
+// pinned batches: the kernel reads the 64-byte tweak blobs, the outputs and
+// their Arrow list offsets (cudasp_stream_batch.output_lengths NULL) over PCIe
+// and writes the matching row indices back.  Same algorithm as the Python
+// cudasp_amd.PinnedTable, without the interpreter in the publish loop.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../../include/cudasp_abi.h"
+#include "../../../include/cudasp_host.h"
+#include "bind_data.hpp"
+
+extern "C" void cudasp_internal_set_error(const char* msg);
+
+namespace {
+
+constexpr uint64_t TWEAK_KEY_SIZE = 64;      // CudaspScanBindData::TWEAK_KEY_SIZE
+constexpr uint64_t MAX_BATCH = 10000000;     // CudaspScanBind's batch_size limit (:474-487)
+constexpr uint64_t STREAM_RING = 64;         // batches published and not yet harvested, per stream
+constexpr uint64_t MAX_WORDS = 0xFFFFFFFFu;  // a batch's outputs: u32 offsets
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  cudasp_internal_set_error(buf);
+  return code;
+}
+
+inline bool bit(const uint8_t* bm, uint64_t i) { return bm == nullptr || ((bm[i >> 3] >> (i & 7)) & 1u); }
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct DeviceSet {
+  int prev = -1;
+  explicit DeviceSet(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceSet() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// One closed batch: pinned rows, outputs, Arrow offsets (n + 1) and match
+// indices, a device mirror of its outputs, and the input numbers of its rows.
+struct Batch {
+  uint32_t n = 0;
+  uint64_t words = 0;
+  uint8_t* rows = nullptr;
+  int64_t* outputs = nullptr;
+  uint32_t* offsets = nullptr;
+  uint32_t* matches = nullptr;
+  int64_t* d_mirror = nullptr;
+  int device = 0;
+  uint32_t lg = 0;
+  uint64_t ord0 = 0;          // input number of row 0
+  std::vector<uint64_t> ord;  // every row's input number, when rows were skipped (else ord0 + r)
+  uint64_t number(uint32_t r) const { return ord.empty() ? ord0 + r : ord[r]; }
+};
+
+// The open batch, in pageable memory until it closes.
+struct Staging {
+  std::vector<uint8_t> rows;
+  std::vector<int64_t> outputs;
+  std::vector<uint32_t> offsets{0};
+  std::vector<uint64_t> ord;
+  bool dense = true;  // ord[r] == ord[0] + r
+  uint64_t n() const { return ord.size(); }
+};
+
+struct Shape {
+  uint32_t labels = 0, output_count = 0, negation = 0;
+  bool operator==(const Shape& o) const {
+    return labels == o.labels && output_count == o.output_count && negation == o.negation;
+  }
+};
+
+}  // namespace
+
+struct cudasp_pinned_table {
+  uint64_t batch_size = CUDASP_TF_DEFAULT_BATCH;
+  std::vector<int> devices;  // per logical GPU
+  std::vector<uint32_t> blocks;
+  std::vector<Batch> batches;
+  Staging open;
+  uint64_t appended = 0, pinned_rows = 0, pinned_bytes = 0;
+  std::vector<cudasp_scanner*> scanners;
+  std::vector<cudasp_stream*> streams;
+  bool stream_ok = false;
+  Shape shape;
+  bool abandoned = false;  // a scan's kernel outlived its timeout: never free what it may touch
+  uint64_t last_matches = 0;
+  double last_scan_s = 0, last_publish_s = 0;
+  mutable std::mutex mu;
+};
+
+namespace {
+
+void free_batch(Batch& b) {
+  if (b.d_mirror) {
+    DeviceSet ds(b.device);
+    (void)hipFree(b.d_mirror);
+  }
+  cudasp_host_free(b.rows);
+  cudasp_host_free(b.outputs);
+  cudasp_host_free(b.offsets);
+  cudasp_host_free(b.matches);
+  b = Batch();
+}
+
+// Close the open batch: copy it into pinned memory and give it its mirror on
+// its logical GPU's device.
+int seal(cudasp_pinned_table& t) {
+  Staging& s = t.open;
+  const uint64_t n = s.n();
+  if (n == 0) return CUDASP_OK;
+  Batch b;
+  b.n = (uint32_t)n;
+  b.words = s.outputs.size();
+  b.lg = (uint32_t)(t.batches.size() % t.devices.size());
+  b.device = t.devices[b.lg];
+  b.ord0 = s.ord[0];
+  const size_t wb = std::max<size_t>(1, b.words) * sizeof(int64_t);
+  int rc = cudasp_host_alloc((void**)&b.rows, n * TWEAK_KEY_SIZE);
+  if (rc == CUDASP_OK) rc = cudasp_host_alloc((void**)&b.outputs, wb);
+  if (rc == CUDASP_OK) rc = cudasp_host_alloc((void**)&b.offsets, (n + 1) * sizeof(uint32_t));
+  if (rc == CUDASP_OK) rc = cudasp_host_alloc((void**)&b.matches, n * sizeof(uint32_t));
+  if (rc != CUDASP_OK) {
+    free_batch(b);
+    return fail(CUDASP_ERR_CAPACITY, "pinned table: host allocation for a batch of %llu rows failed",
+                (unsigned long long)n);
+  }
+  {
+    DeviceSet ds(b.device);
+    if (hipMalloc((void**)&b.d_mirror, wb) != hipSuccess) {
+      b.d_mirror = nullptr;
+      free_batch(b);
+      return fail(CUDASP_ERR_HIP, "pinned table: outputs mirror of %zu bytes on device %d: allocation failed", wb,
+                  b.device);
+    }
+  }
+  memcpy(b.rows, s.rows.data(), n * TWEAK_KEY_SIZE);
+  if (b.words) memcpy(b.outputs, s.outputs.data(), b.words * sizeof(int64_t));
+  memcpy(b.offsets, s.offsets.data(), (n + 1) * sizeof(uint32_t));
+  if (!s.dense) b.ord = s.ord;
+  t.pinned_bytes += n * TWEAK_KEY_SIZE + wb + (2 * n + 1) * sizeof(uint32_t);
+  t.pinned_rows += n;
+  t.batches.push_back(std::move(b));
+  s.rows.clear();
+  s.outputs.clear();
+  s.offsets.assign(1, 0);
+  s.ord.clear();
+  s.dense = true;
+  return CUDASP_OK;
+}
+
+// Finish every stream after a failed scan; a stream whose kernel is still
+// running after the timeout pins the table (nothing it reads may be freed).
+void reset_streams(cudasp_pinned_table& t) {
+  for (size_t lg = 0; lg < t.streams.size(); lg++) {
+    if (!t.streams[lg]) continue;
+    DeviceSet ds(t.devices[lg]);
+    (void)cudasp_stream_finish(t.streams[lg]);
+    if (cudasp_stream_abandoned(t.streams[lg])) {
+      t.abandoned = true;
+      continue;
+    }
+    cudasp_stream_destroy(t.streams[lg]);
+    t.streams[lg] = nullptr;
+  }
+  t.stream_ok = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cudasp_pinned_create(uint64_t batch_size, const int* devices, uint32_t device_count, cudasp_pinned_table** out) {
+  if (!out) return fail(CUDASP_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  if (batch_size == 0) batch_size = CUDASP_TF_DEFAULT_BATCH;
+  if (batch_size > MAX_BATCH)
+    return fail(CUDASP_ERR_INVALID_ARG, "batch_size too large (max 10,000,000), got %llu",
+                (unsigned long long)batch_size);
+  if (devices && device_count == 0) return fail(CUDASP_ERR_INVALID_ARG, "device_count must be positive");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(CUDASP_ERR_NO_DEVICE, "no GPU");
+  auto* t = new cudasp_pinned_table();
+  t->batch_size = batch_size;
+  if (devices)
+    t->devices.assign(devices, devices + device_count);
+  else
+    t->devices.assign(1, 0);
+  for (int d : t->devices)
+    if (d < 0 || d >= ndev) {
+      delete t;
+      return fail(CUDASP_ERR_INVALID_ARG, "device %d out of range (%d GPUs)", d, ndev);
+    }
+  // a logical GPU's grid: its device's wave slots shared by the logical GPUs
+  // on it (0 = the whole device, 3 waves per SIMD)
+  for (int d : t->devices) {
+    const int m = (int)std::count(t->devices.begin(), t->devices.end(), d);
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || cus <= 0) cus = 256;
+    t->blocks.push_back(m == 1 ? 0u : (uint32_t)(cus * 3 / m));
+  }
+  t->scanners.assign(t->devices.size(), nullptr);
+  t->streams.assign(t->devices.size(), nullptr);
+  t->open.rows.reserve(std::min<uint64_t>(batch_size, 1u << 16) * TWEAK_KEY_SIZE);
+  *out = t;
+  return CUDASP_OK;
+}
+
+int cudasp_pinned_append(cudasp_pinned_table* t, const cudasp_tf_columns* cols) {
+  if (!t || !cols) return fail(CUDASP_ERR_INVALID_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(t->mu);
+  if (t->abandoned) return fail(CUDASP_ERR_HIP, "pinned table: a scan's kernel is still running");
+  const cudasp_tf_columns& c = *cols;
+  const uint64_t n = c.count;
+  if (n == 0) return CUDASP_OK;
+  if (!c.tweak_data || !c.list_offsets) return fail(CUDASP_ERR_INVALID_ARG, "tweak_key and outputs columns needed");
+  if (!c.tweak_offsets && c.tweak_fixed_width <= 0)
+    return fail(CUDASP_ERR_INVALID_ARG, "tweak_key: offsets or a fixed width needed");
+  auto row_ok = [&](uint64_t i) {
+    return bit(c.txid_validity, c.txid_offset + i) && bit(c.height_validity, c.height_offset + i) &&
+           bit(c.tweak_validity, c.tweak_offset + i);
+  };
+  auto tweak_size = [&](uint64_t i) -> uint64_t {
+    if (c.tweak_offsets) {
+      const int32_t* to = c.tweak_offsets + c.tweak_offset;
+      return (uint64_t)(to[i + 1] - to[i]);
+    }
+    return (uint64_t)c.tweak_fixed_width;
+  };
+  auto tweak_ptr = [&](uint64_t i) -> const uint8_t* {
+    if (c.tweak_offsets) return c.tweak_data + c.tweak_offsets[c.tweak_offset + i];
+    return c.tweak_data + (c.tweak_offset + i) * (uint64_t)c.tweak_fixed_width;
+  };
+  const int32_t* lo = c.list_offsets + c.list_offset;
+  // the run is checked first: a bad tweak keeps nothing of it
+  for (uint64_t i = 0; i < n; i++) {
+    if (!row_ok(i)) continue;
+    const uint64_t sz = tweak_size(i);
+    if (sz != TWEAK_KEY_SIZE)
+      return fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %llu bytes", (unsigned long long)sz);
+    if (bit(c.list_validity, c.list_offset + i) && lo[i + 1] > lo[i] && !c.child_values)
+      return fail(CUDASP_ERR_INVALID_ARG, "pinned tables take int64 outputs (child_values)");
+  }
+  Staging& s = t->open;
+  for (uint64_t i = 0; i < n; i++) {
+    if (!row_ok(i)) continue;
+    const bool lv = bit(c.list_validity, c.list_offset + i);
+    const uint64_t len = lv ? (uint64_t)(lo[i + 1] - lo[i]) : 0;
+    if (s.n() && s.outputs.size() + len > MAX_WORDS) {  // keep u32 offsets: close the batch early
+      const int rc = seal(*t);
+      if (rc != CUDASP_OK) return rc;
+    }
+    const uint64_t num = t->appended + i;
+    if (s.n() && num != s.ord[0] + s.n()) s.dense = false;
+    s.ord.push_back(num);
+    const uint8_t* tw = tweak_ptr(i);
+    s.rows.insert(s.rows.end(), tw, tw + TWEAK_KEY_SIZE);
+    if (len) {
+      const int64_t* v = c.child_values + c.child_offset + lo[i];
+      if (!c.child_validity) {
+        s.outputs.insert(s.outputs.end(), v, v + len);
+      } else {
+        for (uint64_t k = 0; k < len; k++)
+          if (bit(c.child_validity, c.child_offset + (uint64_t)lo[i] + k)) s.outputs.push_back(v[k]);
+      }
+    }
+    s.offsets.push_back((uint32_t)s.outputs.size());
+    if (s.n() == t->batch_size) {
+      const int rc = seal(*t);
+      if (rc != CUDASP_OK) return rc;
+    }
+  }
+  t->appended += n;
+  return CUDASP_OK;
+}
+
+int cudasp_pinned_scan(cudasp_pinned_table* t, const cudasp_tf_bind_data* b, uint64_t** rows, uint64_t* count) {
+  if (!t || !b || !rows || !count) return fail(CUDASP_ERR_INVALID_ARG, "null argument");
+  *rows = nullptr;
+  *count = 0;
+  std::lock_guard<std::mutex> lk(t->mu);
+  if (t->abandoned) return fail(CUDASP_ERR_HIP, "pinned table: a scan's kernel is still running");
+  if (b->opt.full_x) return fail(CUDASP_ERR_INVALID_ARG, "pinned tables do not take full_x outputs");
+  const double t0 = now_s();
+  int rc = seal(*t);
+  if (rc != CUDASP_OK) return rc;
+  const auto* scan = (const uint8_t*)b->scan_private_key_data.data();
+  const auto* spend = (const uint8_t*)b->spend_public_key_data.data();
+  const auto* labels = (const uint8_t*)b->label_keys_flat.data();
+  const auto nlabels = (uint32_t)b->label_keys_data.size();
+  const Shape shape{nlabels, b->opt.output_count, b->opt.label_negation ? 1u : 0u};
+  const bool fresh = !t->stream_ok || !(shape == t->shape);
+  const size_t nl = t->devices.size();
+  // one scanner and streaming kernel per logical GPU, kept and rebound to
+  // each scan's keys (creating them costs milliseconds; a 1M-row scan ~6 ms)
+  for (size_t lg = 0; lg < nl; lg++) {
+    DeviceSet ds(t->devices[lg]);
+    if (!t->scanners[lg]) {
+      rc = cudasp_scanner_create(t->devices[lg], scan, spend, labels, nlabels,
+                                 std::max<uint64_t>(1, std::min<uint64_t>(t->batch_size, CUDASP_TF_DEFAULT_BATCH)),
+                                 &t->scanners[lg]);
+    } else {
+      rc = cudasp_scanner_set_keys(t->scanners[lg], scan, spend, labels, nlabels);
+    }
+    if (rc == CUDASP_OK) rc = cudasp_scanner_set_options(t->scanners[lg], &b->opt);
+    if (rc != CUDASP_OK) {
+      t->stream_ok = false;
+      return rc;  // the scanner call's message
+    }
+    if (!cudasp_stream_supported(t->scanners[lg])) {
+      t->stream_ok = false;
+      return fail(CUDASP_ERR_INVALID_ARG, "pinned table: the streaming scan cannot run %u label keys", nlabels);
+    }
+    // a stream is sized (scratch, grid) for its scanner's label count and
+    // output indices when created: a new one when they change
+    if (fresh || !t->streams[lg]) {
+      if (t->streams[lg]) {
+        cudasp_stream_destroy(t->streams[lg]);
+        t->streams[lg] = nullptr;
+      }
+      rc = cudasp_stream_create(t->scanners[lg], t->blocks[lg], &t->streams[lg]);
+      if (rc != CUDASP_OK) {
+        t->streams[lg] = nullptr;
+        t->stream_ok = false;
+        return rc;
+      }
+    }
+  }
+  t->shape = shape;
+  t->stream_ok = false;  // until this scan finishes
+  std::vector<uint64_t> hits;
+  std::vector<std::deque<std::pair<size_t, uint64_t>>> pend(nl);  // (batch, seq) in publish order
+  std::string msg;
+  // a done batch's matches: the count is readable until 64 more batches are
+  // published on its stream, the row indices stay in its buffer
+  auto collect = [&](size_t lg) -> int {
+    const auto [j, seq] = pend[lg].front();
+    pend[lg].pop_front();
+    cudasp_stream* st = t->streams[lg];
+    int r = cudasp_stream_wait(st, seq);
+    uint32_t m = 0;
+    if (r == CUDASP_OK) r = cudasp_stream_matches(st, seq, &m);
+    if (r != CUDASP_OK) return r;
+    const Batch& bt = t->batches[j];
+    if (m > bt.n) return fail(CUDASP_ERR_HIP, "pinned table: batch %zu reports %u matches of %u rows", j, m, bt.n);
+    for (uint32_t k = 0; k < m; k++) {
+      if (bt.matches[k] >= bt.n)
+        return fail(CUDASP_ERR_HIP, "pinned table: batch %zu reports row %u of %u", j, bt.matches[k], bt.n);
+      hits.push_back(bt.number(bt.matches[k]));
+    }
+    return CUDASP_OK;
+  };
+  for (size_t j = 0; j < t->batches.size() && rc == CUDASP_OK; j++) {
+    const Batch& bt = t->batches[j];
+    DeviceSet ds(t->devices[bt.lg]);
+    if (pend[bt.lg].size() >= STREAM_RING) rc = collect(bt.lg);
+    if (rc != CUDASP_OK) break;
+    cudasp_stream_batch sb{};
+    sb.tweak_keys = bt.rows;
+    sb.outputs = bt.outputs;
+    sb.output_offsets = bt.offsets;
+    sb.output_lengths = nullptr;  // Arrow offsets: n + 1
+    sb.n = bt.n;
+    sb.match_rows = bt.matches;
+    sb.d_mirror = bt.d_mirror;
+    uint64_t seq = 0;
+    rc = cudasp_stream_publish_batch(t->streams[bt.lg], &sb, &seq);
+    if (rc == CUDASP_OK) pend[bt.lg].emplace_back(j, seq);
+  }
+  for (size_t lg = 0; lg < nl && rc == CUDASP_OK; lg++) {
+    DeviceSet ds(t->devices[lg]);
+    rc = cudasp_stream_close(t->streams[lg]);
+  }
+  const double t_pub = now_s();
+  for (size_t lg = 0; lg < nl && rc == CUDASP_OK; lg++) {
+    DeviceSet ds(t->devices[lg]);
+    while (!pend[lg].empty() && rc == CUDASP_OK) rc = collect(lg);
+    if (rc == CUDASP_OK) rc = cudasp_stream_finish(t->streams[lg]);  // reset for the next scan
+  }
+  if (rc != CUDASP_OK) {
+    msg = cudasp_last_error();
+    reset_streams(*t);
+    return fail(rc, "%s", msg.c_str());
+  }
+  t->stream_ok = true;
+  std::sort(hits.begin(), hits.end());
+  auto* out = (uint64_t*)malloc(std::max<size_t>(1, hits.size()) * sizeof(uint64_t));
+  if (!out) return fail(CUDASP_ERR_CAPACITY, "pinned table: %zu result rows: allocation failed", hits.size());
+  if (!hits.empty()) memcpy(out, hits.data(), hits.size() * sizeof(uint64_t));
+  *rows = out;
+  *count = hits.size();
+  t->last_matches = hits.size();
+  t->last_publish_s = t_pub - t0;
+  t->last_scan_s = now_s() - t0;
+  return CUDASP_OK;
+}
+
+void cudasp_pinned_free_rows(uint64_t* rows) { free(rows); }
+
+int cudasp_pinned_info(const cudasp_pinned_table* t, cudasp_pinned_info_t* out) {
+  if (!t || !out) return fail(CUDASP_ERR_INVALID_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(t->mu);
+  out->rows_appended = t->appended;
+  out->rows_pinned = t->pinned_rows + t->open.n();
+  out->batches = t->batches.size() + (t->open.n() ? 1 : 0);
+  out->pinned_bytes = t->pinned_bytes;
+  out->last_matches = t->last_matches;
+  out->last_scan_s = t->last_scan_s;
+  out->last_publish_s = t->last_publish_s;
+  return CUDASP_OK;
+}
+
+void cudasp_pinned_free(cudasp_pinned_table* t) {
+  if (!t) return;
+  {
+    std::lock_guard<std::mutex> lk(t->mu);
+    if (t->abandoned) return;  // its kernel may still read the batches
+    for (size_t lg = 0; lg < t->streams.size(); lg++) {
+      if (t->streams[lg]) {
+        DeviceSet ds(t->devices[lg]);
+        cudasp_stream_destroy(t->streams[lg]);
+      }
+      if (t->scanners[lg]) cudasp_scanner_destroy(t->scanners[lg]);
+    }
+    for (Batch& bt : t->batches) free_batch(bt);
+  }
+  delete t;
+}
+
+}  // extern "C"

@@ -6,6 +6,6 @@ the C ABI in ``include/cudasp_abi.h``, table-function host behind
 """
 from ._native import CudaspError, load as load_native  # noqa: F401
 from .scanner import HostBuffer, Scanner, ScanStream, StreamBatch  # noqa: F401
-from .pinned import PinnedTable  # noqa: F401
+from .pinned import NativePinnedTable, PinnedTable  # noqa: F401
 from .table_function import (BoundScan, assign_gpu, InvalidInputException, cudasp_scan, cudasp_scan_arrow, pool_size,  # noqa: F401
                              release_pool)

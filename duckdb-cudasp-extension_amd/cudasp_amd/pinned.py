@@ -109,15 +109,7 @@ class PinnedTable:
     def __init__(self, data, batch_size=None, device=0, devices=None):
         import pyarrow as pa
         import torch
-        # the bind's batch_size rules and messages (CudaspScanBind :474-487)
-        if batch_size is None:
-            batch_size = 300000
-        elif not isinstance(batch_size, int) or isinstance(batch_size, bool):
-            raise InvalidInputException("batch_size parameter must be an INTEGER")
-        elif batch_size <= 0:
-            raise InvalidInputException("batch_size must be positive, got %d" % batch_size)
-        elif batch_size > 10_000_000:
-            raise InvalidInputException("batch_size too large (max 10,000,000), got %d" % batch_size)
+        batch_size = _batch_size_arg(batch_size)
         t = _table(data)
         if t.num_columns < 4:
             raise InvalidInputException("cudasp_scan needs the columns (txid, height, tweak_key, outputs)")
@@ -253,6 +245,110 @@ class PinnedTable:
             for k in ("rows", "outputs", "offsets", "matches"):
                 b[k].close()
         self.batches = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def _batch_size_arg(batch_size):
+    """The bind's batch_size rules and messages (CudaspScanBind :474-487)."""
+    if batch_size is None:
+        return 300000
+    if not isinstance(batch_size, int) or isinstance(batch_size, bool):
+        raise InvalidInputException("batch_size parameter must be an INTEGER")
+    if batch_size <= 0:
+        raise InvalidInputException("batch_size must be positive, got %d" % batch_size)
+    if batch_size > 10_000_000:
+        raise InvalidInputException("batch_size too large (max 10,000,000), got %d" % batch_size)
+    return batch_size
+
+
+class NativePinnedTable:
+    """PinnedTable on the C pinned-table ABI (include/cudasp_host.h,
+    cudasp_pinned_*; csrc/host/pinned_table.cpp): the rows reach pinned memory
+    through cudasp_pinned_append (Arrow buffers, bulk reads, the
+    table-function host's row semantics) and each scan's publish / harvest
+    loop runs in C++.  Same constructor, scan(), last_stats and close() as
+    PinnedTable; what a DuckDB host would call beside cudasp_scan."""
+
+    def __init__(self, data, batch_size=None, device=0, devices=None, piece_rows=1 << 20):
+        import ctypes
+
+        from . import _native
+        from .table_function import _arrow_pieces, _columns, _lib
+        self.batch_size = _batch_size_arg(batch_size)
+        t = _table(data)
+        if t.num_columns < 4:
+            raise InvalidInputException("cudasp_scan needs the columns (txid, height, tweak_key, outputs)")
+        self.txid, self.height, self.tweak = (t.column(i).combine_chunks() if t.column(i).num_chunks != 1
+                                              else t.column(i).chunk(0) for i in range(3))
+        self.n = t.num_rows
+        self.devices = [int(d) for d in (devices if devices else [device])]
+        lib = self._lib = _lib()
+        h = ctypes.c_void_p()
+        devs = (ctypes.c_int * len(self.devices))(*self.devices)
+        _native.check(lib.cudasp_pinned_create(self.batch_size, devs, len(self.devices), ctypes.byref(h)))
+        self._h = h
+        try:
+            for piece in _arrow_pieces(t, piece_rows):  # row numbers: positions in t
+                cols = _columns(*piece)
+                _native.check(lib.cudasp_pinned_append(h, ctypes.byref(cols)))
+        except Exception:
+            self.close()
+            raise
+        self.last_stats = None
+
+    def info(self):
+        import ctypes
+
+        from . import _native
+        from .table_function import _PinnedInfo
+        st = _PinnedInfo()
+        _native.check(self._lib.cudasp_pinned_info(self._h, ctypes.byref(st)))
+        return {name: getattr(st, name) for name, _ in _PinnedInfo._fields_}
+
+    def scan_rows(self, scan_private_key, spend_public_key, label_keys, output_count=None, label_negation=None):
+        """The matching rows' numbers (positions in the table), ascending."""
+        import ctypes
+
+        from . import _native
+        bound = BoundScan(scan_private_key, spend_public_key, label_keys, self.batch_size,
+                          output_count=output_count, label_negation=label_negation)
+        rows = ctypes.POINTER(ctypes.c_uint64)()
+        count = ctypes.c_uint64()
+        _native.check(self._lib.cudasp_pinned_scan(self._h, bound._h, ctypes.byref(rows), ctypes.byref(count)))
+        try:
+            idx = np.ctypeslib.as_array(rows, (count.value,)).astype(np.int64) if count.value else \
+                np.zeros(0, dtype=np.int64)
+        finally:
+            self._lib.cudasp_pinned_free_rows(rows)
+        return idx
+
+    def scan(self, scan_private_key, spend_public_key, label_keys, output_count=None, label_negation=None):
+        """As PinnedTable.scan: a pyarrow Table (txid, height, tweak_key)."""
+        import pyarrow as pa
+        t0 = time.perf_counter()
+        idx = self.scan_rows(scan_private_key, spend_public_key, label_keys, output_count, label_negation)
+        t1 = time.perf_counter()
+        ia = pa.array(idx, type=pa.int64())
+        out = pa.table({"txid": self.txid.take(ia).cast(pa.binary()), "height": self.height.take(ia),
+                        "tweak_key": self.tweak.take(ia).cast(pa.binary())})
+        inf = self.info()
+        self.last_stats = dict(rows=self.n, batches=inf["batches"], matches=int(idx.size), scan_s=t1 - t0,
+                               native_scan_s=inf["last_scan_s"], publish_s=inf["last_publish_s"],
+                               tx_per_s=self.n / (t1 - t0) if t1 > t0 else 0.0)
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.cudasp_pinned_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
 
     def __enter__(self):
         return self

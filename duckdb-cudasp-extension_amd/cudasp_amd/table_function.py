@@ -104,6 +104,19 @@ class _Stats(ctypes.Structure):
     ]
 
 
+class _PinnedInfo(ctypes.Structure):
+    """cudasp_pinned_info_t (include/cudasp_host.h)."""
+    _fields_ = [
+        ("rows_appended", ctypes.c_uint64),
+        ("rows_pinned", ctypes.c_uint64),
+        ("batches", ctypes.c_uint64),
+        ("pinned_bytes", ctypes.c_uint64),
+        ("last_matches", ctypes.c_uint64),
+        ("last_scan_s", ctypes.c_double),
+        ("last_publish_s", ctypes.c_double),
+    ]
+
+
 def _read_stats(lib, g, stats):
     """Fill the dict `stats` from cudasp_tf_get_stats (after the last final)."""
     if stats is None:
@@ -136,6 +149,14 @@ _HOST_SIGNATURES = {
     "cudasp_tf_final": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Output)]),
     "cudasp_tf_function_columns": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Columns)]),
     "cudasp_tf_get_stats": (ctypes.c_int, [_P, ctypes.POINTER(_Stats)]),
+    "cudasp_pinned_create": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_int), ctypes.c_uint32,
+                                            ctypes.POINTER(_P)]),
+    "cudasp_pinned_append": (ctypes.c_int, [_P, ctypes.POINTER(_Columns)]),
+    "cudasp_pinned_scan": (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                          ctypes.POINTER(ctypes.c_uint64)]),
+    "cudasp_pinned_free_rows": (None, [ctypes.POINTER(ctypes.c_uint64)]),
+    "cudasp_pinned_info": (ctypes.c_int, [_P, ctypes.POINTER(_PinnedInfo)]),
+    "cudasp_pinned_free": (None, [_P]),
 }
 
 _host = None

@@ -238,6 +238,65 @@ typedef struct {
  * CUDASP_TF_HAVE_MORE_OUTPUT (1), or a negative error code. */
 int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l, cudasp_tf_output* out);
 
+/* Pinned tables (no reference counterpart: the reference copies every row of
+ * every query into per-thread strings and managed buffers,
+ * src/cudasp_extension.cu:188-223, 327-337).  A tweak table is static while
+ * wallets come and go: a pinned table copies its rows ONCE into coherent
+ * pinned host memory (cudasp_host_alloc), batched and laid out as the
+ * streaming kernel reads them (64-byte tweak blobs, int64 outputs with Arrow
+ * list offsets), and every scan publishes those batches in place to one
+ * persistent k_scan_stream per GPU -- no host copy per query.
+ *
+ *   cudasp_pinned_create  batch_size rows per batch (0 = 300000; at most
+ *                        10,000,000, CUDASP_ERR_INVALID_ARG otherwise);
+ *                        devices: the HIP device of each logical GPU (NULL =
+ *                        {0}); batch k goes to logical GPU k mod
+ *                        device_count, round-robin like the reference's
+ *                        threads over its GPUs (src/cudasp_extension.cu:523-529);
+ *                        a device listed m times runs m streaming kernels on
+ *                        1/m of its wave slots each.
+ *   cudasp_pinned_append  one run of rows (cudasp_tf_columns, int64 outputs;
+ *                        not full_x), numbered after the rows appended before
+ *                        (skipped rows keep their numbers).  The rows'
+ *                        semantics are cudasp_tf_function_columns's: a NULL
+ *                        txid, height or tweak skips the row, a tweak of
+ *                        another size than 64 bytes fails the whole run
+ *                        (nothing of it is kept), a NULL list has no outputs,
+ *                        NULL elements are dropped.  A batch is closed (copied
+ *                        into pinned memory) at batch_size rows, or earlier
+ *                        when its outputs would pass 2^32 words.  Not while a
+ *                        scan of the same table runs.
+ *   cudasp_pinned_scan   cudasp_scan over every appended row with the bound
+ *                        keys and options of b (cudasp_tf_bind and
+ *                        cudasp_tf_bind_options; full_x is
+ *                        CUDASP_ERR_INVALID_ARG, as are label counts the
+ *                        streaming scan cannot hold).  *rows receives the
+ *                        numbers of the matching rows, ascending (free with
+ *                        cudasp_pinned_free_rows), *count their count.  Scans
+ *                        of one table run one at a time (a lock); scanners and
+ *                        streaming kernels are kept and rebound between scans.
+ *   cudasp_pinned_info   rows appended, rows pinned (non-skipped), batches,
+ *                        pinned bytes, and the last scan's seconds.
+ *   cudasp_pinned_free   frees the table (a table whose last scan timed out
+ *                        with a kernel still running keeps its memory).
+ * Errors: negative CUDASP_ERR_* codes with the message in cudasp_last_error(). */
+typedef struct cudasp_pinned_table cudasp_pinned_table;
+typedef struct {
+  uint64_t rows_appended;
+  uint64_t rows_pinned;
+  uint64_t batches;
+  uint64_t pinned_bytes;
+  uint64_t last_matches;
+  double last_scan_s;    /* the whole cudasp_pinned_scan call */
+  double last_publish_s; /* until every batch was published */
+} cudasp_pinned_info_t;
+int cudasp_pinned_create(uint64_t batch_size, const int* devices, uint32_t device_count, cudasp_pinned_table** out);
+int cudasp_pinned_append(cudasp_pinned_table* t, const cudasp_tf_columns* cols);
+int cudasp_pinned_scan(cudasp_pinned_table* t, const cudasp_tf_bind_data* b, uint64_t** rows, uint64_t* count);
+void cudasp_pinned_free_rows(uint64_t* rows);
+int cudasp_pinned_info(const cudasp_pinned_table* t, cudasp_pinned_info_t* out);
+void cudasp_pinned_free(cudasp_pinned_table* t);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,3 +37,20 @@ def test_blob64_types_and_errors():
         assert (_blob64(a.slice(2, 2))[:, 0] == [2, 3]).all()
     with pytest.raises(CudaspError, match="64 bytes"):
         _blob64(pa.array([bytes(64), bytes(63)], pa.binary()))
+
+
+def test_native_pinned_table_fails_loudly_without_a_device():
+    """The C pinned table (cudasp_pinned_create) checks batch_size like the
+    bind and needs a GPU: no CPU fallback."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    from cudasp_amd import CudaspError, InvalidInputException, NativePinnedTable, _native
+    tbl = pa.table({"txid": pa.array([b"t"]), "height": pa.array([1], pa.int32()),
+                    "tweak_key": pa.array([bytes(64)]), "outputs": pa.array([[1]], pa.list_(pa.int64()))})
+    for bs, msg in ((0, "positive"), (10_000_001, "too large"), ("7", "INTEGER")):
+        with pytest.raises(InvalidInputException, match=msg):
+            NativePinnedTable(tbl, batch_size=bs)
+    with pytest.raises(CudaspError) as e:
+        NativePinnedTable(tbl)
+    assert e.value.code == _native.CUDASP_ERR_NO_DEVICE

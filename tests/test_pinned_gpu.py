@@ -4,7 +4,9 @@ list offsets (cudasp_stream_batch.output_lengths NULL) -- gives exactly
 cudasp_scan_arrow's rows: the SQL file's queries, NULL rules and slices,
 batch sizes that wrap the 64-entry descriptor ring, repeated scans of one
 pinned table with different keys, the protocol variants, and the reference's
-tweak-length error."""
+tweak-length error.  Every test runs on both implementations: PinnedTable
+(Python publish loop) and NativePinnedTable (the C ABI cudasp_pinned_*,
+csrc/host/pinned_table.cpp, fed Arrow runs through cudasp_pinned_append)."""
 import pytest
 
 import golden_io
@@ -21,24 +23,34 @@ def gpu():
         pytest.skip("no GPU")
 
 
+@pytest.fixture(params=["PinnedTable", "NativePinnedTable"])
+def cls(request):
+    import cudasp_amd
+    return getattr(cudasp_amd, request.param)
+
+
+def _nbatches(pt):
+    return pt.info()["batches"] if hasattr(pt, "info") else len(pt.batches)
+
+
 def _keys(q):
     return bytes.fromhex(q["scan_key"]), bytes.fromhex(q["spend_key"]), [bytes.fromhex(l) for l in q["label_keys"]]
 
 
-def test_sql_file_pinned(gpu):
-    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+def test_sql_file_pinned(gpu, cls):
+    from cudasp_amd import cudasp_scan_arrow
     sc = golden_io.load("sql_cases.json")
     for q in sc["queries"]:
         tbl = _arrow(_sql_table(sc, q))
-        with PinnedTable(tbl, batch_size=q["batch_size"]) as pt:
+        with cls(tbl, batch_size=q["batch_size"]) as pt:
             out = pt.scan(*_keys(q))
         assert _rows(out) == _rows(cudasp_scan_arrow(tbl, *_keys(q), batch_size=q["batch_size"])), q["line"]
         got = [out.num_rows] if q["select"] == "count" else sorted(out.column("height").to_pylist())
         assert got == q["expected"], (q["line"], got)
 
 
-def test_nulls_slices_types(gpu):
-    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+def test_nulls_slices_types(gpu, cls):
+    from cudasp_amd import cudasp_scan_arrow
     sc = golden_io.load("sql_cases.json")
     q = sc["queries"][2]
     r = [x for x in sc["tables"]["test_data"] if x["height"] == 200][0]
@@ -54,18 +66,18 @@ def test_nulls_slices_types(gpu):
                 continue
             tbl = _arrow(rows, tweak_type, large)
             for t in (tbl, tbl.slice(37, 250)):
-                with PinnedTable(t, batch_size=64) as pt:
+                with cls(t, batch_size=64) as pt:
                     assert _rows(pt.scan(*keys)) == _rows(cudasp_scan_arrow(t, *keys))
-    with PinnedTable(_arrow([]), batch_size=10) as pt:
+    with cls(_arrow([]), batch_size=10) as pt:
         assert pt.scan(*keys).num_rows == 0
 
 
 @pytest.mark.parametrize("batch_size", [1, 37, 2048, 300000])
-def test_batches_ring_and_repeated_scans(gpu, batch_size):
+def test_batches_ring_and_repeated_scans(gpu, cls, batch_size):
     """5120 random rows with planted base and label matches: at batch_size 1
     and 37 more than 64 batches pass the descriptor ring; one pinned table is
     scanned again with other keys and again with the first ones."""
-    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+    from cudasp_amd import cudasp_scan_arrow
     rr = golden_io.load("random_rows.json")
     rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
     tbl = _arrow(rows * 40 if batch_size > 1 else rows * 2)
@@ -74,48 +86,74 @@ def test_batches_ring_and_repeated_scans(gpu, batch_size):
     want1 = _rows(cudasp_scan_arrow(tbl, *k1))
     want2 = _rows(cudasp_scan_arrow(tbl, *k2))
     assert want1 and want1 != want2
-    with PinnedTable(tbl, batch_size=batch_size) as pt:
+    with cls(tbl, batch_size=batch_size) as pt:
         assert _rows(pt.scan(*k1)) == want1
         assert _rows(pt.scan(*k2)) == want2
         assert _rows(pt.scan(*k1)) == want1
-        assert pt.last_stats["matches"] == len(want1) and pt.last_stats["batches"] == len(pt.batches)
+        assert pt.last_stats["matches"] == len(want1) and pt.last_stats["batches"] == _nbatches(pt)
 
 
-def test_variants(gpu):
-    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+def test_variants(gpu, cls):
+    from cudasp_amd import cudasp_scan_arrow
     rr = golden_io.load("random_rows.json")
     rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
     tbl = _arrow(rows * 4)
     keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
-    with PinnedTable(tbl, batch_size=100) as pt:
+    with cls(tbl, batch_size=100) as pt:
         for oc, neg in ((2, None), (8, True), (None, True)):
             want = _rows(cudasp_scan_arrow(tbl, *keys, batch_size=100, output_count=oc, label_negation=neg))
             assert _rows(pt.scan(*keys, output_count=oc, label_negation=neg)) == want, (oc, neg)
 
 
-def test_errors(gpu):
-    from cudasp_amd import CudaspError, InvalidInputException, PinnedTable
+def test_errors(gpu, cls):
+    from cudasp_amd import CudaspError, InvalidInputException
     rr = golden_io.load("random_rows.json")
     with pytest.raises(CudaspError, match="64 bytes"):
-        PinnedTable(_arrow([(b"t", 1, bytes.fromhex(rr["rows"][0]["tweak"]), [1]), (b"u", 2, b"\x01" * 63, [1])]))
+        cls(_arrow([(b"t", 1, bytes.fromhex(rr["rows"][0]["tweak"]), [1]), (b"u", 2, b"\x01" * 63, [1])]))
     rows = [(b"t", 1, bytes.fromhex(rr["rows"][0]["tweak"]), [1])]
-    with PinnedTable(_arrow(rows)) as pt:
+    with cls(_arrow(rows)) as pt:
         with pytest.raises(InvalidInputException):
             pt.scan(b"\x01" * 31, bytes.fromhex(rr["spend_key"]), [])
 
 
 @pytest.mark.parametrize("devices,batch_size", [([0, 0], 37), ([0, 0, 0], 2048)])
-def test_logical_gpus(gpu, devices, batch_size):
+def test_logical_gpus(gpu, cls, devices, batch_size):
     """Batches round-robin over 2 or 3 logical GPUs on the one card (each its
     own scanner and streaming kernel on a share of the wave slots; at
     batch_size 37 each stream's 64-entry ring wraps): the rows of one GPU."""
-    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+    from cudasp_amd import cudasp_scan_arrow
     rr = golden_io.load("random_rows.json")
     rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
     tbl = _arrow(rows * 40)
     keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
     want = _rows(cudasp_scan_arrow(tbl, *keys))
-    with PinnedTable(tbl, batch_size=batch_size, devices=devices) as pt:
-        assert {b["lg"] for b in pt.batches} == set(range(len(devices)))
+    with cls(tbl, batch_size=batch_size, devices=devices) as pt:
+        if hasattr(pt, "batches"):
+            assert {b["lg"] for b in pt.batches} == set(range(len(devices)))
+        else:
+            assert pt.info()["batches"] >= len(devices)
         assert _rows(pt.scan(*keys)) == want
         assert _rows(pt.scan(*keys[:2], [])) == _rows(cudasp_scan_arrow(tbl, *keys[:2], []))
+
+
+@pytest.mark.parametrize("piece_rows", [1, 37, 5000])
+def test_native_runs_and_numbers(gpu, piece_rows):
+    """The C table takes the rows as many appended runs (batches span runs;
+    NULL rows skipped but numbered): scan_rows gives the matching rows'
+    positions in the input, ascending, as the oracle-pinned Arrow path finds
+    them."""
+    from cudasp_amd import NativePinnedTable, cudasp_scan_arrow
+    rr = golden_io.load("random_rows.json")
+    rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
+    rows = [r if i % 7 else (None,) + r[1:] for i, r in enumerate(rows * 2)]  # every 7th row skipped
+    tbl = _arrow(rows)
+    keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
+    want = _rows(cudasp_scan_arrow(tbl, *keys, batch_size=500))
+    with NativePinnedTable(tbl, batch_size=500, piece_rows=piece_rows) as pt:
+        idx = pt.scan_rows(*keys)
+        inf = pt.info()
+    assert idx.tolist() == sorted(set(idx.tolist())) and all(i % 7 for i in idx.tolist())
+    assert inf["rows_appended"] == len(rows) and inf["rows_pinned"] == len(rows) - len(range(0, len(rows), 7))
+    assert inf["batches"] == -(-inf["rows_pinned"] // 500) and inf["last_matches"] == len(idx)
+    got = _rows(tbl.take(__import__("pyarrow").array(idx)).select([0, 1, 2]))
+    assert got == want

@@ -33,12 +33,13 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--probe", action="store_true", help="diagnosis: scan the last batch alone two ways")
     ap.add_argument("--devices", default="0", help="GPUs of the scans, e.g. 0,1,2,3 (batches round-robin)")
+    ap.add_argument("--native", action="store_true", help="the C pinned table (NativePinnedTable, cudasp_pinned_*)")
     a = ap.parse_args()
     import pyarrow as pa
     import torch
 
     import bench
-    from cudasp_amd import PinnedTable, _native, assign_gpu
+    from cudasp_amd import NativePinnedTable, PinnedTable, _native, assign_gpu
     lib = _native.load()
     device = 0
     torch.cuda.set_device(device)
@@ -81,7 +82,7 @@ def main():
     t_build = time.perf_counter() - t0
     t0 = time.perf_counter()
     devices = [int(x) for x in a.devices.split(",")]
-    pt = PinnedTable(table, batch_size=a.batch_size, devices=devices)
+    pt = (NativePinnedTable if a.native else PinnedTable)(table, batch_size=a.batch_size, devices=devices)
     t_pin = time.perf_counter() - t0
     scans = []
     for r in range(a.reps + 1):  # the first scan warms the process (tables, scratch)
@@ -102,14 +103,14 @@ def main():
         from cudasp_amd import cudasp_scan_arrow
         r0 = (a.rows - 1) // a.batch_size * a.batch_size
         sl = table.slice(r0)
-        with PinnedTable(sl, batch_size=a.batch_size) as p2:
+        with (NativePinnedTable if a.native else PinnedTable)(sl, batch_size=a.batch_size) as p2:
             n_pinned = p2.scan(bench.SCAN_KEY, bench.SPEND_KEY, labels).num_rows
         n_arrow = cudasp_scan_arrow(sl, bench.SCAN_KEY, bench.SPEND_KEY, labels, batch_size=a.batch_size).num_rows
         print(json.dumps(dict(probe_last_batch_rows=a.rows - r0, pinned=n_pinned, arrow=n_arrow)), flush=True)
     timed = scans[1:]
     med = float(np.median([s["scan_s"] for s in timed]))
     res = dict(what="PinnedTable.scan: pinned host table scanned in place (one streaming kernel, no host copies)",
-               rows=a.rows, batch_size=a.batch_size, labels=a.labels, outputs_max=a.outputs_max, devices=devices,
+               rows=a.rows, batch_size=a.batch_size, native=a.native, labels=a.labels, outputs_max=a.outputs_max, devices=devices,
                expected=expected, exact=all(s["exact"] for s in scans), build_s=round(t_build, 2),
                pin_s=round(t_pin, 2), scans=[dict(s=round(s["scan_s"], 4), tx_per_s=round(s["tx_per_s"])) for s in timed],
                tx_per_s=a.rows / med, warmup_s=round(scans[0]["scan_s"], 4),

@@ -1,4 +1,5 @@
-"""Randomized soak of cudasp_amd.PinnedTable on the GPU box (robustness only):
+"""Randomized soak of cudasp_amd.PinnedTable and NativePinnedTable (the C
+cudasp_pinned_* ABI, appended in random run sizes) on the GPU box (robustness only):
 seeded random tables built from the golden random rows (planted base and label
 matches; tests/golden/random_rows.json) -- replicated, shuffled, sliced, with
 NULL txids / heights / tweaks / lists / list elements injected, binary or
@@ -30,7 +31,7 @@ def main():
     import pyarrow as pa
 
     import golden_io
-    from cudasp_amd import PinnedTable, cudasp_scan_arrow
+    from cudasp_amd import NativePinnedTable, PinnedTable, cudasp_scan_arrow
     rr = golden_io.load("random_rows.json")
     base = [(bytes.fromhex(x["tweak"]), x["outputs"]) for x in rr["rows"]]
     scan, spend = bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"])
@@ -69,7 +70,9 @@ def main():
             tbl = tbl.slice(s0, rng.randrange(1, n - s0))
         bs = rng.choice([1, 7, 64, 500, 2048, 300000])
         devices = [0] * rng.choice([1, 1, 2, 3])
-        with PinnedTable(tbl, batch_size=bs, devices=devices) as pt:
+        native = rng.random() < 0.5
+        kw = dict(piece_rows=rng.choice([1, 97, 65536])) if native else {}
+        with (NativePinnedTable if native else PinnedTable)(tbl, batch_size=bs, devices=devices, **kw) as pt:
             for _ in range(rng.choice([1, 2, 3])):
                 L = labels[:rng.randrange(len(labels) + 1)]
                 oc = rng.choice([None, None, 2, 7])
@@ -81,7 +84,8 @@ def main():
                                                                              label_negation=neg).columns]))
                 scans += 1
                 if got != want:
-                    print(json.dumps(dict(failed=True, run=runs, rows=tbl.num_rows, batch_size=bs, devices=devices,
+                    print(json.dumps(dict(failed=True, run=runs, native=native, rows=tbl.num_rows, batch_size=bs,
+                                          devices=devices,
                                           labels=len(L), output_count=oc, label_negation=neg, got=len(got),
                                           want=len(want))), flush=True)
                     sys.exit(1)
