@@ -37,6 +37,22 @@ constexpr uint64_t MAX_BATCH = 10000000;     // CudaspScanBind's batch_size limi
 constexpr uint64_t STREAM_RING = 64;         // batches published and not yet harvested, per stream
 constexpr uint64_t MAX_WORDS = 0xFFFFFFFFu;  // a batch's outputs: u32 offsets
 
+// Test hooks, read at cudasp_pinned_create:
+//   CUDASP_TF_NULL_DEVICE=1           batches in plain host memory, no device
+//                                     call (appends testable without a GPU;
+//                                     a scan fails with CUDASP_ERR_NO_DEVICE)
+//   CUDASP_PINNED_TEST_MAX_WORDS=w    a batch's outputs capped at w words
+//                                     instead of 2^32 - 1 (the early close)
+bool env_null_device() {
+  const char* e = getenv("CUDASP_TF_NULL_DEVICE");
+  return e && atoi(e) == 1;
+}
+uint64_t env_max_words() {
+  const char* e = getenv("CUDASP_PINNED_TEST_MAX_WORDS");
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 && (uint64_t)v < MAX_WORDS ? (uint64_t)v : MAX_WORDS;
+}
+
 int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
@@ -76,6 +92,7 @@ struct Batch {
   int64_t* d_mirror = nullptr;
   int device = 0;
   uint32_t lg = 0;
+  bool host_mem = false;      // null-device table: malloc'd, no mirror
   uint64_t ord0 = 0;          // input number of row 0
   std::vector<uint64_t> ord;  // every row's input number, when rows were skipped (else ord0 + r)
   uint64_t number(uint32_t r) const { return ord.empty() ? ord0 + r : ord[r]; }
@@ -112,6 +129,8 @@ struct cudasp_pinned_table {
   bool stream_ok = false;
   Shape shape;
   bool abandoned = false;  // a scan's kernel outlived its timeout: never free what it may touch
+  bool host_only = false;  // CUDASP_TF_NULL_DEVICE
+  uint64_t max_words = MAX_WORDS;
   uint64_t last_matches = 0;
   double last_scan_s = 0, last_publish_s = 0;
   mutable std::mutex mu;
@@ -120,6 +139,14 @@ struct cudasp_pinned_table {
 namespace {
 
 void free_batch(Batch& b) {
+  if (b.host_mem) {
+    free(b.rows);
+    free(b.outputs);
+    free(b.offsets);
+    free(b.matches);
+    b = Batch();
+    return;
+  }
   if (b.d_mirror) {
     DeviceSet ds(b.device);
     (void)hipFree(b.d_mirror);
@@ -144,16 +171,26 @@ int seal(cudasp_pinned_table& t) {
   b.device = t.devices[b.lg];
   b.ord0 = s.ord[0];
   const size_t wb = std::max<size_t>(1, b.words) * sizeof(int64_t);
-  int rc = cudasp_host_alloc((void**)&b.rows, n * TWEAK_KEY_SIZE);
-  if (rc == CUDASP_OK) rc = cudasp_host_alloc((void**)&b.outputs, wb);
-  if (rc == CUDASP_OK) rc = cudasp_host_alloc((void**)&b.offsets, (n + 1) * sizeof(uint32_t));
-  if (rc == CUDASP_OK) rc = cudasp_host_alloc((void**)&b.matches, n * sizeof(uint32_t));
+  int rc = CUDASP_OK;
+  if (t.host_only) {
+    b.host_mem = true;
+    b.rows = (uint8_t*)malloc(n * TWEAK_KEY_SIZE);
+    b.outputs = (int64_t*)malloc(wb);
+    b.offsets = (uint32_t*)malloc((n + 1) * sizeof(uint32_t));
+    b.matches = (uint32_t*)malloc(n * sizeof(uint32_t));
+    if (!b.rows || !b.outputs || !b.offsets || !b.matches) rc = CUDASP_ERR_CAPACITY;
+  } else {
+    rc = cudasp_host_alloc((void**)&b.rows, n * TWEAK_KEY_SIZE);
+    if (rc == CUDASP_OK) rc = cudasp_host_alloc((void**)&b.outputs, wb);
+    if (rc == CUDASP_OK) rc = cudasp_host_alloc((void**)&b.offsets, (n + 1) * sizeof(uint32_t));
+    if (rc == CUDASP_OK) rc = cudasp_host_alloc((void**)&b.matches, n * sizeof(uint32_t));
+  }
   if (rc != CUDASP_OK) {
     free_batch(b);
     return fail(CUDASP_ERR_CAPACITY, "pinned table: host allocation for a batch of %llu rows failed",
                 (unsigned long long)n);
   }
-  {
+  if (!t.host_only) {
     DeviceSet ds(b.device);
     if (hipMalloc((void**)&b.d_mirror, wb) != hipSuccess) {
       b.d_mirror = nullptr;
@@ -206,10 +243,16 @@ int cudasp_pinned_create(uint64_t batch_size, const int* devices, uint32_t devic
     return fail(CUDASP_ERR_INVALID_ARG, "batch_size too large (max 10,000,000), got %llu",
                 (unsigned long long)batch_size);
   if (devices && device_count == 0) return fail(CUDASP_ERR_INVALID_ARG, "device_count must be positive");
+  const bool host_only = env_null_device();
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(CUDASP_ERR_NO_DEVICE, "no GPU");
+  if (host_only)
+    ndev = 1 << 16;
+  else if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(CUDASP_ERR_NO_DEVICE, "no GPU");
   auto* t = new cudasp_pinned_table();
   t->batch_size = batch_size;
+  t->host_only = host_only;
+  t->max_words = env_max_words();
   if (devices)
     t->devices.assign(devices, devices + device_count);
   else
@@ -224,6 +267,10 @@ int cudasp_pinned_create(uint64_t batch_size, const int* devices, uint32_t devic
   for (int d : t->devices) {
     const int m = (int)std::count(t->devices.begin(), t->devices.end(), d);
     int cus = 0;
+    if (host_only) {
+      t->blocks.push_back(0);
+      continue;
+    }
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || cus <= 0) cus = 256;
     t->blocks.push_back(m == 1 ? 0u : (uint32_t)(cus * 3 / m));
   }
@@ -274,7 +321,7 @@ int cudasp_pinned_append(cudasp_pinned_table* t, const cudasp_tf_columns* cols) 
     if (!row_ok(i)) continue;
     const bool lv = bit(c.list_validity, c.list_offset + i);
     const uint64_t len = lv ? (uint64_t)(lo[i + 1] - lo[i]) : 0;
-    if (s.n() && s.outputs.size() + len > MAX_WORDS) {  // keep u32 offsets: close the batch early
+    if (s.n() && s.outputs.size() + len > t->max_words) {  // keep u32 offsets: close the batch early
       const int rc = seal(*t);
       if (rc != CUDASP_OK) return rc;
     }
@@ -309,6 +356,7 @@ int cudasp_pinned_scan(cudasp_pinned_table* t, const cudasp_tf_bind_data* b, uin
   std::lock_guard<std::mutex> lk(t->mu);
   if (t->abandoned) return fail(CUDASP_ERR_HIP, "pinned table: a scan's kernel is still running");
   if (b->opt.full_x) return fail(CUDASP_ERR_INVALID_ARG, "pinned tables do not take full_x outputs");
+  if (t->host_only) return fail(CUDASP_ERR_NO_DEVICE, "pinned table without a device (CUDASP_TF_NULL_DEVICE)");
   const double t0 = now_s();
   int rc = seal(*t);
   if (rc != CUDASP_OK) return rc;

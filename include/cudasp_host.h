@@ -279,6 +279,10 @@ int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf
  *                        pinned bytes, and the last scan's seconds.
  *   cudasp_pinned_free   frees the table (a table whose last scan timed out
  *                        with a kernel still running keeps its memory).
+ * Test hooks (environment, read at create): CUDASP_TF_NULL_DEVICE=1 keeps the
+ * batches in plain host memory with no device call (scans fail with
+ * CUDASP_ERR_NO_DEVICE); CUDASP_PINNED_TEST_MAX_WORDS lowers the 2^32 - 1
+ * words at which a batch closes early. 
  * Errors: negative CUDASP_ERR_* codes with the message in cudasp_last_error(). */
 typedef struct cudasp_pinned_table cudasp_pinned_table;
 typedef struct {

@@ -54,3 +54,64 @@ def test_native_pinned_table_fails_loudly_without_a_device():
     with pytest.raises(CudaspError) as e:
         NativePinnedTable(tbl)
     assert e.value.code == _native.CUDASP_ERR_NO_DEVICE
+
+
+def _native_table(n, bad_tweak_at=None, outputs=2):
+    rows_ok = [i % 7 != 0 for i in range(n)]
+    return pa.table({
+        "txid": pa.array([bytes([i % 256]) * 32 if rows_ok[i] else None for i in range(n)], pa.binary()),
+        "height": pa.array(list(range(n)), pa.int32()),
+        "tweak_key": pa.array([bytes(63) if i == bad_tweak_at else bytes([i % 256]) * 64 for i in range(n)]),
+        "outputs": pa.array([None if i % 11 == 0 else [i] * outputs for i in range(n)], pa.list_(pa.int64())),
+    })
+
+
+@pytest.mark.parametrize("piece_rows", [1, 37, 1000])
+def test_native_pinned_appends_without_a_device(monkeypatch, piece_rows):
+    """cudasp_pinned_append's batching in the null-device mode (batches in
+    plain host memory): NULL-txid rows skipped but counted, batches closed at
+    batch_size across appended runs, and early when a batch's outputs would
+    pass the word cap (CUDASP_PINNED_TEST_MAX_WORDS; 2^32 - 1 in the
+    product); a run with a bad tweak keeps nothing; a scan fails loudly."""
+    import ctypes
+
+    from cudasp_amd import CudaspError, NativePinnedTable, _native
+    from cudasp_amd.table_function import _PinnedInfo, _arrow_pieces, _columns, _lib
+    monkeypatch.setenv("CUDASP_TF_NULL_DEVICE", "1")
+    tbl = _native_table(1000)
+    pinned = sum(1 for i in range(1000) if i % 7)
+    with NativePinnedTable(tbl, batch_size=100, piece_rows=piece_rows) as pt:
+        inf = pt.info()
+        assert inf["rows_appended"] == 1000 and inf["rows_pinned"] == pinned
+        assert inf["batches"] == -(-pinned // 100)
+        with pytest.raises(CudaspError) as e:
+            pt.scan(bytes(31) + b"\x01", bytes(64), [])
+        assert e.value.code == _native.CUDASP_ERR_NO_DEVICE
+    # early close: 2 outputs per row (none for NULL lists), at most 9 words per batch
+    monkeypatch.setenv("CUDASP_PINNED_TEST_MAX_WORDS", "9")
+    with NativePinnedTable(tbl, batch_size=100, piece_rows=piece_rows) as pt:
+        words, nb = 0, 1
+        for i in range(1000):
+            if i % 7 == 0:
+                continue
+            w = 0 if i % 11 == 0 else 2
+            if words + w > 9 and words > 0:
+                nb, words = nb + 1, 0
+            words += w
+        assert pt.info()["batches"] == nb and pt.info()["rows_pinned"] == pinned
+    monkeypatch.delenv("CUDASP_PINNED_TEST_MAX_WORDS")
+    # a bad tweak in a later run: the earlier runs stay, nothing of that run
+    with pytest.raises(CudaspError, match="64 bytes"):
+        NativePinnedTable(_native_table(300, bad_tweak_at=250), batch_size=64, piece_rows=200)
+    lib = _lib()
+    h = ctypes.c_void_p()
+    _native.check(lib.cudasp_pinned_create(64, None, 0, ctypes.byref(h)))
+    try:
+        pieces = _arrow_pieces(_native_table(300, bad_tweak_at=250), 200)
+        _native.check(lib.cudasp_pinned_append(h, ctypes.byref(_columns(*pieces[0]))))
+        assert lib.cudasp_pinned_append(h, ctypes.byref(_columns(*pieces[1]))) == _native.CUDASP_ERR_INVALID_ARG
+        inf = _PinnedInfo()
+        _native.check(lib.cudasp_pinned_info(h, ctypes.byref(inf)))
+        assert inf.rows_appended == 200 and inf.rows_pinned == sum(1 for i in range(200) if i % 7)
+    finally:
+        lib.cudasp_pinned_free(h)

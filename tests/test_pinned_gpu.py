@@ -157,3 +157,19 @@ def test_native_runs_and_numbers(gpu, piece_rows):
     assert inf["batches"] == -(-inf["rows_pinned"] // 500) and inf["last_matches"] == len(idx)
     got = _rows(tbl.take(__import__("pyarrow").array(idx)).select([0, 1, 2]))
     assert got == want
+
+
+def test_native_early_close(gpu, monkeypatch):
+    """Batches closed early by the outputs word cap (the u32-offset guard,
+    lowered by CUDASP_PINNED_TEST_MAX_WORDS): more than 64 small batches of
+    uneven row counts, the ring wrapped, rows as the Arrow path's."""
+    from cudasp_amd import NativePinnedTable, cudasp_scan_arrow
+    monkeypatch.setenv("CUDASP_PINNED_TEST_MAX_WORDS", "40")
+    rr = golden_io.load("random_rows.json")
+    rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
+    tbl = _arrow(rows * 8)
+    keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
+    with NativePinnedTable(tbl, batch_size=1000) as pt:
+        got = _rows(pt.scan(*keys))
+        assert pt.info()["batches"] > 64
+    assert got == _rows(cudasp_scan_arrow(tbl, *keys))
