@@ -10,8 +10,11 @@ without a GPU, so the host is compiled here with the sanitizers (host code
 only: -Xarch_host), linked ahead of the in-tree library (whose own host
 symbols it interposes), and driven by tools/host_e2e --null-device
 --cpu-table: many threads, 1 and 8 feeds, row chunks and Arrow columns,
-small batches (many slot cycles), fixed and variable output lists.  Any
-sanitizer report fails the test."""
+small batches (many slot cycles), fixed and variable output lists.  The C
+pinned table (csrc/host/pinned_table.cpp) is compiled in the same way and its
+appends run under them too (host_e2e --pinned --null-device: batches in plain
+host memory, runs spanning batches, 1 to 4 logical GPUs).  Any sanitizer
+report fails the test."""
 import json
 import os
 import subprocess
@@ -41,16 +44,19 @@ def sanitized(request):
     common = [HIPCC, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", "-fno-omit-frame-pointer"] + flags
     subprocess.check_call(common + ["-fPIC", "-c", "-o", os.path.join(d, "host.o"),
                                     os.path.join(PKG, "csrc", "host", "cudasp_host.cpp")])
+    subprocess.check_call(common + ["-fPIC", "-c", "-o", os.path.join(d, "pinned.o"),
+                                    os.path.join(PKG, "csrc", "host", "pinned_table.cpp")])
     subprocess.check_call(common + ["-c", "-o", os.path.join(d, "e2e.o"), os.path.join(ROOT, "tools", "host_e2e.cpp")])
     exe = os.path.join(d, "host_e2e")
     subprocess.check_call([HIPCC, "--offload-arch=gfx950"] + flags + ["-o", exe, os.path.join(d, "e2e.o"),
-                                                                       os.path.join(d, "host.o"), "-L" + PKG,
+                                                                       os.path.join(d, "host.o"),
+                                                                       os.path.join(d, "pinned.o"), "-L" + PKG,
                                                                        "-lcudasp_amd", "-Wl,-rpath," + PKG, "-lpthread"])
     # the sanitized host is the one that runs: the executable defines the
     # host's entry points (interposing the library's) and the sanitizer runtime
     syms = subprocess.check_output(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-s", "--wide", exe], text=True)
     defined = {ln.split()[-1] for ln in syms.splitlines() if len(ln.split()) >= 8 and ln.split()[6] != "UND"}
-    assert "cudasp_tf_function" in defined and "cudasp_tf_init" in defined
+    assert "cudasp_tf_function" in defined and "cudasp_tf_init" in defined and "cudasp_pinned_append" in defined
     assert ("__tsan_init" if request.param == "thread" else "__asan_init") in defined
     return request.param, exe
 
@@ -78,3 +84,17 @@ def test_host_feeds_clean_under_sanitizers(sanitized, case):
     assert res["null_device"] is True and res["emitted_equal_planted"] is True  # null device: nothing emitted
     assert res["feeds"] == len(dmap.split(","))
     assert res["launches"] >= 150000 // batch
+
+
+@pytest.mark.parametrize("devices,batch,outs", [("0", 4096, ["--outputs-max", "7"]), ("0,0,0,0", 70000, ["--outputs", "2"])])
+def test_pinned_appends_clean_under_sanitizers(sanitized, devices, batch, outs):
+    name, exe = sanitized
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:report_signal_unsafe=0",
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe, "--null-device", "--cpu-table", "--rows", "150000", "--batch", str(batch),
+                        "--pinned", devices] + outs, capture_output=True, text=True, timeout=600, env=env)
+    assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, (name, r.stderr[-4000:])
+    assert r.returncode == 0, (name, r.returncode, r.stderr[-2000:])
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["null_device"] is True and res["rows_pinned"] == 150000
+    assert res["batches"] == -(-150000 // batch) and res["devices"] == [int(x) for x in devices.split(",")]

@@ -23,6 +23,7 @@
 //            [--outputs K | --outputs-max KMAX] [--input rows|columns]
 //            [--reps R] [--warm-reps W [--warm-ms MS]] [--plant-sample FILE]
 //            [--null-device [--cpu-table]] [--output-count K] [--label-negation]
+//            [--pinned DEVICES]
 // (W more queries, each started right after MS ms of a busy kernel on every
 // GPU: the rate at full clock, without the ramp from idle; warm_tx_per_s)
 // --plant-sample writes 256 planted rows and 256 unplanted rows, strided over
@@ -43,6 +44,13 @@
 // --output-count / --label-negation bind the protocol variants (DESIGN.md
 // section 6b); the planted values stay the reference's (output index 0, labels
 // added), which every variant still matches, and no other row may match.
+// --pinned DEVICES (e.g. 0 or 0,0,0,0): instead of table-function queries,
+// the C pinned table (cudasp_pinned_*, include/cudasp_host.h): the table is
+// appended once in 65536-row Arrow runs, then scanned R + 1 times (the first
+// warms the scanners and streams; each scan binds the keys like a query),
+// batches round-robin over DEVICES (a device listed m times: m logical GPUs
+// on it); a scan passes when its row numbers are exactly the planted rows.
+// With --null-device only the appends run (no scan).
 // Label keys: F holds L 64-byte keys (x || y, little-endian, bench.label_keys);
 // without F, L must be 0 or 1 (the SQL test's label, test/sql/cudasp.test:104).
 // Prints one JSON line; exit 0 iff every timed query emitted exactly the
@@ -112,6 +120,7 @@ struct Args {
   bool cpu_table = false;    // with null_device: table generated on the CPU, no GPU needed
   int output_count = 1;        // protocol variant: output indices per row (bind option output_count)
   bool label_negation = false;  // protocol variant: labels also negated (bind option label_negation)
+  std::vector<int> pinned;      // --pinned: the pinned table's devices (empty: table-function queries)
 };
 
 static Args parse(int argc, char** argv) {
@@ -141,6 +150,15 @@ static Args parse(int argc, char** argv) {
     else if (s == "--cpu-table") a.cpu_table = true;
     else if (s == "--output-count") a.output_count = atoi(val());
     else if (s == "--label-negation") a.label_negation = true;
+    else if (s == "--pinned") {
+      std::string v = val();
+      for (size_t p = 0; p <= v.size();) {
+        const size_t q = v.find(',', p);
+        a.pinned.push_back(atoi(v.substr(p, q == std::string::npos ? std::string::npos : q - p).c_str()));
+        if (q == std::string::npos) break;
+        p = q + 1;
+      }
+    }
     else {
       fprintf(stderr, "unknown argument %s\n", s.c_str());
       exit(1);
@@ -508,6 +526,93 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
   return q;
 }
 
+// --pinned: the C pinned table over the same rows (see the header).
+static int run_pinned(const Args& a, const uint8_t scan[32], const uint8_t spend[64],
+                      const std::vector<uint8_t>& labels, const Table& t, double gen_s) {
+  const int L = a.labels;
+  const uint64_t rows = t.rows;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto since = [](std::chrono::steady_clock::time_point x) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - x).count();
+  };
+  cudasp_pinned_table* pt;
+  CK(cudasp_pinned_create((uint64_t)a.batch, a.pinned.data(), (uint32_t)a.pinned.size(), &pt));
+  const uint64_t piece = 65536;
+  std::vector<int32_t> txo(piece + 1), lo(piece + 1);
+  for (uint64_t c0 = 0; c0 < rows; c0 += piece) {
+    const uint64_t m = std::min<uint64_t>(piece, rows - c0);
+    for (uint64_t r = 0; r <= m; r++) {
+      txo[r] = (int32_t)(r * 32);
+      lo[r] = (int32_t)((c0 + r < rows ? t.list_off[c0 + r] : t.outputs.size()) - t.list_off[c0]);
+    }
+    cudasp_tf_columns c{};
+    c.count = m;
+    c.txid_offsets = txo.data();
+    c.txid_data = t.txids.data() + c0 * 32;
+    c.height = t.heights.data() + c0;
+    c.tweak_data = t.tweaks.data() + c0 * 64;
+    c.tweak_fixed_width = 64;
+    c.list_offsets = lo.data();
+    c.child_values = t.outputs.data() + t.list_off[c0];
+    CK(cudasp_pinned_append(pt, &c));
+  }
+  const double pin_s = since(t0);
+  cudasp_pinned_info_t inf{};
+  CK(cudasp_pinned_info(pt, &inf));
+  std::vector<double> secs;
+  bool exact = true;
+  uint64_t matches = 0;
+  for (int r = 0; !a.null_device && r <= a.reps; r++) {
+    const auto s0 = std::chrono::steady_clock::now();
+    cudasp_tf_blob_arg a_scan{scan, 32, 1}, a_spend{spend, 64, 1};
+    std::vector<cudasp_tf_blob_arg> a_lab(std::max(1, L));
+    for (int j = 0; j < L; j++) a_lab[j] = {labels.data() + 64 * j, 64, 1};
+    cudasp_tf_bind_data* bd;
+    char err[512];
+    if (cudasp_tf_bind(4, a_scan, a_spend, 1, a_lab.data(), (uint32_t)L, 1, 1, a.batch, &bd, err, sizeof(err)) != 0 ||
+        ((a.output_count != 1 || a.label_negation) &&
+         cudasp_tf_bind_options(bd, 1, a.output_count, 1, a.label_negation ? 1 : 0, 0, 0, err, sizeof(err)) != 0)) {
+      fprintf(stderr, "bind: %s\n", err);
+      return 1;
+    }
+    uint64_t* got = nullptr;
+    uint64_t n = 0;
+    CK(cudasp_pinned_scan(pt, bd, &got, &n));
+    cudasp_tf_bind_free(bd);
+    const double sec = since(s0);
+    const bool ok = n == t.planted.size() && std::equal(got, got + n, t.planted.begin());
+    if (!ok) fprintf(stderr, "pinned scan %d not exact: %llu rows, %zu planted\n", r, (unsigned long long)n,
+                     t.planted.size());
+    cudasp_pinned_free_rows(got);
+    if (r > 0) {  // scan 0 warms the scanners and streams
+      secs.push_back(sec);
+      exact = exact && ok;
+      matches = n;
+    }
+  }
+  CK(cudasp_pinned_info(pt, &inf));
+  cudasp_pinned_free(pt);
+  std::vector<double> sorted = secs;
+  std::sort(sorted.begin(), sorted.end());
+  const double med = sorted.empty() ? 0.0 : sorted[sorted.size() / 2];
+  std::string all = "[", devs = "[";
+  for (size_t i = 0; i < secs.size(); i++) all += (i ? ", " : "") + std::to_string(secs[i]);
+  for (size_t i = 0; i < a.pinned.size(); i++) devs += (i ? ", " : "") + std::to_string(a.pinned[i]);
+  all += "]";
+  devs += "]";
+  printf("{\"what\": \"C pinned table (cudasp_pinned_*): appended once, scanned in place per query\", "
+         "\"rows\": %llu, \"batch_size\": %lld, \"labels\": %d, \"outputs_total\": %llu, \"devices\": %s, "
+         "\"batches\": %llu, \"rows_pinned\": %llu, \"pinned_bytes\": %llu, \"pin_s\": %.3f, "
+         "\"generate_seconds\": %.2f, \"reps\": %d, \"seconds\": %.5f, \"seconds_all\": %s, \"tx_per_s\": %.1f, "
+         "\"matches\": %llu, \"planted\": %zu, \"emitted_equal_planted\": %s, \"last_publish_s\": %.5f, "
+         "\"null_device\": %s}\n",
+         (unsigned long long)rows, (long long)a.batch, L, (unsigned long long)t.outputs.size(), devs.c_str(),
+         (unsigned long long)inf.batches, (unsigned long long)inf.rows_pinned, (unsigned long long)inf.pinned_bytes,
+         pin_s, gen_s, (int)secs.size(), med, all.c_str(), med > 0 ? rows / med : 0.0, (unsigned long long)matches,
+         t.planted.size(), exact ? "true" : "false", inf.last_publish_s, a.null_device ? "true" : "false");
+  return exact ? 0 : 1;
+}
+
 static std::string hex(const uint8_t* p, size_t n) {
   static const char* d = "0123456789abcdef";
   std::string s(2 * n, '0');
@@ -589,6 +694,7 @@ int main(int argc, char** argv) {
   Table t;
   generate(a, scan, spend, labels, t);
   const double gen_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - g0).count();
+  if (!a.pinned.empty()) return run_pinned(a, scan, spend, labels, t, gen_s);
 
   const QueryResult warm = run_query(a, scan, spend, labels, t);  // scanners, slots, tables
   std::vector<QueryResult> qs;
