@@ -49,8 +49,8 @@ flags; it also recomputes the planted values of 256 planted rows spread over
 the whole rank table, `planted_oracle_check`, and of a 256-row sample of the
 end-to-end leg's planted and unplanted rows, `e2e.planted_oracle_check`).
 The `pinned` leg scans the same table pinned once in host memory, in place
-(cudasp_amd.PinnedTable over all N GPUs, no host copy per query; DESIGN.md
-section 7e).
+(the C pinned table cudasp_pinned_* driven by tools/host_e2e --pinned, over
+all N GPUs, no host copy per query).
 `cpu_baseline` itself is the strongest CPU stand-in the image allows:
 `port-optimized` (tools/cpu_port, the product's row pipeline compiled for the
 host) where it covers the options, else the oracle port.
@@ -508,28 +508,45 @@ def host_cores():
 
 
 def pinned_leg(args, labels, world):
-    """Zero-copy scans of the same table (cudasp_amd.PinnedTable, DESIGN.md
-    section 7e): tools/pinned_bench.py as a child process builds the table,
-    copies it ONCE into pinned host memory and scans it 3 times in place over
-    all `world` GPUs (batches round-robin, one streaming kernel per GPU, no
-    host copy per query); every scan must emit exactly the planted rows."""
+    """Zero-copy scans of the same table through the C pinned table
+    (cudasp_pinned_*, include/cudasp_host.h):
+    tools/host_e2e --pinned as a child process builds the table in host
+    memory, appends it ONCE (Arrow runs) into pinned memory and scans it 4
+    times in place over all `world` GPUs (batches round-robin, one streaming
+    kernel per GPU, no host copy per query; each scan binds its keys like a
+    query); the first scan warms the scanners and streams, the median of the
+    other 3 is reported, and every scan must return exactly the planted rows."""
     import subprocess
-    cmd = [sys.executable, os.path.join(ROOT, "tools", "pinned_bench.py"), "--rows", str(args.rows), "--batch-size",
-           str(args.batch_size), "--labels", str(len(labels)), "--reps", "3",
-           "--devices", ",".join(str(r % max(1, torch.cuda.device_count())) for r in range(world))]
-    if args.outputs_max:
-        cmd += ["--outputs-max", str(args.outputs_max)]
+    import tempfile
+    exe = os.path.join(ROOT, "tools", "host_e2e")
+    if not os.path.exists(exe):
+        return dict(error="tools/host_e2e not built (make -C duckdb-cudasp-extension_amd)")
+    devices = ",".join(str(r % max(1, torch.cuda.device_count())) for r in range(world))
+    cmd = [exe, "--rows", str(args.rows), "--batch", str(args.batch_size), "--labels", str(len(labels)),
+           "--reps", "3", "--pinned", devices]
+    cmd += ["--outputs-max", str(args.outputs_max)] if args.outputs_max else ["--outputs", str(args.outputs_per_row)]
+    lf = None
+    if labels:
+        lf = tempfile.NamedTemporaryFile(prefix="cudasp_labels_", suffix=".bin", delete=False)
+        lf.write(b"".join(labels))
+        lf.close()
+        cmd += ["--labels-file", lf.name]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.e2e_timeout)
     except subprocess.TimeoutExpired:
         return dict(error="timed out after %d s" % args.e2e_timeout)
+    finally:
+        if lf is not None:
+            os.unlink(lf.name)
     line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else ""
     try:
         res = json.loads(line)
     except ValueError:
         return dict(error="exit %d: %s" % (r.returncode, (r.stderr or r.stdout)[-400:]))
-    if not res.get("diffs"):
-        res.pop("diffs", None)
+    res["exit_code"] = r.returncode
+    res["args"] = " ".join(c if c != (lf.name if lf else None) else "<label keys>" for c in cmd[1:])
+    if r.stderr.strip():
+        res["stderr_tail"] = r.stderr.strip()[-300:]
     return res
 
 
@@ -929,7 +946,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layout-probe", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--no-pinned", action="store_true", help="skip the pinned-table leg (cudasp_amd.PinnedTable)")
+    ap.add_argument("--no-pinned", action="store_true", help="skip the pinned-table leg (cudasp_pinned_*, tools/host_e2e --pinned)")
     ap.add_argument("--no-e2e-launch", action="store_true",
                     help="skip the second end-to-end leg with the host's per-slot launches (CUDASP_TF_MODE=launch)")
     ap.add_argument("--e2e-threads", type=int, default=0,
