@@ -11,6 +11,13 @@
 // their Arrow list offsets (cudasp_stream_batch.output_lengths NULL) over PCIe
 // and writes the matching row indices back.  Same algorithm as the Python
 // cudasp_amd.PinnedTable, without the interpreter in the publish loop.
+//
+// Placement CUDASP_TABLE_HBM keeps the batches resident in device memory
+// instead, in k_scan_multi's layout (tweak x / y columns, the outputs CSR with
+// per-row offsets and lengths), and a scan is one cudasp_scan_device_batches
+// launch per logical GPU over all of its batches: the device-resident rate of
+// bench.py's headline, for a table that fits in HBM (~93 B per row with 2
+// outputs; 288 GB per MI355X).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -93,6 +100,14 @@ struct Batch {
   int device = 0;
   uint32_t lg = 0;
   bool host_mem = false;      // null-device table: malloc'd, no mirror
+  // CUDASP_TABLE_HBM: the batch on its device (no pinned buffers)
+  uint32_t* d_x = nullptr;
+  uint32_t* d_y = nullptr;
+  int64_t* d_out = nullptr;
+  uint32_t* d_offs = nullptr;
+  uint32_t* d_lens = nullptr;
+  uint8_t* d_flags = nullptr;
+  uint32_t* d_rows = nullptr;
   uint64_t ord0 = 0;          // input number of row 0
   std::vector<uint64_t> ord;  // every row's input number, when rows were skipped (else ord0 + r)
   uint64_t number(uint32_t r) const { return ord.empty() ? ord0 + r : ord[r]; }
@@ -130,6 +145,10 @@ struct cudasp_pinned_table {
   Shape shape;
   bool abandoned = false;  // a scan's kernel outlived its timeout: never free what it may touch
   bool host_only = false;  // CUDASP_TF_NULL_DEVICE
+  bool hbm = false;        // CUDASP_TABLE_HBM
+  uint64_t device_bytes = 0;
+  std::vector<uint32_t*> d_counts;  // HBM: per logical GPU, one match count per batch
+  std::vector<size_t> counts_cap;
   uint64_t max_words = MAX_WORDS;
   uint64_t last_matches = 0;
   double last_scan_s = 0, last_publish_s = 0;
@@ -147,15 +166,60 @@ void free_batch(Batch& b) {
     b = Batch();
     return;
   }
-  if (b.d_mirror) {
+  if (b.d_mirror || b.d_x) {
     DeviceSet ds(b.device);
-    (void)hipFree(b.d_mirror);
+    for (void* p : {(void*)b.d_mirror, (void*)b.d_x, (void*)b.d_y, (void*)b.d_out, (void*)b.d_offs, (void*)b.d_lens,
+                    (void*)b.d_flags, (void*)b.d_rows})
+      if (p) (void)hipFree(p);
   }
   cudasp_host_free(b.rows);
   cudasp_host_free(b.outputs);
   cudasp_host_free(b.offsets);
   cudasp_host_free(b.matches);
   b = Batch();
+}
+
+void reset_staging(cudasp_pinned_table& t) {
+  Staging& s = t.open;
+  s.rows.clear();
+  s.outputs.clear();
+  s.offsets.assign(1, 0);
+  s.ord.clear();
+  s.dense = true;
+}
+
+// CUDASP_TABLE_HBM: the open batch uploaded in k_scan_multi's layout (the
+// blobs transposed on the device into x / y columns; per-row offsets and
+// lengths from the Arrow offsets).
+int seal_hbm(cudasp_pinned_table& t, Batch& b, size_t wb) {
+  Staging& s = t.open;
+  const uint64_t n = b.n;
+  DeviceSet ds(b.device);
+  std::vector<uint32_t> lens(n);
+  for (uint64_t r = 0; r < n; r++) lens[r] = s.offsets[r + 1] - s.offsets[r];
+  uint8_t* d_tmp = nullptr;
+  bool ok = hipMalloc((void**)&b.d_x, n * 32) == hipSuccess && hipMalloc((void**)&b.d_y, n * 32) == hipSuccess &&
+            hipMalloc((void**)&b.d_out, wb) == hipSuccess && hipMalloc((void**)&b.d_offs, n * 4) == hipSuccess &&
+            hipMalloc((void**)&b.d_lens, n * 4) == hipSuccess && hipMalloc((void**)&b.d_flags, n) == hipSuccess &&
+            hipMalloc((void**)&b.d_rows, n * 4) == hipSuccess && hipMalloc((void**)&d_tmp, n * TWEAK_KEY_SIZE) == hipSuccess;
+  ok = ok && hipMemcpy(d_tmp, s.rows.data(), n * TWEAK_KEY_SIZE, hipMemcpyHostToDevice) == hipSuccess &&
+       (b.words == 0 || hipMemcpy(b.d_out, s.outputs.data(), b.words * 8, hipMemcpyHostToDevice) == hipSuccess) &&
+       hipMemcpy(b.d_offs, s.offsets.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(b.d_lens, lens.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess;
+  if (ok) ok = cudasp_tweaks_to_columns(d_tmp, (uint32_t)n, b.d_x, b.d_y, nullptr) == CUDASP_OK;
+  if (ok) ok = hipDeviceSynchronize() == hipSuccess;
+  if (d_tmp) (void)hipFree(d_tmp);
+  if (!ok) {
+    free_batch(b);
+    return fail(CUDASP_ERR_HIP, "resident table: a batch of %llu rows on device %d: allocation or upload failed",
+                (unsigned long long)n, t.devices[b.lg]);
+  }
+  if (!s.dense) b.ord = s.ord;
+  t.device_bytes += n * (32 + 32 + 4 + 4 + 1 + 4) + wb;
+  t.pinned_rows += n;
+  t.batches.push_back(std::move(b));
+  reset_staging(t);
+  return CUDASP_OK;
 }
 
 // Close the open batch: copy it into pinned memory and give it its mirror on
@@ -172,6 +236,7 @@ int seal(cudasp_pinned_table& t) {
   b.ord0 = s.ord[0];
   const size_t wb = std::max<size_t>(1, b.words) * sizeof(int64_t);
   int rc = CUDASP_OK;
+  if (t.hbm && !t.host_only) return seal_hbm(t, b, wb);
   if (t.host_only) {
     b.host_mem = true;
     b.rows = (uint8_t*)malloc(n * TWEAK_KEY_SIZE);
@@ -204,13 +269,10 @@ int seal(cudasp_pinned_table& t) {
   memcpy(b.offsets, s.offsets.data(), (n + 1) * sizeof(uint32_t));
   if (!s.dense) b.ord = s.ord;
   t.pinned_bytes += n * TWEAK_KEY_SIZE + wb + (2 * n + 1) * sizeof(uint32_t);
+  t.device_bytes += wb;  // the mirror
   t.pinned_rows += n;
   t.batches.push_back(std::move(b));
-  s.rows.clear();
-  s.outputs.clear();
-  s.offsets.assign(1, 0);
-  s.ord.clear();
-  s.dense = true;
+  reset_staging(t);
   return CUDASP_OK;
 }
 
@@ -231,13 +293,146 @@ void reset_streams(cudasp_pinned_table& t) {
   t.stream_ok = false;
 }
 
+// The pinned placement's scan: every batch published in place to its logical
+// GPU's streaming kernel (at most 64 in flight per stream, harvested in
+// order); a failure finishes the streams.
+int scan_streams(cudasp_pinned_table& t, std::vector<uint64_t>& hits, double* t_pub) {
+  const size_t nl = t.devices.size();
+  int rc = CUDASP_OK;
+  t.stream_ok = false;  // until this scan finishes
+  std::vector<std::deque<std::pair<size_t, uint64_t>>> pend(nl);  // (batch, seq) in publish order
+  std::string msg;
+  // a done batch's matches: the count is readable until 64 more batches are
+  // published on its stream, the row indices stay in its buffer
+  auto collect = [&](size_t lg) -> int {
+    const auto [j, seq] = pend[lg].front();
+    pend[lg].pop_front();
+    cudasp_stream* st = t.streams[lg];
+    int r = cudasp_stream_wait(st, seq);
+    uint32_t m = 0;
+    if (r == CUDASP_OK) r = cudasp_stream_matches(st, seq, &m);
+    if (r != CUDASP_OK) return r;
+    const Batch& bt = t.batches[j];
+    if (m > bt.n) return fail(CUDASP_ERR_HIP, "pinned table: batch %zu reports %u matches of %u rows", j, m, bt.n);
+    for (uint32_t k = 0; k < m; k++) {
+      if (bt.matches[k] >= bt.n)
+        return fail(CUDASP_ERR_HIP, "pinned table: batch %zu reports row %u of %u", j, bt.matches[k], bt.n);
+      hits.push_back(bt.number(bt.matches[k]));
+    }
+    return CUDASP_OK;
+  };
+  for (size_t j = 0; j < t.batches.size() && rc == CUDASP_OK; j++) {
+    const Batch& bt = t.batches[j];
+    DeviceSet ds(t.devices[bt.lg]);
+    if (pend[bt.lg].size() >= STREAM_RING) rc = collect(bt.lg);
+    if (rc != CUDASP_OK) break;
+    cudasp_stream_batch sb{};
+    sb.tweak_keys = bt.rows;
+    sb.outputs = bt.outputs;
+    sb.output_offsets = bt.offsets;
+    sb.output_lengths = nullptr;  // Arrow offsets: n + 1
+    sb.n = bt.n;
+    sb.match_rows = bt.matches;
+    sb.d_mirror = bt.d_mirror;
+    uint64_t seq = 0;
+    rc = cudasp_stream_publish_batch(t.streams[bt.lg], &sb, &seq);
+    if (rc == CUDASP_OK) pend[bt.lg].emplace_back(j, seq);
+  }
+  for (size_t lg = 0; lg < nl && rc == CUDASP_OK; lg++) {
+    DeviceSet ds(t.devices[lg]);
+    rc = cudasp_stream_close(t.streams[lg]);
+  }
+  *t_pub = now_s();
+  for (size_t lg = 0; lg < nl && rc == CUDASP_OK; lg++) {
+    DeviceSet ds(t.devices[lg]);
+    while (!pend[lg].empty() && rc == CUDASP_OK) rc = collect(lg);
+    if (rc == CUDASP_OK) rc = cudasp_stream_finish(t.streams[lg]);  // reset for the next scan
+  }
+  if (rc != CUDASP_OK) {
+    msg = cudasp_last_error();
+    reset_streams(t);
+    return fail(rc, "%s", msg.c_str());
+  }
+  t.stream_ok = true;
+  return CUDASP_OK;
+}
+
+// The HBM placement's scan: one cudasp_scan_device_batches launch per logical
+// GPU over all of its resident batches (all launched before any is waited
+// for), then each batch's match count and rows read back.
+int scan_hbm(cudasp_pinned_table& t, std::vector<uint64_t>& hits) {
+  const size_t nl = t.devices.size();
+  std::vector<std::vector<size_t>> of(nl);  // batch indices per logical GPU
+  for (size_t j = 0; j < t.batches.size(); j++) of[t.batches[j].lg].push_back(j);
+  for (size_t lg = 0; lg < nl; lg++) {
+    if (of[lg].empty()) continue;
+    DeviceSet ds(t.devices[lg]);
+    if (t.counts_cap[lg] < of[lg].size()) {
+      if (t.d_counts[lg]) (void)hipFree(t.d_counts[lg]);
+      t.d_counts[lg] = nullptr;
+      t.counts_cap[lg] = 0;
+      if (hipMalloc((void**)&t.d_counts[lg], of[lg].size() * 4) != hipSuccess)
+        return fail(CUDASP_ERR_HIP, "resident table: match counts on device %d: allocation failed", t.devices[lg]);
+      t.counts_cap[lg] = of[lg].size();
+    }
+    // the counts are added to: zeroed first (ordered before the scanner's
+    // stream by the device-wide synchronisation)
+    if (hipMemset(t.d_counts[lg], 0, of[lg].size() * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      return fail(CUDASP_ERR_HIP, "resident table: zeroing the match counts on device %d failed", t.devices[lg]);
+  }
+  for (size_t lg = 0; lg < nl; lg++) {
+    if (of[lg].empty()) continue;
+    DeviceSet ds(t.devices[lg]);
+    std::vector<cudasp_device_batch> db(of[lg].size());
+    for (size_t k = 0; k < of[lg].size(); k++) {
+      const Batch& bt = t.batches[of[lg][k]];
+      db[k] = cudasp_device_batch{bt.d_x, bt.d_y, bt.d_out, bt.d_offs, bt.d_lens, bt.n, bt.d_flags, bt.d_rows,
+                                  t.d_counts[lg] + k};
+    }
+    const int rc = cudasp_scan_device_batches(t.scanners[lg], db.data(), (uint32_t)db.size(), nullptr);
+    if (rc != CUDASP_OK) return rc;
+  }
+  std::vector<uint32_t> cnt, idx;
+  for (size_t lg = 0; lg < nl; lg++) {
+    if (of[lg].empty()) continue;
+    DeviceSet ds(t.devices[lg]);
+    int rc = cudasp_scanner_sync(t.scanners[lg]);
+    if (rc != CUDASP_OK) return rc;
+    cnt.resize(of[lg].size());
+    if (hipMemcpy(cnt.data(), t.d_counts[lg], cnt.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(CUDASP_ERR_HIP, "resident table: reading the match counts on device %d failed", t.devices[lg]);
+    for (size_t k = 0; k < of[lg].size(); k++) {
+      const Batch& bt = t.batches[of[lg][k]];
+      const uint32_t m = cnt[k];
+      if (m == 0) continue;
+      if (m > bt.n)
+        return fail(CUDASP_ERR_HIP, "resident table: batch %zu reports %u matches of %u rows", of[lg][k], m, bt.n);
+      idx.resize(m);
+      if (hipMemcpy(idx.data(), bt.d_rows, (size_t)m * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(CUDASP_ERR_HIP, "resident table: reading batch %zu's matches failed", of[lg][k]);
+      for (uint32_t r : idx) {
+        if (r >= bt.n) return fail(CUDASP_ERR_HIP, "resident table: batch %zu reports row %u of %u", of[lg][k], r, bt.n);
+        hits.push_back(bt.number(r));
+      }
+    }
+  }
+  return CUDASP_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int cudasp_pinned_create(uint64_t batch_size, const int* devices, uint32_t device_count, cudasp_pinned_table** out) {
+  return cudasp_pinned_create_placed(batch_size, devices, device_count, CUDASP_TABLE_PINNED, out);
+}
+
+int cudasp_pinned_create_placed(uint64_t batch_size, const int* devices, uint32_t device_count, int placement,
+                                cudasp_pinned_table** out) {
   if (!out) return fail(CUDASP_ERR_INVALID_ARG, "null argument");
   *out = nullptr;
+  if (placement != CUDASP_TABLE_PINNED && placement != CUDASP_TABLE_HBM)
+    return fail(CUDASP_ERR_INVALID_ARG, "placement must be CUDASP_TABLE_PINNED or CUDASP_TABLE_HBM, got %d", placement);
   if (batch_size == 0) batch_size = CUDASP_TF_DEFAULT_BATCH;
   if (batch_size > MAX_BATCH)
     return fail(CUDASP_ERR_INVALID_ARG, "batch_size too large (max 10,000,000), got %llu",
@@ -252,6 +447,7 @@ int cudasp_pinned_create(uint64_t batch_size, const int* devices, uint32_t devic
   auto* t = new cudasp_pinned_table();
   t->batch_size = batch_size;
   t->host_only = host_only;
+  t->hbm = placement == CUDASP_TABLE_HBM;
   t->max_words = env_max_words();
   if (devices)
     t->devices.assign(devices, devices + device_count);
@@ -276,6 +472,8 @@ int cudasp_pinned_create(uint64_t batch_size, const int* devices, uint32_t devic
   }
   t->scanners.assign(t->devices.size(), nullptr);
   t->streams.assign(t->devices.size(), nullptr);
+  t->d_counts.assign(t->devices.size(), nullptr);
+  t->counts_cap.assign(t->devices.size(), 0);
   t->open.rows.reserve(std::min<uint64_t>(batch_size, 1u << 16) * TWEAK_KEY_SIZE);
   *out = t;
   return CUDASP_OK;
@@ -372,8 +570,10 @@ int cudasp_pinned_scan(cudasp_pinned_table* t, const cudasp_tf_bind_data* b, uin
   for (size_t lg = 0; lg < nl; lg++) {
     DeviceSet ds(t->devices[lg]);
     if (!t->scanners[lg]) {
-      rc = cudasp_scanner_create(t->devices[lg], scan, spend, labels, nlabels,
-                                 std::max<uint64_t>(1, std::min<uint64_t>(t->batch_size, CUDASP_TF_DEFAULT_BATCH)),
+      // (the resident scan's per-batch path, taken for output_count > 1,
+      // needs a batch's rows within the scanner's capacity)
+      const uint64_t cap = t->hbm ? t->batch_size : std::min<uint64_t>(t->batch_size, CUDASP_TF_DEFAULT_BATCH);
+      rc = cudasp_scanner_create(t->devices[lg], scan, spend, labels, nlabels, std::max<uint64_t>(1, cap),
                                  &t->scanners[lg]);
     } else {
       rc = cudasp_scanner_set_keys(t->scanners[lg], scan, spend, labels, nlabels);
@@ -383,6 +583,7 @@ int cudasp_pinned_scan(cudasp_pinned_table* t, const cudasp_tf_bind_data* b, uin
       t->stream_ok = false;
       return rc;  // the scanner call's message
     }
+    if (t->hbm) continue;  // no streams
     if (!cudasp_stream_supported(t->scanners[lg])) {
       t->stream_ok = false;
       return fail(CUDASP_ERR_INVALID_ARG, "pinned table: the streaming scan cannot run %u label keys", nlabels);
@@ -403,62 +604,16 @@ int cudasp_pinned_scan(cudasp_pinned_table* t, const cudasp_tf_bind_data* b, uin
     }
   }
   t->shape = shape;
-  t->stream_ok = false;  // until this scan finishes
   std::vector<uint64_t> hits;
-  std::vector<std::deque<std::pair<size_t, uint64_t>>> pend(nl);  // (batch, seq) in publish order
-  std::string msg;
-  // a done batch's matches: the count is readable until 64 more batches are
-  // published on its stream, the row indices stay in its buffer
-  auto collect = [&](size_t lg) -> int {
-    const auto [j, seq] = pend[lg].front();
-    pend[lg].pop_front();
-    cudasp_stream* st = t->streams[lg];
-    int r = cudasp_stream_wait(st, seq);
-    uint32_t m = 0;
-    if (r == CUDASP_OK) r = cudasp_stream_matches(st, seq, &m);
-    if (r != CUDASP_OK) return r;
-    const Batch& bt = t->batches[j];
-    if (m > bt.n) return fail(CUDASP_ERR_HIP, "pinned table: batch %zu reports %u matches of %u rows", j, m, bt.n);
-    for (uint32_t k = 0; k < m; k++) {
-      if (bt.matches[k] >= bt.n)
-        return fail(CUDASP_ERR_HIP, "pinned table: batch %zu reports row %u of %u", j, bt.matches[k], bt.n);
-      hits.push_back(bt.number(bt.matches[k]));
-    }
-    return CUDASP_OK;
-  };
-  for (size_t j = 0; j < t->batches.size() && rc == CUDASP_OK; j++) {
-    const Batch& bt = t->batches[j];
-    DeviceSet ds(t->devices[bt.lg]);
-    if (pend[bt.lg].size() >= STREAM_RING) rc = collect(bt.lg);
-    if (rc != CUDASP_OK) break;
-    cudasp_stream_batch sb{};
-    sb.tweak_keys = bt.rows;
-    sb.outputs = bt.outputs;
-    sb.output_offsets = bt.offsets;
-    sb.output_lengths = nullptr;  // Arrow offsets: n + 1
-    sb.n = bt.n;
-    sb.match_rows = bt.matches;
-    sb.d_mirror = bt.d_mirror;
-    uint64_t seq = 0;
-    rc = cudasp_stream_publish_batch(t->streams[bt.lg], &sb, &seq);
-    if (rc == CUDASP_OK) pend[bt.lg].emplace_back(j, seq);
+  double t_pub = 0;
+  if (t->hbm) {
+    rc = scan_hbm(*t, hits);
+    if (rc != CUDASP_OK) return rc;
+    t_pub = now_s();
+  } else {
+    rc = scan_streams(*t, hits, &t_pub);
+    if (rc != CUDASP_OK) return rc;
   }
-  for (size_t lg = 0; lg < nl && rc == CUDASP_OK; lg++) {
-    DeviceSet ds(t->devices[lg]);
-    rc = cudasp_stream_close(t->streams[lg]);
-  }
-  const double t_pub = now_s();
-  for (size_t lg = 0; lg < nl && rc == CUDASP_OK; lg++) {
-    DeviceSet ds(t->devices[lg]);
-    while (!pend[lg].empty() && rc == CUDASP_OK) rc = collect(lg);
-    if (rc == CUDASP_OK) rc = cudasp_stream_finish(t->streams[lg]);  // reset for the next scan
-  }
-  if (rc != CUDASP_OK) {
-    msg = cudasp_last_error();
-    reset_streams(*t);
-    return fail(rc, "%s", msg.c_str());
-  }
-  t->stream_ok = true;
   std::sort(hits.begin(), hits.end());
   auto* out = (uint64_t*)malloc(std::max<size_t>(1, hits.size()) * sizeof(uint64_t));
   if (!out) return fail(CUDASP_ERR_CAPACITY, "pinned table: %zu result rows: allocation failed", hits.size());
@@ -483,6 +638,8 @@ int cudasp_pinned_info(const cudasp_pinned_table* t, cudasp_pinned_info_t* out) 
   out->last_matches = t->last_matches;
   out->last_scan_s = t->last_scan_s;
   out->last_publish_s = t->last_publish_s;
+  out->placement = t->hbm ? CUDASP_TABLE_HBM : CUDASP_TABLE_PINNED;
+  out->device_bytes = t->device_bytes;
   return CUDASP_OK;
 }
 
@@ -497,6 +654,10 @@ void cudasp_pinned_free(cudasp_pinned_table* t) {
         cudasp_stream_destroy(t->streams[lg]);
       }
       if (t->scanners[lg]) cudasp_scanner_destroy(t->scanners[lg]);
+      if (t->d_counts[lg]) {
+        DeviceSet ds(t->devices[lg]);
+        (void)hipFree(t->d_counts[lg]);
+      }
     }
     for (Batch& bt : t->batches) free_batch(bt);
   }

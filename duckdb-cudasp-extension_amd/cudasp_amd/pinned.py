@@ -272,9 +272,14 @@ class NativePinnedTable:
     through cudasp_pinned_append (Arrow buffers, bulk reads, the
     table-function host's row semantics) and each scan's publish / harvest
     loop runs in C++.  Same constructor, scan(), last_stats and close() as
-    PinnedTable; what a DuckDB host would call beside cudasp_scan."""
+    PinnedTable; what a DuckDB host would call beside cudasp_scan.
+    placement="hbm" keeps the table resident in device memory instead
+    (CUDASP_TABLE_HBM: each scan one k_scan_multi launch per GPU over all of
+    its batches)."""
 
-    def __init__(self, data, batch_size=None, device=0, devices=None, piece_rows=1 << 20):
+    PLACEMENTS = {"pinned": 0, "hbm": 1}  # CUDASP_TABLE_PINNED / CUDASP_TABLE_HBM
+
+    def __init__(self, data, batch_size=None, device=0, devices=None, piece_rows=1 << 20, placement="pinned"):
         import ctypes
 
         from . import _native
@@ -290,7 +295,10 @@ class NativePinnedTable:
         lib = self._lib = _lib()
         h = ctypes.c_void_p()
         devs = (ctypes.c_int * len(self.devices))(*self.devices)
-        _native.check(lib.cudasp_pinned_create(self.batch_size, devs, len(self.devices), ctypes.byref(h)))
+        if placement not in self.PLACEMENTS:
+            raise ValueError("placement must be 'pinned' or 'hbm', got %r" % (placement,))
+        _native.check(lib.cudasp_pinned_create_placed(self.batch_size, devs, len(self.devices),
+                                                      self.PLACEMENTS[placement], ctypes.byref(h)))
         self._h = h
         try:
             for piece in _arrow_pieces(t, piece_rows):  # row numbers: positions in t

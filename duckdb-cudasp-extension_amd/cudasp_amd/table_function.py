@@ -114,6 +114,8 @@ class _PinnedInfo(ctypes.Structure):
         ("last_matches", ctypes.c_uint64),
         ("last_scan_s", ctypes.c_double),
         ("last_publish_s", ctypes.c_double),
+        ("placement", ctypes.c_int32),
+        ("device_bytes", ctypes.c_uint64),
     ]
 
 
@@ -151,6 +153,8 @@ _HOST_SIGNATURES = {
     "cudasp_tf_get_stats": (ctypes.c_int, [_P, ctypes.POINTER(_Stats)]),
     "cudasp_pinned_create": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_int), ctypes.c_uint32,
                                             ctypes.POINTER(_P)]),
+    "cudasp_pinned_create_placed": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_int), ctypes.c_uint32,
+                                                   ctypes.c_int, ctypes.POINTER(_P)]),
     "cudasp_pinned_append": (ctypes.c_int, [_P, ctypes.POINTER(_Columns)]),
     "cudasp_pinned_scan": (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
                                           ctypes.POINTER(ctypes.c_uint64)]),

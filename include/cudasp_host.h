@@ -255,6 +255,15 @@ int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf
  *                        threads over its GPUs (src/cudasp_extension.cu:523-529);
  *                        a device listed m times runs m streaming kernels on
  *                        1/m of its wave slots each.
+ *   cudasp_pinned_create_placed  the same with a placement:
+ *                        CUDASP_TABLE_PINNED (cudasp_pinned_create's): the
+ *                        rows in pinned host memory, read over PCIe by each
+ *                        scan's streaming kernels;
+ *                        CUDASP_TABLE_HBM: the rows resident in device memory
+ *                        in k_scan_multi's layout (~93 B per row with 2
+ *                        outputs), each scan one cudasp_scan_device_batches
+ *                        launch per logical GPU over all of its batches (the
+ *                        device-resident rate; any label count).
  *   cudasp_pinned_append  one run of rows (cudasp_tf_columns, int64 outputs;
  *                        not full_x), numbered after the rows appended before
  *                        (skipped rows keep their numbers).  The rows'
@@ -270,7 +279,7 @@ int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf
  *                        keys and options of b (cudasp_tf_bind and
  *                        cudasp_tf_bind_options; full_x is
  *                        CUDASP_ERR_INVALID_ARG, as are label counts the
- *                        streaming scan cannot hold).  *rows receives the
+ *                        streaming scan cannot hold, in the pinned placement).  *rows receives the
  *                        numbers of the matching rows, ascending (free with
  *                        cudasp_pinned_free_rows), *count their count.  Scans
  *                        of one table run one at a time (a lock); scanners and
@@ -293,8 +302,14 @@ typedef struct {
   uint64_t last_matches;
   double last_scan_s;    /* the whole cudasp_pinned_scan call */
   double last_publish_s; /* until every batch was published */
+  int32_t placement;     /* CUDASP_TABLE_PINNED or CUDASP_TABLE_HBM */
+  uint64_t device_bytes; /* device memory of the batches (HBM: all of them; pinned: the outputs mirrors) */
 } cudasp_pinned_info_t;
+#define CUDASP_TABLE_PINNED 0
+#define CUDASP_TABLE_HBM 1
 int cudasp_pinned_create(uint64_t batch_size, const int* devices, uint32_t device_count, cudasp_pinned_table** out);
+int cudasp_pinned_create_placed(uint64_t batch_size, const int* devices, uint32_t device_count, int placement,
+                                cudasp_pinned_table** out);
 int cudasp_pinned_append(cudasp_pinned_table* t, const cudasp_tf_columns* cols);
 int cudasp_pinned_scan(cudasp_pinned_table* t, const cudasp_tf_bind_data* b, uint64_t** rows, uint64_t* count);
 void cudasp_pinned_free_rows(uint64_t* rows);

@@ -6,7 +6,9 @@ batch sizes that wrap the 64-entry descriptor ring, repeated scans of one
 pinned table with different keys, the protocol variants, and the reference's
 tweak-length error.  Every test runs on both implementations: PinnedTable
 (Python publish loop) and NativePinnedTable (the C ABI cudasp_pinned_*,
-csrc/host/pinned_table.cpp, fed Arrow runs through cudasp_pinned_append)."""
+csrc/host/pinned_table.cpp, fed Arrow runs through cudasp_pinned_append), in
+both placements: pinned host memory (streaming kernels) and resident in HBM
+(CUDASP_TABLE_HBM, k_scan_multi)."""
 import pytest
 
 import golden_io
@@ -23,9 +25,13 @@ def gpu():
         pytest.skip("no GPU")
 
 
-@pytest.fixture(params=["PinnedTable", "NativePinnedTable"])
+@pytest.fixture(params=["PinnedTable", "NativePinnedTable", "NativePinnedTable-hbm"])
 def cls(request):
+    import functools
+
     import cudasp_amd
+    if request.param.endswith("-hbm"):
+        return functools.partial(cudasp_amd.NativePinnedTable, placement="hbm")
     return getattr(cudasp_amd, request.param)
 
 
@@ -136,8 +142,9 @@ def test_logical_gpus(gpu, cls, devices, batch_size):
         assert _rows(pt.scan(*keys[:2], [])) == _rows(cudasp_scan_arrow(tbl, *keys[:2], []))
 
 
+@pytest.mark.parametrize("placement", ["pinned", "hbm"])
 @pytest.mark.parametrize("piece_rows", [1, 37, 5000])
-def test_native_runs_and_numbers(gpu, piece_rows):
+def test_native_runs_and_numbers(gpu, piece_rows, placement):
     """The C table takes the rows as many appended runs (batches span runs;
     NULL rows skipped but numbered): scan_rows gives the matching rows'
     positions in the input, ascending, as the oracle-pinned Arrow path finds
@@ -149,17 +156,19 @@ def test_native_runs_and_numbers(gpu, piece_rows):
     tbl = _arrow(rows)
     keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
     want = _rows(cudasp_scan_arrow(tbl, *keys, batch_size=500))
-    with NativePinnedTable(tbl, batch_size=500, piece_rows=piece_rows) as pt:
+    with NativePinnedTable(tbl, batch_size=500, piece_rows=piece_rows, placement=placement) as pt:
         idx = pt.scan_rows(*keys)
         inf = pt.info()
     assert idx.tolist() == sorted(set(idx.tolist())) and all(i % 7 for i in idx.tolist())
     assert inf["rows_appended"] == len(rows) and inf["rows_pinned"] == len(rows) - len(range(0, len(rows), 7))
     assert inf["batches"] == -(-inf["rows_pinned"] // 500) and inf["last_matches"] == len(idx)
+    assert inf["placement"] == (1 if placement == "hbm" else 0) and inf["device_bytes"] > 0
     got = _rows(tbl.take(__import__("pyarrow").array(idx)).select([0, 1, 2]))
     assert got == want
 
 
-def test_native_early_close(gpu, monkeypatch):
+@pytest.mark.parametrize("placement", ["pinned", "hbm"])
+def test_native_early_close(gpu, monkeypatch, placement):
     """Batches closed early by the outputs word cap (the u32-offset guard,
     lowered by CUDASP_PINNED_TEST_MAX_WORDS): more than 64 small batches of
     uneven row counts, the ring wrapped, rows as the Arrow path's."""
@@ -169,7 +178,26 @@ def test_native_early_close(gpu, monkeypatch):
     rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
     tbl = _arrow(rows * 8)
     keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
-    with NativePinnedTable(tbl, batch_size=1000) as pt:
+    with NativePinnedTable(tbl, batch_size=1000, placement=placement) as pt:
         got = _rows(pt.scan(*keys))
         assert pt.info()["batches"] > 64
     assert got == _rows(cudasp_scan_arrow(tbl, *keys))
+
+
+@pytest.mark.parametrize("output_count", [None, 3])
+def test_hbm_many_labels(gpu, output_count):
+    """The resident placement takes any label count (k_scan_multi; the
+    streaming kernel's scratch bounds the pinned placement's) and the
+    per-batch path of output_count > 1: 40 labels, rows as the Arrow path's."""
+    from cudasp_amd import NativePinnedTable, cudasp_scan_arrow
+    rr = golden_io.load("random_rows.json")
+    rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
+    tbl = _arrow(rows * 4)
+    labels = [bytes.fromhex(l) for l in rr["label_keys"]]
+    import bench
+    labels = labels + bench.label_keys(40)[len(labels):]
+    keys = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), labels)
+    want = _rows(cudasp_scan_arrow(tbl, *keys, batch_size=200, output_count=output_count))
+    assert want
+    with NativePinnedTable(tbl, batch_size=200, placement="hbm") as pt:
+        assert _rows(pt.scan(*keys, output_count=output_count)) == want

@@ -23,7 +23,7 @@
 //            [--outputs K | --outputs-max KMAX] [--input rows|columns]
 //            [--reps R] [--warm-reps W [--warm-ms MS]] [--plant-sample FILE]
 //            [--null-device [--cpu-table]] [--output-count K] [--label-negation]
-//            [--pinned DEVICES]
+//            [--pinned DEVICES [--hbm]]
 // (W more queries, each started right after MS ms of a busy kernel on every
 // GPU: the rate at full clock, without the ramp from idle; warm_tx_per_s)
 // --plant-sample writes 256 planted rows and 256 unplanted rows, strided over
@@ -50,7 +50,8 @@
 // warms the scanners and streams; each scan binds the keys like a query),
 // batches round-robin over DEVICES (a device listed m times: m logical GPUs
 // on it); a scan passes when its row numbers are exactly the planted rows.
-// With --null-device only the appends run (no scan).
+// With --null-device only the appends run (no scan).  --hbm: the table
+// resident in device memory instead (CUDASP_TABLE_HBM, k_scan_multi per scan).
 // Label keys: F holds L 64-byte keys (x || y, little-endian, bench.label_keys);
 // without F, L must be 0 or 1 (the SQL test's label, test/sql/cudasp.test:104).
 // Prints one JSON line; exit 0 iff every timed query emitted exactly the
@@ -121,6 +122,7 @@ struct Args {
   int output_count = 1;        // protocol variant: output indices per row (bind option output_count)
   bool label_negation = false;  // protocol variant: labels also negated (bind option label_negation)
   std::vector<int> pinned;      // --pinned: the pinned table's devices (empty: table-function queries)
+  bool hbm = false;             // --hbm: CUDASP_TABLE_HBM placement
 };
 
 static Args parse(int argc, char** argv) {
@@ -150,6 +152,7 @@ static Args parse(int argc, char** argv) {
     else if (s == "--cpu-table") a.cpu_table = true;
     else if (s == "--output-count") a.output_count = atoi(val());
     else if (s == "--label-negation") a.label_negation = true;
+    else if (s == "--hbm") a.hbm = true;
     else if (s == "--pinned") {
       std::string v = val();
       for (size_t p = 0; p <= v.size();) {
@@ -536,7 +539,8 @@ static int run_pinned(const Args& a, const uint8_t scan[32], const uint8_t spend
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - x).count();
   };
   cudasp_pinned_table* pt;
-  CK(cudasp_pinned_create((uint64_t)a.batch, a.pinned.data(), (uint32_t)a.pinned.size(), &pt));
+  CK(cudasp_pinned_create_placed((uint64_t)a.batch, a.pinned.data(), (uint32_t)a.pinned.size(),
+                                 a.hbm ? CUDASP_TABLE_HBM : CUDASP_TABLE_PINNED, &pt));
   const uint64_t piece = 65536;
   std::vector<int32_t> txo(piece + 1), lo(piece + 1);
   for (uint64_t c0 = 0; c0 < rows; c0 += piece) {
@@ -600,16 +604,18 @@ static int run_pinned(const Args& a, const uint8_t scan[32], const uint8_t spend
   for (size_t i = 0; i < a.pinned.size(); i++) devs += (i ? ", " : "") + std::to_string(a.pinned[i]);
   all += "]";
   devs += "]";
-  printf("{\"what\": \"C pinned table (cudasp_pinned_*): appended once, scanned in place per query\", "
+  printf("{\"what\": \"C pinned table (cudasp_pinned_*): appended once, scanned in place per query\", \"placement\": \"%s\", "
          "\"rows\": %llu, \"batch_size\": %lld, \"labels\": %d, \"outputs_total\": %llu, \"devices\": %s, "
          "\"batches\": %llu, \"rows_pinned\": %llu, \"pinned_bytes\": %llu, \"pin_s\": %.3f, "
          "\"generate_seconds\": %.2f, \"reps\": %d, \"seconds\": %.5f, \"seconds_all\": %s, \"tx_per_s\": %.1f, "
          "\"matches\": %llu, \"planted\": %zu, \"emitted_equal_planted\": %s, \"last_publish_s\": %.5f, "
-         "\"null_device\": %s}\n",
-         (unsigned long long)rows, (long long)a.batch, L, (unsigned long long)t.outputs.size(), devs.c_str(),
+         "\"device_bytes\": %llu, \"null_device\": %s}\n",
+         a.hbm ? "hbm" : "pinned", (unsigned long long)rows, (long long)a.batch, L,
+         (unsigned long long)t.outputs.size(), devs.c_str(),
          (unsigned long long)inf.batches, (unsigned long long)inf.rows_pinned, (unsigned long long)inf.pinned_bytes,
          pin_s, gen_s, (int)secs.size(), med, all.c_str(), med > 0 ? rows / med : 0.0, (unsigned long long)matches,
-         t.planted.size(), exact ? "true" : "false", inf.last_publish_s, a.null_device ? "true" : "false");
+         t.planted.size(), exact ? "true" : "false", inf.last_publish_s, (unsigned long long)inf.device_bytes,
+         a.null_device ? "true" : "false");
   return exact ? 0 : 1;
 }
 
