@@ -50,7 +50,8 @@ the whole rank table, `planted_oracle_check`, and of a 256-row sample of the
 end-to-end leg's planted and unplanted rows, `e2e.planted_oracle_check`).
 The `pinned` leg scans the same table pinned once in host memory, in place
 (the C pinned table cudasp_pinned_* driven by tools/host_e2e --pinned, over
-all N GPUs, no host copy per query).
+all N GPUs, no host copy per query); the `resident` leg
+the same table kept in HBM by the same ABI (CUDASP_TABLE_HBM).
 `cpu_baseline` itself is the strongest CPU stand-in the image allows:
 `port-optimized` (tools/cpu_port, the product's row pipeline compiled for the
 host) where it covers the options, else the oracle port.
@@ -507,7 +508,7 @@ def host_cores():
     return visible, visible, "sched_getaffinity"
 
 
-def pinned_leg(args, labels, world):
+def pinned_leg(args, labels, world, hbm=False):
     """Zero-copy scans of the same table through the C pinned table
     (cudasp_pinned_*, include/cudasp_host.h):
     tools/host_e2e --pinned as a child process builds the table in host
@@ -515,7 +516,9 @@ def pinned_leg(args, labels, world):
     times in place over all `world` GPUs (batches round-robin, one streaming
     kernel per GPU, no host copy per query; each scan binds its keys like a
     query); the first scan warms the scanners and streams, the median of the
-    other 3 is reported, and every scan must return exactly the planted rows."""
+    other 3 is reported, and every scan must return exactly the planted rows.
+    hbm=True: the same table resident in device memory instead
+    (CUDASP_TABLE_HBM: each scan one k_scan_multi launch per GPU)."""
     import subprocess
     import tempfile
     exe = os.path.join(ROOT, "tools", "host_e2e")
@@ -523,7 +526,7 @@ def pinned_leg(args, labels, world):
         return dict(error="tools/host_e2e not built (make -C duckdb-cudasp-extension_amd)")
     devices = ",".join(str(r % max(1, torch.cuda.device_count())) for r in range(world))
     cmd = [exe, "--rows", str(args.rows), "--batch", str(args.batch_size), "--labels", str(len(labels)),
-           "--reps", "3", "--pinned", devices]
+           "--reps", "3", "--pinned", devices] + (["--hbm"] if hbm else [])
     cmd += ["--outputs-max", str(args.outputs_max)] if args.outputs_max else ["--outputs", str(args.outputs_per_row)]
     lf = None
     if labels:
@@ -1239,6 +1242,9 @@ def main():
                 pn = pinned_leg(args, labels, world)
                 result["pinned"] = pn
                 result["pinned_tx_s"] = pn.get("tx_per_s")
+                rs = pinned_leg(args, labels, world, hbm=True)
+                result["resident"] = rs
+                result["resident_tx_s"] = rs.get("tx_per_s")
         if world > 1:
             dist.barrier(group=cpu_group)
     if rank == 0:

@@ -279,13 +279,15 @@ int cudasp_tf_final(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf
  *                        keys and options of b (cudasp_tf_bind and
  *                        cudasp_tf_bind_options; full_x is
  *                        CUDASP_ERR_INVALID_ARG, as are label counts the
- *                        streaming scan cannot hold, in the pinned placement).  *rows receives the
+ *                        streaming scan cannot hold in the pinned
+ *                        placement).  *rows receives the
  *                        numbers of the matching rows, ascending (free with
  *                        cudasp_pinned_free_rows), *count their count.  Scans
  *                        of one table run one at a time (a lock); scanners and
  *                        streaming kernels are kept and rebound between scans.
  *   cudasp_pinned_info   rows appended, rows pinned (non-skipped), batches,
- *                        pinned bytes, and the last scan's seconds.
+ *                        pinned and device bytes, the placement, and the last
+ *                        scan's seconds.
  *   cudasp_pinned_free   frees the table (a table whose last scan timed out
  *                        with a kernel still running keeps its memory).
  * Test hooks (environment, read at create): CUDASP_TF_NULL_DEVICE=1 keeps the

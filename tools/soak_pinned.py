@@ -71,7 +71,7 @@ def main():
         bs = rng.choice([1, 7, 64, 500, 2048, 300000])
         devices = [0] * rng.choice([1, 1, 2, 3])
         native = rng.random() < 0.5
-        kw = dict(piece_rows=rng.choice([1, 97, 65536])) if native else {}
+        kw = dict(piece_rows=rng.choice([1, 97, 65536]), placement=rng.choice(["pinned", "hbm"])) if native else {}
         with (NativePinnedTable if native else PinnedTable)(tbl, batch_size=bs, devices=devices, **kw) as pt:
             for _ in range(rng.choice([1, 2, 3])):
                 L = labels[:rng.randrange(len(labels) + 1)]
@@ -84,7 +84,8 @@ def main():
                                                                              label_negation=neg).columns]))
                 scans += 1
                 if got != want:
-                    print(json.dumps(dict(failed=True, run=runs, native=native, rows=tbl.num_rows, batch_size=bs,
+                    print(json.dumps(dict(failed=True, run=runs, native=native, kw=str(kw), rows=tbl.num_rows,
+                                          batch_size=bs,
                                           devices=devices,
                                           labels=len(L), output_count=oc, label_negation=neg, got=len(got),
                                           want=len(want))), flush=True)
