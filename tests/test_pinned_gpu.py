@@ -201,3 +201,16 @@ def test_hbm_many_labels(gpu, output_count):
     assert want
     with NativePinnedTable(tbl, batch_size=200, placement="hbm") as pt:
         assert _rows(pt.scan(*keys, output_count=output_count)) == want
+
+
+def test_library_loaded_before_torch_cuda(gpu):
+    """A fresh process whose first GPU call is the library's (a
+    NativePinnedTable) can still use torch's GPU afterwards: the package
+    loads torch's HIP runtime before the library (cudasp_amd/_native.py)."""
+    import os
+    import subprocess
+    import sys
+    probe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "probes",
+                         "init_order.py")
+    r = subprocess.run([sys.executable, probe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "torch tensor ok" in r.stdout, (r.stdout[-500:], r.stderr[-1500:])
