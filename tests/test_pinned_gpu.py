@@ -214,3 +214,38 @@ def test_library_loaded_before_torch_cuda(gpu):
                          "init_order.py")
     r = subprocess.run([sys.executable, probe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "torch tensor ok" in r.stdout, (r.stdout[-500:], r.stderr[-1500:])
+
+
+def test_native_tables_scanned_concurrently(gpu):
+    """Two C tables on one GPU (one pinned, one resident), each scanned from
+    its own thread with different keys at the same time, three times over:
+    every scan's rows as the Arrow path's (separate scanners and kernels;
+    the library's error state is per thread)."""
+    import threading
+
+    from cudasp_amd import NativePinnedTable, cudasp_scan_arrow
+    rr = golden_io.load("random_rows.json")
+    rows = [(i.to_bytes(32, "big"), i, bytes.fromhex(x["tweak"]), x["outputs"]) for i, x in enumerate(rr["rows"])]
+    tbl = _arrow(rows * 20)
+    k1 = (bytes.fromhex(rr["scan_key"]), bytes.fromhex(rr["spend_key"]), [bytes.fromhex(l) for l in rr["label_keys"]])
+    k2 = (k1[0], k1[1], [])
+    want = {0: _rows(cudasp_scan_arrow(tbl, *k1)), 1: _rows(cudasp_scan_arrow(tbl, *k2))}
+    got, errors = {0: [], 1: []}, []
+    tables = [NativePinnedTable(tbl, batch_size=700), NativePinnedTable(tbl, batch_size=900, placement="hbm")]
+    try:
+        def run(i):
+            try:
+                for _ in range(3):
+                    got[i].append(_rows(tables[i].scan(*(k1 if i == 0 else k2))))
+            except Exception as e:  # surfaced after join
+                errors.append(e)
+        ths = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(timeout=120)
+        assert not errors, errors
+        assert got[0] == [want[0]] * 3 and got[1] == [want[1]] * 3
+    finally:
+        for t in tables:
+            t.close()
