@@ -115,3 +115,32 @@ def test_native_pinned_appends_without_a_device(monkeypatch, piece_rows):
         assert inf.rows_appended == 200 and inf.rows_pinned == sum(1 for i in range(200) if i % 7)
     finally:
         lib.cudasp_pinned_free(h)
+
+
+def test_native_pinned_argument_errors(monkeypatch):
+    """cudasp_pinned_create_placed / _scan argument errors, loud and coded
+    (null-device mode: no GPU needed): an unknown placement, batch_size above
+    the bind's limit, an empty device list, and full_x at scan time."""
+    import ctypes
+
+    from cudasp_amd import _native
+    from cudasp_amd.table_function import BoundScan, _lib
+    monkeypatch.setenv("CUDASP_TF_NULL_DEVICE", "1")
+    lib = _lib()
+    h = ctypes.c_void_p()
+    dev = (ctypes.c_int * 1)(0)
+    assert lib.cudasp_pinned_create_placed(100, dev, 1, 5, ctypes.byref(h)) == _native.CUDASP_ERR_INVALID_ARG
+    assert b"placement" in _native.load().cudasp_last_error()
+    assert lib.cudasp_pinned_create_placed(10_000_001, dev, 1, 1, ctypes.byref(h)) == _native.CUDASP_ERR_INVALID_ARG
+    assert b"too large" in _native.load().cudasp_last_error()
+    assert lib.cudasp_pinned_create_placed(100, dev, 0, 0, ctypes.byref(h)) == _native.CUDASP_ERR_INVALID_ARG
+    for placement in (0, 1):
+        _native.check(lib.cudasp_pinned_create_placed(100, dev, 1, placement, ctypes.byref(h)))
+        try:
+            bound = BoundScan(bytes(31) + b"\x01", bytes(64), [], full_x=True)
+            rows, count = ctypes.POINTER(ctypes.c_uint64)(), ctypes.c_uint64()
+            assert lib.cudasp_pinned_scan(h, bound._h, ctypes.byref(rows), ctypes.byref(count)) == \
+                _native.CUDASP_ERR_INVALID_ARG
+            assert b"full_x" in _native.load().cudasp_last_error()
+        finally:
+            lib.cudasp_pinned_free(h)
