@@ -36,6 +36,7 @@
 #include "bind_data.hpp"
 
 extern "C" void cudasp_internal_set_error(const char* msg);
+extern "C" void* cudasp_internal_scanner_stream(cudasp_scanner* s);
 
 namespace {
 
@@ -375,9 +376,10 @@ int scan_hbm(cudasp_pinned_table& t, std::vector<uint64_t>& hits) {
         return fail(CUDASP_ERR_HIP, "resident table: match counts on device %d: allocation failed", t.devices[lg]);
       t.counts_cap[lg] = of[lg].size();
     }
-    // the counts are added to: zeroed first (ordered before the scanner's
-    // stream by the device-wide synchronisation)
-    if (hipMemset(t.d_counts[lg], 0, of[lg].size() * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    // the counts are added to: zeroed first, on the scanner's own stream
+    // (the launch below runs there, after it)
+    auto* st = (hipStream_t)cudasp_internal_scanner_stream(t.scanners[lg]);
+    if (hipMemsetAsync(t.d_counts[lg], 0, of[lg].size() * 4, st) != hipSuccess)
       return fail(CUDASP_ERR_HIP, "resident table: zeroing the match counts on device %d failed", t.devices[lg]);
   }
   for (size_t lg = 0; lg < nl; lg++) {
