@@ -48,16 +48,19 @@ on this box's host cores as `cpu_baseline_port` and checked against the GPU
 flags; it also recomputes the planted values of 256 planted rows spread over
 the whole rank table, `planted_oracle_check`, and of a 256-row sample of the
 end-to-end leg's planted and unplanted rows, `e2e.planted_oracle_check`).
-The `pinned` leg scans the same table pinned once in host memory, in place
-(the C pinned table cudasp_pinned_* driven by tools/host_e2e --pinned, over
-all N GPUs, no host copy per query); the `resident` leg
-the same table kept in HBM by the same ABI (CUDASP_TABLE_HBM).
+With --pinned, the `pinned` leg scans the same table pinned once in host
+memory, in place (the C pinned table cudasp_pinned_* driven by tools/host_e2e
+--pinned, over all N GPUs, no host copy per query) and
+the `resident` leg the same table kept in HBM by the same ABI
+(CUDASP_TABLE_HBM); both are off by default (an API the reference's SQL
+interface does not reach).
 `cpu_baseline` itself is the strongest CPU stand-in the image allows:
 `port-optimized` (tools/cpu_port, the product's row pipeline compiled for the
 host) where it covers the options, else the oracle port.
 """
 import argparse
 import ctypes
+import glob
 import hashlib
 import json
 import os
@@ -71,6 +74,9 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "duckdb-cudasp-extension_amd"))
 
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import codeobj  # noqa: E402
 from cudasp_amd import Scanner, _native  # noqa: E402
 
 METRIC = "tx/sec through cudasp_scan on 32M-row tweak table at 1/2/4/8 MI355X"
@@ -795,33 +801,43 @@ def cpu_port_sweep(smp, labels, cores, rows):
     return dict(rows=n, unit="tx/s", kind="port-optimized", points=out)
 
 
-def sq_profile_path(args):
-    """The PMC instruction-count summary matching this run's shape (launch
+def stamped_summary(name, key, stamp):
+    """The newest profiles/r0N_<name>.json measured on the machine code the
+    process loaded: its `code_stamp[key]` (tools/pmc_summary.py --stamp-lib)
+    must equal `stamp`, the loaded kernel's (tools/codeobj.py).  Counters of
+    another build of the kernel are never used: (None, reason) instead."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*_%s.json" % name)), reverse=True)
+    seen = []
+    for p in paths:
+        with open(p) as f:
+            d = json.load(f)
+        st = ((d.get("code_stamp") or {}).get(key) or {}).get("sha256")
+        if stamp and st == stamp:
+            return p, d, None
+        seen.append("%s: %s" % (os.path.relpath(p, ROOT), st or "unstamped"))
+    return None, None, ("no %s summary measured on the loaded %s (stamp %s); on file: %s"
+                        % (name, key, stamp, "; ".join(seen) or "none"))
+
+
+def sq_profile_name(args):
+    """The PMC instruction-count summary name matching this run's shape (launch
     mode, labels, outputs per row, fixed-base width, variants):
-    profiles/r0N_pmc_sq_[multi_]L<labels>_k<outputs>_w<bits>[_neg][_K<k>].json,
-    this round's (r03) when it has one, else round 2's."""
+    pmc_sq_[multi_]L<labels>_k<outputs>_w<bits>[_neg][_K<k>]."""
     kdesc = "1-%d" % args.outputs_max if args.outputs_max else str(args.outputs_per_row)
     name = "pmc_sq_%sL%d_k%s_w%d" % ("multi_" if args.launch == "multi" else "", args.labels, kdesc, args.fb_bits)
     if args.label_negation:
         name += "_neg"
     if args.output_count != 1:
         name += "_K%d" % args.output_count
-    for rnd in ("r03", "r02"):
-        path = os.path.join(ROOT, "profiles", "%s_%s.json" % (rnd, name))
-        if os.path.exists(path):
-            return path
-    return os.path.join(ROOT, "profiles", "r03_%s.json" % name)
+    return name
 
 
-def alu_roofline(path, value_per_gpu, multi=False):
+def alu_roofline(sq, path, value_per_gpu, multi=False, clock_mhz=None, stamp=None):
     """Integer-VALU roofline of the whole path: VALU wave-instructions per row
-    (rocprofv3 SQ_INSTS_VALU of the same shape of run, profiles/: both stage
-    kernels per batch, or k_scan_multi per row with --launch multi) x rows/s
-    per GPU, against the nominal VALU issue rate and the measured VOP3 rate."""
-    if not path or not os.path.exists(path):
-        return dict(error="no PMC summary for this shape: %s" % os.path.relpath(path, ROOT) if path else "none")
-    with open(path) as f:
-        sq = json.load(f)
+    (rocprofv3 SQ_INSTS_VALU of a run of the same shape on the same machine
+    code, profiles/: k_scan_multi per row with --launch multi, both stage
+    kernels per batch otherwise) x rows/s per GPU, against the nominal VALU
+    issue rate, the measured VOP3 rate and the kernel's own mix ceiling."""
     per = sq["per_kernel"]
     if multi:
         m = per.get("k_scan_multi", {}).get("SQ_INSTS_VALU")
@@ -830,6 +846,10 @@ def alu_roofline(path, value_per_gpu, multi=False):
             return dict(error="%s lacks k_scan_multi" % os.path.relpath(path, ROOT))
         wi_per_row = m / float(rows)
         per64 = dict(k_scan_multi=wi_per_row * 64)
+        g = per.get("k_scan_multi", {}).get("GRBM_GUI_ACTIVE")
+        # issue rate in the profiled launch itself: VALU wave-instructions per
+        # 4 SIMD cycles (GRBM_GUI_ACTIVE sums the 8 XCDs), clock-independent
+        kernel_u = 4 * m / (g / 8 * 1024) if g else None
     else:
         rpl = float(sq.get("rows_per_launch", 300000))
         a = per.get("k_shared_secret", {}).get("SQ_INSTS_VALU")
@@ -838,46 +858,46 @@ def alu_roofline(path, value_per_gpu, multi=False):
             return dict(error="%s lacks the stage kernels" % os.path.relpath(path, ROOT))
         wi_per_row = (a + bm) / rpl
         per64 = dict(k_shared_secret=a / rpl * 64, k_match=bm / rpl * 64)
+        kernel_u = None
     achieved_wi = wi_per_row * value_per_gpu
     out = dict(bound="valu", unit="wave-instr/s per GPU", achieved=achieved_wi, peak=VALU_WAVE_INSTR_PEAK,
                frac=achieved_wi / VALU_WAVE_INSTR_PEAK, measured_vop3_issue_rate=VOP3_WAVE_INSTR_MEASURED,
                frac_of_measured_vop3_rate=achieved_wi / VOP3_WAVE_INSTR_MEASURED,
-               valu_wave_instr_per_64_rows=per64,
-               source=os.path.relpath(path, ROOT),
-               note="SQ_INSTS_VALU per row of a run of this shape (%s); peak = nominal VALU issue rate; VOP3 "
-                    "integer ops issue at about half of it on gfx950" % sq.get("shape", "see source"))
-    mix = mix_ceiling(achieved_wi)
-    if mix:
-        out["mix_ceiling"] = mix
+               valu_wave_instr_per_64_rows=per64, kernel_U_profiled=kernel_u,
+               source=os.path.relpath(path, ROOT), code_stamp=stamp,
+               note="SQ_INSTS_VALU per row of a run of this shape on this machine code (%s); peak = nominal VALU "
+                    "issue rate; VOP3 integer ops issue at about half of it on gfx950 (the measured rate is at "
+                    "2.4 GHz)" % sq.get("shape", "see source"))
+    if multi:
+        mix = mix_ceiling(achieved_wi, clock_mhz, stamp, kernel_u)
+        if mix:
+            out["mix_ceiling"] = mix
     return out
 
 
-VALU_CEILING_PROFILE = os.path.join(ROOT, "profiles", "r03_valu_ceiling.json")
-
-
-def mix_ceiling(achieved_wi):
-    """The issue ceiling of the scan's own instruction mix at the 2.4 GHz
-    peak clock (profiles/r03_valu_ceiling.json, tools/valu_ceiling.py): the
-    kernel's stage-A ladder (126 doublings + 39 mixed additions, ~88% of its
-    VALU) run as register-resident loops at the kernel's 3 waves per SIMD
-    issues U_ladder VALU wave-instructions per 4 SIMD cycles; x 1024 SIMDs x
-    2.4 GHz / 4 is the rate this mix sustains when nothing else limits it.
-    frac > 1 within a few percent means the kernel is at that ceiling (its
-    other ~12% of instructions issue a little faster than the ladder's)."""
-    if not os.path.exists(VALU_CEILING_PROFILE):
-        return None
-    with open(VALU_CEILING_PROFILE) as f:
-        vc = json.load(f)
+def mix_ceiling(achieved_wi, clock_mhz, stamp, kernel_u):
+    """The issue ceiling of the scan's own instruction mix (tools/valu_ceiling.py,
+    profiles/r0N_valu_ceiling.json, stamped like the counters): the kernel's
+    stage-A ladder (~88% of its VALU) run as register-resident loops at the
+    kernel's 3 waves per SIMD issues U_ladder VALU wave-instructions per 4
+    SIMD cycles; x 1024 SIMDs x f / 4 is the rate this mix sustains at clock f
+    when nothing else limits it.  f is the timed launch's own shader clock
+    (`clock`), else the 2.4 GHz peak.  The clock-free form is the profiled
+    launch's U over U_ladder."""
+    path, vc, why = stamped_summary("valu_ceiling", "k_scan_multi", stamp)
+    if vc is None:
+        return dict(error=why)
     u = vc.get("ladder_mix_U")
     if not u:
-        return None
-    ceiling = u * 1024 * 2.4e9 / 4
-    k = vc.get("k_scan_multi_L0", {})
-    return dict(ladder_mix_U=u, ceiling_wave_instr_per_s_at_peak_clock=ceiling, frac=achieved_wi / ceiling,
-                kernel_U_measured=k.get("U"), kernel_frac_of_ladder_mix_measured=k.get("frac_of_ladder_mix_ceiling"),
-                source=os.path.relpath(VALU_CEILING_PROFILE, ROOT),
-                note="U = VALU wave-instructions per 4 SIMD cycles (PMC); the kernel's own U over the ladder loops' "
-                     "U is clock-independent; frac here also assumes the peak clock")
+        return dict(error="%s has no ladder_mix_U" % os.path.relpath(path, ROOT))
+    f = clock_mhz * 1e6 if clock_mhz else 2.4e9
+    ceiling = u * 1024 * f / 4
+    return dict(ladder_mix_U=u, clock_hz=f, clock_source="timed launch" if clock_mhz else "peak (no clock read)",
+                ceiling_wave_instr_per_s=ceiling, frac=achieved_wi / ceiling,
+                kernel_frac_of_ladder_mix_profiled=(kernel_u / u) if kernel_u else None,
+                source=os.path.relpath(path, ROOT),
+                note="U = VALU wave-instructions per 4 SIMD cycles (PMC); frac = achieved / (U_ladder x SIMDs x "
+                     "clock / 4); kernel_frac_of_ladder_mix_profiled = the profiled launch's U / U_ladder")
 
 
 def timed_steps(step, steps, warmup, device, barrier, counter=None):
@@ -949,7 +969,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layout-probe", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--no-pinned", action="store_true", help="skip the pinned-table leg (cudasp_pinned_*, tools/host_e2e --pinned)")
+    ap.add_argument("--pinned", action="store_true",
+                    help="also run the pinned and resident table legs (cudasp_pinned_*, tools/host_e2e --pinned; "
+                         "an API beside the reference's interface, off by default)")
+    ap.add_argument("--no-pinned", action="store_true", help=argparse.SUPPRESS)  # the default since round 6
     ap.add_argument("--no-e2e-launch", action="store_true",
                     help="skip the second end-to-end leg with the host's per-slot launches (CUDASP_TF_MODE=launch)")
     ap.add_argument("--e2e-threads", type=int, default=0,
@@ -962,15 +985,13 @@ def main():
     ap.add_argument("--idle-samples", type=int, default=3,
                     help="device-resident steps each after 100 ms of GPU idle (device_after_idle); 0 = none")
     ap.add_argument("--pmc-summary", default="",
-                    help="HBM traffic summary (default: profiles/r03_pmc_hbm_multi.json with --launch multi, "
-                         "profiles/r02_pmc_hbm_k_shared_secret.json with --launch batches)")
-    ap.add_argument("--pmc-sq", default="", help="SQ counter summary (default: the file matching this run's shape)")
+                    help="HBM traffic summary (default: the newest profiles/r0N_pmc_hbm_multi.json measured on the "
+                         "loaded kernel's machine code); a summary of other machine code is never used")
+    ap.add_argument("--pmc-sq", default="", help="SQ counter summary (default: the newest file matching this run's "
+                    "shape and the loaded kernel's machine code)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) for the barrier/max; gloo to rehearse "
                     "several ranks on one GPU")
     args = ap.parse_args()
-    if not args.pmc_summary:
-        args.pmc_summary = os.path.join(ROOT, "profiles", "r03_pmc_hbm_multi.json" if args.launch == "multi"
-                                        else "r02_pmc_hbm_k_shared_secret.json")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -1073,11 +1094,32 @@ def main():
     # the timed region).  Both modes also report the per-batch kernels alone.
     excl = exclusive_launches(tab, scanners[0], streams[0], args.exclusive_batches)
     mean_k = tab.total_outputs / max(1, tab.rows)
+    # Counters are read only from summaries stamped with the machine code of
+    # the kernel this process loaded (tools/codeobj.py): the timed kernel's
+    # instance, k_scan_multi<fb_bits, pipelined> or stage A's k_shared_secret<4>.
+    lib_path = os.environ.get("CUDASP_LIB") or _native.LIB_PATH
+    skey = "k_scan_multi" if multi else "k_shared_secret"
+    spat = codeobj.multi_pattern(args.fb_bits) if multi else r"^_Z15k_shared_secretILi4EE"
+    try:
+        stamp = codeobj.kernel_stamp(lib_path, spat)["sha256"]
+        probe_stamp = codeobj.kernel_stamp(lib_path, codeobj.K_LAYOUT_PROBE)["sha256"]
+    except (OSError, ValueError) as e:
+        stamp = probe_stamp = None
+        print("bench: no code stamp (%s): counters unused" % e, file=sys.stderr)
+
+    def summary(explicit, name):
+        if explicit:
+            with open(explicit) as f:
+                d = json.load(f)
+            st = ((d.get("code_stamp") or {}).get(skey) or {}).get("sha256")
+            if stamp and st == stamp:
+                return explicit, d, None
+            return None, None, "%s: stamp %s, loaded %s %s" % (explicit, st or "none", skey, stamp)
+        return stamped_summary(name, skey, stamp)
+
+    hbm_path, pmc, traffic_why = summary(args.pmc_summary, "pmc_hbm_multi" if multi else "pmc_hbm_k_shared_secret")
+    pmc = pmc or {}
     traffic = None
-    pmc = {}
-    if os.path.exists(args.pmc_summary):
-        with open(args.pmc_summary) as f:
-            pmc = json.load(f)
     if multi:
         spans = [e0.elapsed_time(e1) for e0, e1 in events]
         kernel, kernel_ms, rows_per_launch, launches = "k_scan_multi", float(np.mean(spans)), float(tab.rows), 1
@@ -1105,8 +1147,11 @@ def main():
     ms_per_step = total_s / args.steps * 1e3
     rows_gpu_step = rows_job / world
     step_gbs = bytes_per_row(mean_k) * rows_gpu_step / (ms_per_step * 1e-3) / 1e9
-    sq_path = args.pmc_sq or sq_profile_path(args)
-    alu = alu_roofline(sq_path, value / world, multi)
+    sq_path, sq, sq_why = summary(args.pmc_sq, sq_profile_name(args))
+    if sq is None:
+        alu = dict(bound="valu", error=sq_why, code_stamp=stamp)
+    else:
+        alu = alu_roofline(sq, sq_path, value / world, multi, clock["shader_mhz"] if clock else None, stamp)
 
     result = dict(
         metric=METRIC, value=value, unit="tx/s", n_gpus=world, steps=args.steps, warmup=args.warmup,
@@ -1128,6 +1173,8 @@ def main():
         roofline=dict(bound="hbm", achieved=achieved_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                       frac=achieved_gbs / HBM_PEAK_GBS, traffic=traffic,
                       traffic_ratio=(traffic / algo_bytes) if traffic else None,
+                      traffic_source=os.path.relpath(hbm_path, ROOT) if hbm_path else None,
+                      traffic_null_reason=None if traffic else traffic_why, code_stamp=stamp,
                       traffic_counts=("2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 --pmc derived counters, the "
                                       "MI355X_MICROARCH.md gfx950 correction) per launch: L2-to-fabric traffic, so "
                                       "MALL (Infinity Cache) hits are included -- an upper bound on HBM bytes; the "
@@ -1152,10 +1199,10 @@ def main():
         result["clock"] = clock
     if not args.no_layout_probe:
         result["layout_probe"] = layout_probe(lib, tab)
-        if os.path.exists(args.pmc_summary) and not args.outputs_max and args.outputs_per_row == 2:
-            # the PMC pass profiles the probe at 2 outputs per row (tools/gpu_measure.sh)
-            with open(args.pmc_summary) as f:
-                probe_traffic = json.load(f).get("probe_hbm_bytes_per_row")
+        probe_ok = ((pmc.get("code_stamp") or {}).get("k_layout_probe") or {}).get("sha256") == probe_stamp
+        if pmc and probe_ok and not args.outputs_max and args.outputs_per_row == 2:
+            # the PMC pass profiles the probe at 2 outputs per row (tools/recipes/pmc.sh)
+            probe_traffic = pmc.get("probe_hbm_bytes_per_row")
             if probe_traffic:
                 result["layout_probe"]["traffic_per_row"] = probe_traffic
                 result["layout_probe"]["traffic_ratio"] = probe_traffic / (result["layout_probe"]["algorithmic_bytes"]
@@ -1236,7 +1283,7 @@ def main():
                 el = e2e_leg(args, labels, world, args.fb_bits, mode="launch")
                 result["e2e_launch"] = el
                 result["e2e_launch_tx_s"] = el.get("tx_per_s")
-            if not args.no_pinned and args.fb_bits in (0, 26) and args.rows <= 40_000_000:
+            if args.pinned and args.fb_bits in (0, 26) and args.rows <= 40_000_000:
                 # (the child rebuilds the table in host memory: bounded to config-4 sizes)
                 # the table pinned once and scanned in place: no host copy per query
                 pn = pinned_leg(args, labels, world)

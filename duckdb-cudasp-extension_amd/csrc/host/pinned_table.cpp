@@ -51,9 +51,17 @@ constexpr uint64_t MAX_WORDS = 0xFFFFFFFFu;  // a batch's outputs: u32 offsets
 //                                     a scan fails with CUDASP_ERR_NO_DEVICE)
 //   CUDASP_PINNED_TEST_MAX_WORDS=w    a batch's outputs capped at w words
 //                                     instead of 2^32 - 1 (the early close)
+//   CUDASP_PINNED_TEST_SEAL_FAIL=k    the table's k-th batch close (1-based)
+//                                     fails as an allocation would (the
+//                                     append's rollback)
 bool env_null_device() {
   const char* e = getenv("CUDASP_TF_NULL_DEVICE");
   return e && atoi(e) == 1;
+}
+uint64_t env_seal_fail() {
+  const char* e = getenv("CUDASP_PINNED_TEST_SEAL_FAIL");
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? (uint64_t)v : 0;
 }
 uint64_t env_max_words() {
   const char* e = getenv("CUDASP_PINNED_TEST_MAX_WORDS");
@@ -151,6 +159,7 @@ struct cudasp_pinned_table {
   std::vector<uint32_t*> d_counts;  // HBM: per logical GPU, one match count per batch
   std::vector<size_t> counts_cap;
   uint64_t max_words = MAX_WORDS;
+  uint64_t seals = 0, seal_fail_at = 0;  // test hook CUDASP_PINNED_TEST_SEAL_FAIL
   uint64_t last_matches = 0;
   double last_scan_s = 0, last_publish_s = 0;
   mutable std::mutex mu;
@@ -229,6 +238,9 @@ int seal(cudasp_pinned_table& t) {
   Staging& s = t.open;
   const uint64_t n = s.n();
   if (n == 0) return CUDASP_OK;
+  if (t.seal_fail_at && ++t.seals == t.seal_fail_at)
+    return fail(CUDASP_ERR_CAPACITY, "pinned table: batch close %llu failed (CUDASP_PINNED_TEST_SEAL_FAIL)",
+                (unsigned long long)t.seals);
   Batch b;
   b.n = (uint32_t)n;
   b.words = s.outputs.size();
@@ -451,6 +463,7 @@ int cudasp_pinned_create_placed(uint64_t batch_size, const int* devices, uint32_
   t->host_only = host_only;
   t->hbm = placement == CUDASP_TABLE_HBM;
   t->max_words = env_max_words();
+  t->seal_fail_at = env_seal_fail();
   if (devices)
     t->devices.assign(devices, devices + device_count);
   else
@@ -516,14 +529,59 @@ int cudasp_pinned_append(cudasp_pinned_table* t, const cudasp_tf_columns* cols) 
     if (bit(c.list_validity, c.list_offset + i) && lo[i + 1] > lo[i] && !c.child_values)
       return fail(CUDASP_ERR_INVALID_ARG, "pinned tables take int64 outputs (child_values)");
   }
+  // All or nothing: a batch close that fails (allocation, upload) undoes the
+  // whole run -- the batches closed during it are freed and the open batch
+  // is restored to its state at entry -- so the input numbers handed out stay
+  // t->appended + i of a run that was kept, and a retried run is numbered
+  // the same.  The rows that were open at entry leave the staging at the
+  // run's first close; that prefix is kept until the run succeeds.
   Staging& s = t->open;
+  const size_t nb0 = t->batches.size();
+  const uint64_t n0 = s.n(), w0 = s.outputs.size();
+  const bool dense0 = s.dense;
+  const uint64_t rows0 = t->pinned_rows, pbytes0 = t->pinned_bytes, dbytes0 = t->device_bytes;
+  Staging entry;  // the entry prefix, once the first close took it away
+  bool closed = false;
+  auto close = [&]() -> int {
+    if (!closed && n0) {
+      entry.rows.assign(s.rows.begin(), s.rows.begin() + n0 * TWEAK_KEY_SIZE);
+      entry.outputs.assign(s.outputs.begin(), s.outputs.begin() + w0);
+      entry.offsets.assign(s.offsets.begin(), s.offsets.begin() + n0 + 1);
+      entry.ord.assign(s.ord.begin(), s.ord.begin() + n0);
+      entry.dense = dense0;
+    }
+    const int rc = seal(*t);
+    if (rc == CUDASP_OK) closed = true;
+    return rc;
+  };
+  auto rollback = [&](int rc) -> int {
+    const std::string msg = cudasp_last_error();
+    while (t->batches.size() > nb0) {
+      free_batch(t->batches.back());
+      t->batches.pop_back();
+    }
+    t->pinned_rows = rows0;
+    t->pinned_bytes = pbytes0;
+    t->device_bytes = dbytes0;
+    if (closed) {
+      s = std::move(entry);
+      if (!n0) reset_staging(*t);
+    } else {
+      s.rows.resize(n0 * TWEAK_KEY_SIZE);
+      s.outputs.resize(w0);
+      s.offsets.resize(n0 + 1);
+      s.ord.resize(n0);
+      s.dense = dense0;
+    }
+    return fail(rc, "%s (the run of %llu rows was not appended)", msg.c_str(), (unsigned long long)n);
+  };
   for (uint64_t i = 0; i < n; i++) {
     if (!row_ok(i)) continue;
     const bool lv = bit(c.list_validity, c.list_offset + i);
     const uint64_t len = lv ? (uint64_t)(lo[i + 1] - lo[i]) : 0;
     if (s.n() && s.outputs.size() + len > t->max_words) {  // keep u32 offsets: close the batch early
-      const int rc = seal(*t);
-      if (rc != CUDASP_OK) return rc;
+      const int rc = close();
+      if (rc != CUDASP_OK) return rollback(rc);
     }
     const uint64_t num = t->appended + i;
     if (s.n() && num != s.ord[0] + s.n()) s.dense = false;
@@ -541,8 +599,8 @@ int cudasp_pinned_append(cudasp_pinned_table* t, const cudasp_tf_columns* cols) 
     }
     s.offsets.push_back((uint32_t)s.outputs.size());
     if (s.n() == t->batch_size) {
-      const int rc = seal(*t);
-      if (rc != CUDASP_OK) return rc;
+      const int rc = close();
+      if (rc != CUDASP_OK) return rollback(rc);
     }
   }
   t->appended += n;

@@ -93,13 +93,10 @@ def load(path=None):
         raise CudaspError(CUDASP_ERR_NO_DEVICE,
                           "HIP library %s not built (run `make -C duckdb-cudasp-extension_amd` "
                           "or __graft_entry__.build())" % p)
-    # torch first: it ships its own HIP runtime (torch/lib/libamdhip64.so),
-    # and the library's libamdhip64.so.7 dependency binds to whichever runtime
-    # of that soname is loaded first.  Loaded before torch, the library pulls
-    # in /opt/rocm's, and torch then finds no GPU in the process ("No HIP GPUs
-    # are available" after a NativePinnedTable, tools/probes/init_order.py);
-    # loaded after, both share torch's.
-    import torch  # noqa: F401
+    # No import order to keep: the library names the HIP runtime by the file
+    # name torch's libraries use (DT_NEEDED libamdhip64.so, see the Makefile),
+    # so it and torch share one runtime whichever loads first
+    # (tools/probes/init_order.py, tests/test_init_order_gpu.py).
     lib = ctypes.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -76,3 +76,63 @@ def test_prepared_device_batches_match_the_abi_struct():
     assert {k: getattr(b0, k) for k in names} == want
     assert getattr(prep.array[1], names[5]) == 7
     assert len(Scanner.device_batches([]).array) == 1 and Scanner.device_batches([]).count == 0
+
+
+def _dt_needed(path):
+    """DT_NEEDED names of an ELF64 shared object."""
+    import struct
+    d = open(path, "rb").read()
+    shoff, = struct.unpack_from("<Q", d, 0x28)
+    shentsize, shnum, _ = struct.unpack_from("<HHH", d, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", d, shoff + i * shentsize) for i in range(shnum)]
+    out = []
+    for name, typ, flags, addr, off, size, link, info, align, entsize in secs:
+        if typ != 6:  # SHT_DYNAMIC
+            continue
+        stroff = secs[link][4]
+        for i in range(size // 16):
+            tag, val = struct.unpack_from("<qQ", d, off + 16 * i)
+            if tag == 1:  # DT_NEEDED
+                out.append(d[stroff + val:d.index(b"\0", stroff + val)].decode())
+    return out
+
+
+def test_library_names_the_hip_runtime_like_torch():
+    """The library depends on the HIP runtime by its unversioned file name,
+    the name torch's libraries use, so both bind one runtime in either load
+    order (Makefile, HIPRT_LINK)."""
+    from cudasp_amd import _native
+    needed = _dt_needed(_native.LIB_PATH)
+    assert "libamdhip64.so" in needed, needed
+    assert "libamdhip64.so.7" not in needed, needed
+
+
+_MAPS_PROBE = r"""
+import ctypes, os, sys
+sys.path.insert(0, %r)
+order = sys.argv[1]
+if order == "torch-first":
+    import torch
+from cudasp_amd import _native
+_native.load()
+if order == "lib-first":
+    import torch
+    torch.cuda.device_count()
+maps = {l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l}
+print(sorted({os.path.realpath(m) for m in maps}))
+"""
+
+
+@pytest.mark.parametrize("order", ["lib-first", "torch-first"])
+def test_one_hip_runtime_in_either_load_order(order):
+    """A process that loads the library before torch (a DuckDB host, a
+    NativePinnedTable) and one that imports torch first both map exactly one
+    HIP runtime file."""
+    import ast
+    import subprocess
+    import sys
+    pkg = os.path.join(ROOT, "duckdb-cudasp-extension_amd")
+    r = subprocess.run([sys.executable, "-c", _MAPS_PROBE % pkg, order], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    files = ast.literal_eval(r.stdout.strip().splitlines()[-1])
+    assert len(files) == 1, files

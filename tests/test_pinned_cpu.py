@@ -144,3 +144,51 @@ def test_native_pinned_argument_errors(monkeypatch):
             assert b"full_x" in _native.load().cudasp_last_error()
         finally:
             lib.cudasp_pinned_free(h)
+
+
+@pytest.mark.parametrize("fail_at", [1, 2, 3])
+def test_native_pinned_append_rolls_back_a_failed_close(monkeypatch, fail_at):
+    """A batch close that fails inside cudasp_pinned_append (allocation or
+    upload; forced here by CUDASP_PINNED_TEST_SEAL_FAIL) undoes the whole run:
+    the counters return to their values before it, and retrying the run gives
+    exactly the table appended without a failure -- no input number is handed
+    out twice."""
+    import ctypes
+
+    from cudasp_amd import _native
+    from cudasp_amd.table_function import _PinnedInfo, _arrow_pieces, _columns, _lib
+    monkeypatch.setenv("CUDASP_TF_NULL_DEVICE", "1")
+    lib = _lib()
+    pieces = _arrow_pieces(_native_table(1000), 230)  # runs of 230 rows, batches of 100 (non-NULL rows)
+
+    def info(h):
+        inf = _PinnedInfo()
+        _native.check(lib.cudasp_pinned_info(h, ctypes.byref(inf)))
+        return (inf.rows_appended, inf.rows_pinned, inf.batches, inf.pinned_bytes)
+
+    def build(fail):
+        if fail:
+            monkeypatch.setenv("CUDASP_PINNED_TEST_SEAL_FAIL", str(fail))
+        else:
+            monkeypatch.delenv("CUDASP_PINNED_TEST_SEAL_FAIL", raising=False)
+        h = ctypes.c_void_p()
+        _native.check(lib.cudasp_pinned_create(100, None, 0, ctypes.byref(h)))
+        failed = 0
+        for p in pieces:
+            before = info(h)
+            rc = lib.cudasp_pinned_append(h, ctypes.byref(_columns(*p)))
+            if rc != _native.CUDASP_OK:
+                assert rc == _native.CUDASP_ERR_CAPACITY and b"not appended" in _native.load().cudasp_last_error()
+                assert info(h) == before
+                failed += 1
+                _native.check(lib.cudasp_pinned_append(h, ctypes.byref(_columns(*p))))  # the retry
+        return h, failed
+
+    ref, nf = build(0)
+    got, failed = build(fail_at)
+    try:
+        assert nf == 0 and failed == 1
+        assert info(got) == info(ref)
+    finally:
+        lib.cudasp_pinned_free(ref)
+        lib.cudasp_pinned_free(got)

@@ -42,11 +42,62 @@ def test_committed_profiles_have_bench_keys():
     assert per["k_layout_probe"]["FETCH_SIZE_KiB_per_launch"] > 0
 
 
+def _lib_path():
+    return os.path.join(ROOT, "duckdb-cudasp-extension_amd", "libcudasp_amd.so")
+
+
+def _codeobj():
+    spec = importlib.util.spec_from_file_location("codeobj", os.path.join(ROOT, "tools", "codeobj.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_code_stamp_names_one_kernel():
+    """tools/codeobj.py finds the bench's timed kernel in the library's gfx950
+    code object, and the stamp is a function of its machine code only."""
+    import pytest
+    co = _codeobj()
+    if not os.path.exists(_lib_path()):
+        pytest.skip("library not built")
+    a = co.kernel_stamp(_lib_path(), co.multi_pattern(26))
+    assert a["symbol"].startswith("_Z12k_scan_multiILi26ELb1EE") and a["code_bytes"] > 10000
+    assert co.kernel_stamp(_lib_path(), co.multi_pattern(26)) == a
+    b = co.kernel_stamp(_lib_path(), co.multi_pattern(22))
+    assert b["sha256"] != a["sha256"]
+    with pytest.raises(ValueError):
+        co.kernel_stamp(_lib_path(), r"^_Z12k_scan_multi")  # several instances
+
+
+def test_committed_counters_match_the_built_kernel():
+    """bench.py reads roofline traffic and VALU counts only from summaries
+    stamped with the loaded kernel's machine code.  The tree must carry such
+    summaries for the default shapes (config 4, config 3, the config-5 shape)
+    and the ladder-mix ceiling: a change to k_scan_multi<26,true> without new
+    PMC passes (tools/recipes/pmc.sh) fails here instead of reporting stale
+    counters."""
+    import glob
+    import json
+    import pytest
+    co = _codeobj()
+    if not os.path.exists(_lib_path()):
+        pytest.skip("library not built")
+    want = co.kernel_stamp(_lib_path(), co.multi_pattern(26))["sha256"]
+    for name in ("pmc_hbm_multi", "pmc_sq_multi_L0_k2_w26", "pmc_sq_multi_L1_k2_w26", "pmc_sq_multi_L16_k1-15_w26",
+                 "valu_ceiling"):
+        stamps = []
+        for p in glob.glob(os.path.join(ROOT, "profiles", "r0*_%s.json" % name)):
+            d = json.load(open(p))
+            stamps.append(((d.get("code_stamp") or {}).get("k_scan_multi") or {}).get("sha256"))
+        assert want in stamps, (name, want, stamps)
+
+
 def test_committed_multi_profiles_have_bench_keys():
-    """The summaries bench.py reads by default with --launch multi (the
-    default): k_scan_multi's VALU count per launch with its rows, and its HBM
-    traffic per row."""
-    sq = json.load(open(os.path.join(ROOT, "profiles", "r03_pmc_sq_multi_L0_k2_w26.json")))
-    assert sq["per_kernel"]["k_scan_multi"]["SQ_INSTS_VALU"] > 0 and sq["multi_rows_per_launch"] > 0
-    hbm = json.load(open(os.path.join(ROOT, "profiles", "r03_pmc_hbm_multi.json")))
-    assert hbm["multi_hbm_bytes_per_row"] > 0
+    """The newest summaries bench.py reads with --launch multi (the default):
+    k_scan_multi's VALU count and GRBM cycles per launch with its rows, and
+    its HBM traffic per row."""
+    sq = json.load(open(os.path.join(ROOT, "profiles", "r06_pmc_sq_multi_L0_k2_w26.json")))
+    k = sq["per_kernel"]["k_scan_multi"]
+    assert k["SQ_INSTS_VALU"] > 0 and k["GRBM_GUI_ACTIVE"] > 0 and sq["multi_rows_per_launch"] == 32_700_000
+    hbm = json.load(open(os.path.join(ROOT, "profiles", "r06_pmc_hbm_multi.json")))
+    assert hbm["multi_hbm_bytes_per_row"] > 0 and hbm["probe_hbm_bytes_per_row"] > 0

@@ -3,6 +3,11 @@ profiles/ that bench.py reads.
 
   python tools/pmc_summary.py sq   OUT.json  CSV [CSV ...]   # SQ_* / GRBM_* averages per dispatch
   python tools/pmc_summary.py hbm  OUT.json  FETCH_CSV WRITE_CSV --rows N
+  ... --stamp-lib LIB --stamp k_scan_multi=REGEX   # stamp the kernels' machine code
+
+With --stamp-lib, `code_stamp` records the SHA-256 of each named kernel's
+machine code in the library the run loaded (tools/codeobj.py); bench.py uses a
+summary only while the loaded library's kernel has the same stamp.
 
 `sq`: per kernel, the average of every counter per dispatch (dispatches with the
 largest grid only for the scan kernels, so partial batches do not dilute).
@@ -20,7 +25,11 @@ import argparse
 import collections
 import csv
 import json
+import os
 import re
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 SCAN_KERNELS = ("k_shared_secret", "void k_match<false>", "void k_match<true>", "k_layout_probe", "k_scan_multi")
 
@@ -82,6 +91,10 @@ def main():
     ap.add_argument("--probe-outputs-per-row", type=float, default=2.0)
     ap.add_argument("--multi-rows", type=int, default=0,
                     help="rows of one k_scan_multi launch (cudasp_scan_device_batches) in the profiled run")
+    ap.add_argument("--stamp-lib", default="", help="the library the profiled run loaded: its kernels' machine "
+                    "code is stamped into the summary (tools/codeobj.py) so bench.py can refuse stale counters")
+    ap.add_argument("--stamp", action="append", default=[], metavar="KEY=REGEX",
+                    help="kernel to stamp, e.g. k_scan_multi=^_Z12k_scan_multiILi26ELb1EE (repeatable)")
     a = ap.parse_args()
     if a.mode == "sq":
         res = dict(source=a.source, shape=a.shape, rows_per_launch=a.rows, per_kernel=averages(load(a.csvs)))
@@ -115,6 +128,10 @@ def main():
             res.update(probe_rows=a.probe_rows, probe_read_bytes=read, probe_write_bytes=a.probe_rows,
                        probe_fetch_calibration=read / raw if raw else None,
                        probe_hbm_bytes_per_row=hbm("k_layout_probe") / a.probe_rows)
+    if a.stamp_lib:
+        import codeobj
+        res["code_stamp"] = {key: codeobj.kernel_stamp(a.stamp_lib, rx)
+                             for key, rx in (x.split("=", 1) for x in a.stamp)}
     json.dump(res, open(a.out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "per_kernel"}, indent=1))
     for k in SCAN_KERNELS:

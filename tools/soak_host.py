@@ -1,5 +1,5 @@
-"""Randomized soak of the table-function host on the GPU box (measurement and
-robustness only, not a test the driver runs).
+"""Randomized soak of the table-function host on the GPU box (robustness;
+a shortened seeded form runs in the GPU suite, tests/test_soak_gpu.py).
 
 For a wall-clock budget it runs tools/host_e2e on seeded random query shapes:
 table size, executor threads, batch_size (down to a few rows: many slots and
@@ -14,6 +14,10 @@ oracle (oracle.check_planted_sample, checker use of oracle/).  Prints one line
 per run and a JSON summary; exit 1 on the first failure.
 
   python tools/soak_host.py --minutes 8 --seed 1 --out gpurun_out/soak.jsonl
+
+tests/test_soak_gpu.py runs a seeded one-minute form in the GPU suite
+(streaming feeds with 4 slots, the shape that lost matches to stale cached
+slots in round 5).
 """
 import argparse
 import json
@@ -56,6 +60,10 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default="")
     ap.add_argument("--timeout", type=int, default=240, help="seconds per run")
+    ap.add_argument("--mode", default=None, choices=["", "stream", "launch"],
+                    help="fix the host mode for every run (default: random)")
+    ap.add_argument("--slots", default=None, help="fix CUDASP_TF_STREAM_SLOTS for every run (default: random)")
+    ap.add_argument("--max-rows", type=int, default=0, help="cap every run's table (0 = no cap)")
     a = ap.parse_args()
     import bench
     from oracle import oracle
@@ -66,6 +74,12 @@ def main():
     out = open(a.out, "w") if a.out else None
     while time.time() < t_end:
         sh = shape(rng)
+        if a.mode is not None:
+            sh["mode"] = a.mode
+        if a.slots is not None:
+            sh["slots"] = a.slots
+        if a.max_rows:
+            sh["rows"] = min(sh["rows"], a.max_rows)
         # tiny batches on big tables take many slot cycles, K indices K x stage B:
         # keep a run bounded
         if sh["batch"] < 2048 and sh["rows"] > 65536:

@@ -114,6 +114,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--json", default="")
+    ap.add_argument("--stamp-lib", default="", help="the library the scan passes loaded: stamp k_scan_multi's "
+                    "machine code into the JSON (tools/codeobj.py)")
+    ap.add_argument("--fb-bits", type=int, default=26)
     a = ap.parse_args()
     d = a.dir
     out = {}
@@ -142,7 +145,7 @@ def main():
         u_ladder = tot / sum(n / gu[(op, 3)] for n, op in LADDER)
         print("ladder mix at 3 waves/SIMD (126 dbl x 893 + 39 madd x 1576 VALU): U %.3f" % u_ladder)
     out["ladder_mix_U"] = u_ladder
-    for L in (0, 16):
+    for L in (0, 1, 16):
         sc = analyse(counters(d + "/scan_sq_L%d/*counter_collection.csv" % L),
                      counters(d + "/scan_grbm_L%d/*counter_collection.csv" % L),
                      durations(d + "/scan_kt_L%d/*kernel_trace.csv" % L), skip_first=False)
@@ -162,6 +165,9 @@ def main():
                                            mix_ceiling_wave_instr_per_s=ceiling,
                                            mix_ceiling_at_peak_clock=(ceiling * PEAK_HZ / f) if (ceiling and f) else None,
                                            valu_per_dispatch=r["valu"], seconds=r.get("seconds"))
+    if a.stamp_lib:
+        import codeobj
+        out["code_stamp"] = dict(k_scan_multi=codeobj.kernel_stamp(a.stamp_lib, codeobj.multi_pattern(a.fb_bits)))
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(out, fh, indent=1)
