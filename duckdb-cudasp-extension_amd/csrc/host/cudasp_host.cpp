@@ -1160,27 +1160,107 @@ int next_feed_index(const cudasp_tf_global& g, cudasp_tf_local& l) {
   return g.num_gpus > 1 ? (int)((l.assigned_gpu + c) % (uint64_t)g.num_gpus) : 0;
 }
 
+// Row access for the two per-chunk input forms.  ChunkRows: cudasp_tf_chunk,
+// DuckDB's unified form unpacked by the caller into per-row pointers, sizes
+// and byte validity.  VectorRows: cudasp_tf_vectors, DuckDB's vectors as they
+// are (16-byte string_t, selection vectors, 64-bit validity words,
+// list_entry_t), so the extension passes pointers and nothing is marshalled
+// per row before the slot copy.  Element k of the outputs child is addressed
+// by list_offset + position in both forms (the child's own selection vector,
+// if any, applies on top).
+struct ChunkRows {
+  const cudasp_tf_chunk& c;
+  uint32_t count() const { return c.count; }
+  bool dense() const { return !c.txid_valid && !c.height_valid && !c.tweak_valid && !c.list_valid && !c.child_valid; }
+  bool row_ok(uint32_t i) const {
+    return valid(c.txid_valid, i) && valid(c.height_valid, i) && valid(c.tweak_valid, i);
+  }
+  uint32_t txid_size(uint32_t i) const { return c.txid_size[i]; }
+  const uint8_t* txid(uint32_t i) const { return c.txid_data[i]; }
+  uint32_t tweak_size(uint32_t i) const { return c.tweak_size[i]; }
+  const uint8_t* tweak(uint32_t i) const { return c.tweak_data[i]; }
+  int32_t height(uint32_t i) const { return c.height[i]; }
+  const int32_t* heights() const { return c.height; }  // the chunk's heights back to back
+  bool list_ok(uint32_t i) const { return valid(c.list_valid, i); }
+  uint64_t list_offset(uint32_t i) const { return c.list_offset[i]; }
+  uint64_t list_length(uint32_t i) const { return c.list_length[i]; }
+  bool child_ok(uint64_t k) const { return valid(c.child_valid, k); }
+  int64_t child_value(uint64_t k) const { return c.child_values[k]; }
+  const int64_t* child_values() const { return c.child_values; }  // element k at [k]
+  bool has_child_blobs() const { return c.child_blob_data && c.child_blob_size; }
+  const uint8_t* child_blob(uint64_t k, uint32_t* size) const {
+    *size = c.child_blob_size[k];
+    return c.child_blob_data[k];
+  }
+};
+
+struct VectorRows {
+  const cudasp_tf_vectors& v;
+  static uint64_t at(const cudasp_tf_vector& x, uint64_t i) { return x.sel ? x.sel[i] : i; }
+  static bool ok(const cudasp_tf_vector& x, uint64_t i) {
+    if (!x.validity) return true;
+    const uint64_t j = at(x, i);
+    return (x.validity[j >> 6] >> (j & 63)) & 1u;
+  }
+  static const cudasp_tf_string& str(const cudasp_tf_vector& x, uint64_t i) {
+    return static_cast<const cudasp_tf_string*>(x.data)[at(x, i)];
+  }
+  static const uint8_t* bytes(const cudasp_tf_string& s) {
+    return s.length <= CUDASP_TF_STRING_INLINE ? s.prefix : s.ptr;  // inline bytes start at prefix
+  }
+  uint32_t count() const { return v.count; }
+  bool dense() const {
+    return !v.txid.validity && !v.height.validity && !v.tweak.validity && !v.outputs.validity && !v.child.validity;
+  }
+  bool row_ok(uint32_t i) const { return ok(v.txid, i) && ok(v.height, i) && ok(v.tweak, i); }
+  uint32_t txid_size(uint32_t i) const { return str(v.txid, i).length; }
+  const uint8_t* txid(uint32_t i) const { return bytes(str(v.txid, i)); }
+  uint32_t tweak_size(uint32_t i) const { return str(v.tweak, i).length; }
+  const uint8_t* tweak(uint32_t i) const { return bytes(str(v.tweak, i)); }
+  int32_t height(uint32_t i) const { return static_cast<const int32_t*>(v.height.data)[at(v.height, i)]; }
+  const int32_t* heights() const { return v.height.sel ? nullptr : static_cast<const int32_t*>(v.height.data); }
+  const cudasp_tf_list_entry& list(uint32_t i) const {
+    return static_cast<const cudasp_tf_list_entry*>(v.outputs.data)[at(v.outputs, i)];
+  }
+  bool list_ok(uint32_t i) const { return ok(v.outputs, i); }
+  uint64_t list_offset(uint32_t i) const { return list(i).offset; }
+  uint64_t list_length(uint32_t i) const { return list(i).length; }
+  bool child_ok(uint64_t k) const { return ok(v.child, k); }
+  int64_t child_value(uint64_t k) const { return static_cast<const int64_t*>(v.child.data)[at(v.child, k)]; }
+  const int64_t* child_values() const { return v.child.sel ? nullptr : static_cast<const int64_t*>(v.child.data); }
+  bool has_child_blobs() const { return v.child.data != nullptr; }
+  const uint8_t* child_blob(uint64_t k, uint32_t* size) const {
+    const cudasp_tf_string& s = str(v.child, k);
+    *size = s.length;
+    return bytes(s);
+  }
+};
+
 // AccumulateInput (src/cudasp_extension.cu:154-224) for one DuckDB chunk:
 // count and validate the rows (NULL txid/height/tweak rows skipped, NULL list
 // = no outputs, NULL elements dropped, :195-221), reserve, copy, commit.
-// A chunk without NULLs (no validity arrays) and with int64 outputs: one
-// pass to validate and count, then bulk copies where DuckDB's vectors are
-// contiguous (heights; the list children when the lists are back to back).
-int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l,
-                     const cudasp_tf_chunk& c) {
-  const uint32_t n = c.count;
+// A chunk without NULLs (no validity) and with int64 outputs: one pass to
+// validate and count, then bulk copies where DuckDB's vectors are contiguous
+// (heights; the list children when the lists are back to back).
+template <class Rows>
+int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l, const Rows& c) {
+  const uint32_t n = c.count();
   size_t nouts = 0, ntx = 0;
-  bool lists_contiguous = true;
+  const int64_t* cv = c.child_values();  // nullptr: the child vector has a selection vector
+  bool lists_contiguous = cv != nullptr;
   bool txid32 = true;
-  const uint64_t first = n ? c.list_offset[0] : 0;
+  const uint64_t first = n ? c.list_offset(0) : 0;
   for (uint32_t i = 0; i < n; i++) {
-    if (c.tweak_size[i] != TWEAK_KEY_SIZE)
-      return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", c.tweak_size[i]);
-    ntx += c.txid_size[i];
-    txid32 &= c.txid_size[i] == 32;
-    lists_contiguous &= c.list_offset[i] == first + nouts;
-    nouts += c.list_length[i];
+    if (c.tweak_size(i) != TWEAK_KEY_SIZE)
+      return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", c.tweak_size(i));
+    const uint32_t ts = c.txid_size(i);
+    ntx += ts;
+    txid32 &= ts == 32;
+    const uint64_t len = c.list_length(i);
+    lists_contiguous &= len == 0 || c.list_offset(i) == first + nouts;
+    nouts += len;
   }
+  if (nouts && !cv && !c.has_child_blobs()) return host_fail(CUDASP_ERR_INVALID_ARG, "missing outputs child values");
   Feed* f = nullptr;
   int rc = feed_for(g, b, next_feed_index(g, l), &f);
   if (rc != CUDASP_OK) return rc;
@@ -1193,7 +1273,10 @@ int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_t
   const double t1 = now_s();
   FeedSlot& s = *res.slot;
   const uint32_t r0 = res.row0;
-  memcpy(s.heights.data() + r0, c.height, (size_t)n * sizeof(int32_t));
+  if (const int32_t* h = c.heights())
+    memcpy(s.heights.data() + r0, h, (size_t)n * sizeof(int32_t));
+  else
+    for (uint32_t i = 0; i < n; i++) s.heights[r0 + i] = c.height(i);
   uint8_t* tw = s.h_tweaks + (size_t)r0 * TWEAK_KEY_SIZE;
   size_t tx = res.tx0;
   uint8_t* txb = s.txid_bytes.data();
@@ -1203,36 +1286,33 @@ int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_t
     uint8_t* tb = txb + tx;
     const bool tb16 = ((uintptr_t)tb & 15) == 0;
     for (uint32_t i = 0; i < n; i++) {
-      cudasp_host::nt_copy64(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak_data[i]);
+      cudasp_host::nt_copy64(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak(i));
       if (tb16)
-        cudasp_host::nt_copy32(tb + 32 * (size_t)i, c.txid_data[i]);
+        cudasp_host::nt_copy32(tb + 32 * (size_t)i, c.txid(i));
       else
-        memcpy(tb + 32 * (size_t)i, c.txid_data[i], 32);
+        memcpy(tb + 32 * (size_t)i, c.txid(i), 32);
     }
   } else if (nt) {
     // one pass per row: its 64-byte tweak blob, then its txid (32-byte txids
     // at 16-byte aligned offsets take non-temporal stores too)
     for (uint32_t i = 0; i < n; i++) {
-      cudasp_host::nt_copy64(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak_data[i]);
-      const uint32_t sz = c.txid_size[i];
+      cudasp_host::nt_copy64(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak(i));
+      const uint32_t sz = c.txid_size(i);
       s.txid_off[r0 + i] = tx;
       s.txid_size[r0 + i] = sz;
       if (sz == 32 && ((uintptr_t)(txb + tx) & 15) == 0)
-        cudasp_host::nt_copy32(txb + tx, c.txid_data[i]);
+        cudasp_host::nt_copy32(txb + tx, c.txid(i));
       else if (sz)
-        memcpy(txb + tx, c.txid_data[i], sz);
+        memcpy(txb + tx, c.txid(i), sz);
       tx += sz;
     }
   } else {
-    for (uint32_t i = 0; i < n; i++) memcpy(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak_data[i], TWEAK_KEY_SIZE);
+    for (uint32_t i = 0; i < n; i++) memcpy(tw + (size_t)i * TWEAK_KEY_SIZE, c.tweak(i), TWEAK_KEY_SIZE);
     for (uint32_t i = 0; i < n; i++) {
-      const uint32_t sz = c.txid_size[i];
+      const uint32_t sz = c.txid_size(i);
       s.txid_off[r0 + i] = tx;
       s.txid_size[r0 + i] = sz;
-      if (sz == 32)
-        memcpy(txb + tx, c.txid_data[i], 32);
-      else if (sz)
-        memcpy(txb + tx, c.txid_data[i], sz);
+      if (sz) memcpy(txb + tx, c.txid(i), sz);
       tx += sz;
     }
   }
@@ -1240,32 +1320,42 @@ int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_t
   if (lists_contiguous) {
     if (nouts) {
       if (nt)
-        cudasp_host::nt_copy(s.h_outputs + o, c.child_values + first, nouts * sizeof(int64_t));
+        cudasp_host::nt_copy(s.h_outputs + o, cv + first, nouts * sizeof(int64_t));
       else
-        memcpy(s.h_outputs + o, c.child_values + first, nouts * sizeof(int64_t));
+        memcpy(s.h_outputs + o, cv + first, nouts * sizeof(int64_t));
     }
+    // an empty list's offset is its position in the run, whatever DuckDB
+    // stored for it
     if (nt) {
       // through a small buffer, so the slot's offsets and lengths are
       // written non-temporally too
       uint32_t bo[CUDASP_TF_VECTOR_SIZE], bl[CUDASP_TF_VECTOR_SIZE];
+      size_t run = o;
       for (uint32_t i = 0; i < n; i++) {
-        bo[i] = (uint32_t)(o + (c.list_offset[i] - first));
-        bl[i] = (uint32_t)c.list_length[i];
+        bo[i] = (uint32_t)run;
+        bl[i] = (uint32_t)c.list_length(i);
+        run += bl[i];
       }
       cudasp_host::nt_copy(s.h_offs + r0, bo, (size_t)n * 4);
       cudasp_host::nt_copy(s.h_lens + r0, bl, (size_t)n * 4);
     } else {
+      size_t run = o;
       for (uint32_t i = 0; i < n; i++) {
-        s.h_offs[r0 + i] = (uint32_t)(o + (c.list_offset[i] - first));
-        s.h_lens[r0 + i] = (uint32_t)c.list_length[i];
+        s.h_offs[r0 + i] = (uint32_t)run;
+        s.h_lens[r0 + i] = (uint32_t)c.list_length(i);
+        run += s.h_lens[r0 + i];
       }
     }
   } else {
     for (uint32_t i = 0; i < n; i++) {
-      const uint32_t len = (uint32_t)c.list_length[i];
+      const uint32_t len = (uint32_t)c.list_length(i);
+      const uint64_t off = c.list_offset(i);
       s.h_offs[r0 + i] = (uint32_t)o;
       s.h_lens[r0 + i] = len;
-      if (len) memcpy(s.h_outputs + o, c.child_values + c.list_offset[i], (size_t)len * sizeof(int64_t));
+      if (len && cv)
+        memcpy(s.h_outputs + o, cv + off, (size_t)len * sizeof(int64_t));
+      else
+        for (uint32_t k = 0; k < len; k++) s.h_outputs[o + k] = c.child_value(off + k);
       o += len;
     }
   }
@@ -1273,31 +1363,38 @@ int feed_chunk_dense(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_t
   return feed_commit(*f, s, t1 - t0, now_s() - t1);
 }
 
-int feed_chunk(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l, const cudasp_tf_chunk& c) {
+template <class Rows>
+int feed_chunk(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_local& l, const Rows& c) {
   const size_t ow = out_words(b);
-  if (b.opt.full_x && c.count > 0 && (!c.child_blob_data || !c.child_blob_size))
+  const uint32_t count = c.count();
+  if (b.opt.full_x && count > 0 && !c.has_child_blobs())
     return host_fail(CUDASP_ERR_INVALID_ARG, "full_x needs the outputs column as BLOB[] (child_blob_data)");
-  if (!b.opt.full_x && !c.txid_valid && !c.height_valid && !c.tweak_valid && !c.list_valid && !c.child_valid)
-    return feed_chunk_dense(b, g, l, c);
+  if (!b.opt.full_x && c.dense()) return feed_chunk_dense(b, g, l, c);
   uint32_t nrows = 0;
   size_t nouts = 0, ntx = 0;
-  for (uint32_t i = 0; i < c.count; i++) {
-    if (!(valid(c.txid_valid, i) && valid(c.height_valid, i) && valid(c.tweak_valid, i))) continue;
-    if (c.tweak_size[i] != TWEAK_KEY_SIZE)
-      return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", c.tweak_size[i]);
+  for (uint32_t i = 0; i < count; i++) {
+    if (!c.row_ok(i)) continue;
+    if (c.tweak_size(i) != TWEAK_KEY_SIZE)
+      return host_fail(CUDASP_ERR_INVALID_ARG, "tweak_key must be exactly 64 bytes, got %u bytes", c.tweak_size(i));
     nrows++;
-    ntx += c.txid_size[i];
-    if (!valid(c.list_valid, i)) continue;
-    for (uint64_t k = 0; k < c.list_length[i]; k++) {
-      const uint64_t ci = c.list_offset[i] + k;
-      if (!valid(c.child_valid, ci)) continue;
-      if (b.opt.full_x && c.child_blob_size[ci] != XONLY_SIZE)
-        return host_fail(CUDASP_ERR_INVALID_ARG, "full_x outputs must be 32-byte x-only keys, got %u bytes",
-                         c.child_blob_size[ci]);
+    ntx += c.txid_size(i);
+    if (!c.list_ok(i)) continue;
+    const uint64_t off = c.list_offset(i), len = c.list_length(i);
+    for (uint64_t k = 0; k < len; k++) {
+      const uint64_t ci = off + k;
+      if (!c.child_ok(ci)) continue;
+      if (b.opt.full_x) {
+        uint32_t sz;
+        (void)c.child_blob(ci, &sz);
+        if (sz != XONLY_SIZE)
+          return host_fail(CUDASP_ERR_INVALID_ARG, "full_x outputs must be 32-byte x-only keys, got %u bytes", sz);
+      }
       nouts++;
     }
   }
   if (nrows == 0) return CUDASP_OK;
+  if (nouts && !b.opt.full_x && !c.child_values() && !c.has_child_blobs())
+    return host_fail(CUDASP_ERR_INVALID_ARG, "missing outputs child values");
   Feed* f = nullptr;
   int rc = feed_for(g, b, next_feed_index(g, l), &f);
   if (rc != CUDASP_OK) return rc;
@@ -1310,24 +1407,28 @@ int feed_chunk(const cudasp_tf_bind_data& b, cudasp_tf_global& g, cudasp_tf_loca
   uint32_t r = res.row0;
   size_t o = res.word0 / ow;  // output index
   size_t tx = res.tx0;
-  for (uint32_t i = 0; i < c.count; i++) {
-    if (!(valid(c.txid_valid, i) && valid(c.height_valid, i) && valid(c.tweak_valid, i))) continue;
+  for (uint32_t i = 0; i < count; i++) {
+    if (!c.row_ok(i)) continue;
+    const uint32_t ts = c.txid_size(i);
     s.txid_off[r] = tx;
-    s.txid_size[r] = c.txid_size[i];
-    if (c.txid_size[i]) memcpy(s.txid_bytes.data() + tx, c.txid_data[i], c.txid_size[i]);
-    tx += c.txid_size[i];
-    s.heights[r] = c.height[i];
-    memcpy(s.h_tweaks + (size_t)r * TWEAK_KEY_SIZE, c.tweak_data[i], TWEAK_KEY_SIZE);
+    s.txid_size[r] = ts;
+    if (ts) memcpy(s.txid_bytes.data() + tx, c.txid(i), ts);
+    tx += ts;
+    s.heights[r] = c.height(i);
+    memcpy(s.h_tweaks + (size_t)r * TWEAK_KEY_SIZE, c.tweak(i), TWEAK_KEY_SIZE);
     s.h_offs[r] = (uint32_t)o;
     uint32_t len = 0;
-    if (valid(c.list_valid, i)) {
-      for (uint64_t k = 0; k < c.list_length[i]; k++) {
-        const uint64_t ci = c.list_offset[i] + k;
-        if (!valid(c.child_valid, ci)) continue;
-        if (b.opt.full_x)
-          memcpy(s.h_outputs + o * ow, c.child_blob_data[ci], XONLY_SIZE);
-        else
-          s.h_outputs[o] = c.child_values[ci];
+    if (c.list_ok(i)) {
+      const uint64_t off = c.list_offset(i), ll = c.list_length(i);
+      for (uint64_t k = 0; k < ll; k++) {
+        const uint64_t ci = off + k;
+        if (!c.child_ok(ci)) continue;
+        if (b.opt.full_x) {
+          uint32_t sz;
+          memcpy(s.h_outputs + o * ow, c.child_blob(ci, &sz), XONLY_SIZE);
+        } else {
+          s.h_outputs[o] = c.child_value(ci);
+        }
         o++;
         len++;
       }
@@ -1814,9 +1915,24 @@ int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp
     return host_fail(CUDASP_ERR_INVALID_ARG, "chunk of %u rows exceeds the vector size %d", chunk->count,
                      CUDASP_TF_VECTOR_SIZE);
   if (chunk->count > 0) {
-    const int rc = feed_chunk(*b, *g, *l, *chunk);
+    const int rc = feed_chunk(*b, *g, *l, ChunkRows{*chunk});
     if (rc != CUDASP_OK) return rc;
   }
+  return CUDASP_TF_NEED_MORE_INPUT;
+}
+
+int cudasp_tf_function_vectors(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
+                               const cudasp_tf_vectors* vectors) {
+  if (!b || !g || !l || !vectors) return host_fail(CUDASP_ERR_INVALID_ARG, "null argument");
+  const cudasp_tf_vectors& v = *vectors;
+  if (v.count > CUDASP_TF_VECTOR_SIZE)
+    return host_fail(CUDASP_ERR_INVALID_ARG, "chunk of %u rows exceeds the vector size %d", v.count,
+                     CUDASP_TF_VECTOR_SIZE);
+  if (v.count == 0) return CUDASP_TF_NEED_MORE_INPUT;
+  if (!v.txid.data || !v.height.data || !v.tweak.data || !v.outputs.data)
+    return host_fail(CUDASP_ERR_INVALID_ARG, "missing column vector");
+  const int rc = feed_chunk(*b, *g, *l, VectorRows{v});
+  if (rc != CUDASP_OK) return rc;
   return CUDASP_TF_NEED_MORE_INPUT;
 }
 

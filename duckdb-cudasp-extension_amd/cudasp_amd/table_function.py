@@ -50,6 +50,20 @@ class _Chunk(ctypes.Structure):
     ]
 
 
+class _Vector(ctypes.Structure):
+    """cudasp_tf_vector (include/cudasp_host.h): a DuckDB UnifiedVectorFormat."""
+    _fields_ = [("data", ctypes.c_void_p), ("sel", ctypes.c_void_p), ("validity", ctypes.c_void_p)]
+
+
+class _Vectors(ctypes.Structure):
+    """cudasp_tf_vectors (include/cudasp_host.h)."""
+    _fields_ = [("count", ctypes.c_uint32), ("txid", _Vector), ("height", _Vector), ("tweak", _Vector),
+                ("outputs", _Vector), ("child", _Vector)]
+
+
+STRING_INLINE = 12  # string_t::INLINE_LENGTH
+
+
 class _Output(ctypes.Structure):
     _fields_ = [
         ("count", ctypes.c_uint32),
@@ -148,6 +162,7 @@ _HOST_SIGNATURES = {
     "cudasp_tf_release_pool": (None, []),
     "cudasp_tf_pool_size": (ctypes.c_uint32, []),
     "cudasp_tf_function": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Chunk)]),
+    "cudasp_tf_function_vectors": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Vectors)]),
     "cudasp_tf_final": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Output)]),
     "cudasp_tf_function_columns": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Columns)]),
     "cudasp_tf_get_stats": (ctypes.c_int, [_P, ctypes.POINTER(_Stats)]),
@@ -289,6 +304,74 @@ def _make_chunk(rows, full_x=False):
     return keep, c
 
 
+def _make_vectors(rows, full_x=False, rng=None):
+    """DuckDB's vectors for Python rows (cudasp_tf_vectors), as a DataChunk
+    holds them: 16-byte string_t (bytes inline up to 12, else prefix +
+    pointer), int32 heights, list_entry_t lists into one child vector, 64-bit
+    validity words.  With `rng` (a numpy Generator) every vector -- the child
+    too -- is stored in a shuffled physical order behind a selection vector,
+    as a dictionary or filtered vector reaches an operator.  Returns (keep,
+    vectors)."""
+    import numpy as np
+    n = len(rows)
+    keep = []
+
+    def perm(m):
+        return rng.permutation(m).astype(np.uint32) if rng is not None else None
+
+    def vec(values, ok, kind):
+        """(data, sel, validity) arrays for one column in a physical order."""
+        m = len(values)
+        sel = perm(m)
+        pos = sel if sel is not None else np.arange(m, dtype=np.uint32)  # logical i -> physical pos[i]
+        words = np.zeros(max(1, (m + 63) // 64), dtype=np.uint64)
+        if kind == "str":
+            data = np.zeros((max(1, m), 16), dtype=np.uint8)
+        elif kind == "i32":
+            data = np.zeros(max(1, m), dtype=np.int32)
+        elif kind == "i64":
+            data = np.zeros(max(1, m), dtype=np.int64)
+        else:  # list entries
+            data = np.zeros((max(1, m), 2), dtype=np.uint64)
+        for i, (v, good) in enumerate(zip(values, ok)):
+            p = int(pos[i])
+            if not good:
+                continue
+            words[p >> 6] |= np.uint64(1) << np.uint64(p & 63)
+            if kind == "str":
+                b = bytes(v)
+                data[p, 0:4] = np.frombuffer(np.uint32(len(b)).tobytes(), np.uint8)
+                if len(b) <= STRING_INLINE:
+                    data[p, 4:4 + len(b)] = np.frombuffer(b, np.uint8) if b else 0
+                else:
+                    buf = ctypes.create_string_buffer(b, len(b))
+                    keep.append(buf)
+                    data[p, 4:8] = np.frombuffer(b[:4], np.uint8)
+                    data[p, 8:16] = np.frombuffer(np.uint64(ctypes.addressof(buf)).tobytes(), np.uint8)
+            elif kind == "list":
+                data[p] = v
+            else:
+                data[p] = v
+        keep.extend([data, words] + ([sel] if sel is not None else []))
+        return _Vector(data.ctypes.data, sel.ctypes.data if sel is not None else None,
+                       words.ctypes.data if not all(ok) else None)
+
+    child, child_ok, entries = [], [], []
+    for txid, h, tweak, outs in rows:
+        entries.append((len(child), len(outs) if outs is not None else 0))
+        for o in outs or []:
+            child.append(o if o is not None else (b"" if full_x else 0))
+            child_ok.append(o is not None)
+    v = _Vectors()
+    v.count = n
+    v.txid = vec([r[0] or b"" for r in rows], [r[0] is not None for r in rows], "str")
+    v.height = vec([r[1] or 0 for r in rows], [r[1] is not None for r in rows], "i32")
+    v.tweak = vec([r[2] or b"" for r in rows], [r[2] is not None for r in rows], "str")
+    v.outputs = vec(entries, [r[3] is not None for r in rows], "list")
+    v.child = vec(child, child_ok, "str" if full_x else "i64")
+    return keep, v
+
+
 def assign_gpu(ordinal, num_gpus):
     """The product's multi-GPU work assignment (cudasp_assign_gpu,
     include/cudasp_host.h): unit `ordinal` -> GPU ordinal mod num_gpus, as
@@ -309,7 +392,7 @@ def release_pool():
 
 def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size=None, threads=1,
                 chunk_rows=VECTOR_SIZE, output_count=None, label_negation=None, full_x=None, assignments=None,
-                stats=None):
+                stats=None, input="rows", seed=None):
     """Run the table function over `rows` with `threads` executor threads.
     Chunks are dealt round-robin to the threads, as DuckDB's parallel scan
     would hand out morsels; each thread gets its own local state (and GPU,
@@ -319,7 +402,10 @@ def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size
     x-only keys.  assignments: if a list, receives (logical GPU, HIP device)
     of each thread's local state.  stats: if a dict, receives the query's
     host statistics (cudasp_tf_get_stats: feeds, streams, launches, rows,
-    harvest wait)."""
+    harvest wait).  input: "rows" hands each chunk over as per-row pointers
+    (cudasp_tf_function), "vectors" as DuckDB's own vectors
+    (cudasp_tf_function_vectors: string_t, list_entry_t, validity words; with
+    `seed`, every vector behind a shuffled selection vector)."""
     lib = _lib()
     bound = BoundScan(scan_private_key, spend_public_key, label_keys, batch_size, output_count=output_count,
                       label_negation=label_negation, full_x=full_x)
@@ -341,8 +427,14 @@ def cudasp_scan(rows, scan_private_key, spend_public_key, label_keys, batch_size
         def worker(t):
             try:
                 for ci in range(t, len(chunks), threads):
-                    keep, c = _make_chunk(chunks[ci], bound.full_x)
-                    rc = lib.cudasp_tf_function(bound._h, g, locals_[t], ctypes.byref(c))
+                    if input == "vectors":
+                        import numpy as np
+                        rng = np.random.default_rng([seed, ci]) if seed is not None else None
+                        keep, c = _make_vectors(chunks[ci], bound.full_x, rng)
+                        rc = lib.cudasp_tf_function_vectors(bound._h, g, locals_[t], ctypes.byref(c))
+                    else:
+                        keep, c = _make_chunk(chunks[ci], bound.full_x)
+                        rc = lib.cudasp_tf_function(bound._h, g, locals_[t], ctypes.byref(c))
                     if rc < 0:
                         _native.check(rc)
                 out = _Output()

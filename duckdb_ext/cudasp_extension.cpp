@@ -143,86 +143,38 @@ static OperatorResultType CudaspScanFunction(ExecutionContext &context, TableFun
 	if (count == 0) {
 		return OperatorResultType::NEED_MORE_INPUT;
 	}
-	// Columns by position: txid, height, tweak_key, outputs (src/cudasp_extension.cu:159-163).
-	UnifiedVectorFormat txid, height, tweak, outs;
+	// Columns by position: txid, height, tweak_key, outputs (src/cudasp_extension.cu:159-163),
+	// handed over as DuckDB holds them (cudasp_tf_vectors): each vector's data,
+	// selection and validity words, the list child over its list size.  No
+	// per-row loop and no allocation here; the host copies the rows straight
+	// into its batch slots (the reference re-reads every row into two heap
+	// strings, :188-223).
+	UnifiedVectorFormat txid, height, tweak, outs, child_fmt;
 	input.data[0].ToUnifiedFormat(count, txid);
 	input.data[1].ToUnifiedFormat(count, height);
 	input.data[2].ToUnifiedFormat(count, tweak);
 	input.data[3].ToUnifiedFormat(count, outs);
-	auto txid_ptr = UnifiedVectorFormat::GetData<string_t>(txid);
-	auto height_ptr = UnifiedVectorFormat::GetData<int32_t>(height);
-	auto tweak_ptr = UnifiedVectorFormat::GetData<string_t>(tweak);
-	auto list_ptr = UnifiedVectorFormat::GetData<list_entry_t>(outs);
 	auto &child = ListVector::GetEntry(input.data[3]);
-	UnifiedVectorFormat child_fmt;
 	child.ToUnifiedFormat(ListVector::GetListSize(input.data[3]), child_fmt);
-	// BIGINT[] values, or with full_x BLOB[] x-only keys
-	auto child_ptr = bind.full_x ? nullptr : UnifiedVectorFormat::GetData<int64_t>(child_fmt);
-	auto child_blob_ptr = bind.full_x ? UnifiedVectorFormat::GetData<string_t>(child_fmt) : nullptr;
-
-	vector<const uint8_t *> txid_data(count), tweak_data(count);
-	vector<uint32_t> txid_size(count), tweak_size(count);
-	vector<int32_t> heights(count);
-	vector<uint8_t> txid_valid(count), height_valid(count), tweak_valid(count), list_valid(count);
-	vector<uint64_t> list_offset(count), list_length(count);
-	vector<int64_t> child_values;
-	vector<uint8_t> child_valid;
-	vector<const uint8_t *> child_blob_data;
-	vector<uint32_t> child_blob_size;
-	for (idx_t i = 0; i < count; i++) {
-		auto ti = txid.sel->get_index(i), hi = height.sel->get_index(i), wi = tweak.sel->get_index(i),
-		     oi = outs.sel->get_index(i);
-		txid_valid[i] = txid.validity.RowIsValid(ti);
-		height_valid[i] = height.validity.RowIsValid(hi);
-		tweak_valid[i] = tweak.validity.RowIsValid(wi);
-		list_valid[i] = outs.validity.RowIsValid(oi);
-		if (txid_valid[i]) {
-			txid_data[i] = reinterpret_cast<const uint8_t *>(txid_ptr[ti].GetData());
-			txid_size[i] = static_cast<uint32_t>(txid_ptr[ti].GetSize());
-		}
-		if (height_valid[i]) {
-			heights[i] = height_ptr[hi];
-		}
-		if (tweak_valid[i]) {
-			tweak_data[i] = reinterpret_cast<const uint8_t *>(tweak_ptr[wi].GetData());
-			tweak_size[i] = static_cast<uint32_t>(tweak_ptr[wi].GetSize());
-		}
-		list_offset[i] = child_valid.size();
-		if (list_valid[i]) {
-			auto &e = list_ptr[oi];
-			for (idx_t k = 0; k < e.length; k++) {
-				auto ci = child_fmt.sel->get_index(e.offset + k);
-				child_valid.push_back(child_fmt.validity.RowIsValid(ci));
-				if (bind.full_x) {
-					bool ok = child_valid.back();
-					child_blob_data.push_back(ok ? reinterpret_cast<const uint8_t *>(child_blob_ptr[ci].GetData())
-					                             : nullptr);
-					child_blob_size.push_back(ok ? static_cast<uint32_t>(child_blob_ptr[ci].GetSize()) : 0);
-				} else {
-					child_values.push_back(child_valid.back() ? child_ptr[ci] : 0);
-				}
-			}
-			list_length[i] = e.length;
-		}
-	}
-	cudasp_tf_chunk c {};
+	auto vec = [](const UnifiedVectorFormat &f) {
+		cudasp_tf_vector v;
+		v.data = f.data;
+		v.sel = f.sel->data();
+		v.validity = f.validity.GetData();
+		return v;
+	};
+	// BIGINT[] values, or with full_x BLOB[] x-only keys (string_t): the host
+	// reads the child per the bind's full_x
+	static_assert(sizeof(string_t) == sizeof(cudasp_tf_string), "string_t layout");
+	static_assert(sizeof(list_entry_t) == sizeof(cudasp_tf_list_entry), "list_entry_t layout");
+	cudasp_tf_vectors c {};
 	c.count = static_cast<uint32_t>(count);
-	c.txid_data = txid_data.data();
-	c.txid_size = txid_size.data();
-	c.txid_valid = txid_valid.data();
-	c.height = heights.data();
-	c.height_valid = height_valid.data();
-	c.tweak_data = tweak_data.data();
-	c.tweak_size = tweak_size.data();
-	c.tweak_valid = tweak_valid.data();
-	c.list_offset = list_offset.data();
-	c.list_length = list_length.data();
-	c.list_valid = list_valid.data();
-	c.child_values = child_values.data();
-	c.child_valid = child_valid.data();
-	c.child_blob_data = child_blob_data.data();
-	c.child_blob_size = child_blob_size.data();
-	if (cudasp_tf_function(bind.handle, g.handle, l.handle, &c) < 0) {
+	c.txid = vec(txid);
+	c.height = vec(height);
+	c.tweak = vec(tweak);
+	c.outputs = vec(outs);
+	c.child = vec(child_fmt);
+	if (cudasp_tf_function_vectors(bind.handle, g.handle, l.handle, &c) < 0) {
 		throw IOException("cudasp_scan: %s", cudasp_last_error());
 	}
 	return OperatorResultType::NEED_MORE_INPUT;

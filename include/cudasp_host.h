@@ -174,6 +174,48 @@ typedef struct {
 int cudasp_tf_function(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
                        const cudasp_tf_chunk* chunk);
 
+/* DuckDB's vectors as they are (the extension's pass-through form; replaces
+ * the per-row marshalling of the reference's CudaspScanFunction,
+ * src/cudasp_extension.cu:154-224, and of a cudasp_tf_chunk): each column is
+ * its UnifiedVectorFormat -- the data array, the selection vector (NULL =
+ * identity) and the validity mask's 64-bit words (NULL = all valid, bit i of
+ * word i / 64 LSB-first, indexed through the selection like the data) -- so
+ * CudaspScanFunction passes pointers only.  Element types:
+ *   txid, tweak_key:  string_t (16 bytes: length, then the bytes inline when
+ *                     length <= 12, else a 4-byte prefix and a pointer)
+ *   height:           int32_t
+ *   outputs:          list_entry_t {offset, length} into the child vector
+ *   child:            int64_t, or string_t with full_x (32-byte x-only keys);
+ *                     element k = list offset + position, through the
+ *                     child's own selection vector and validity
+ * Row semantics equal cudasp_tf_function's; count <= CUDASP_TF_VECTOR_SIZE. */
+#define CUDASP_TF_STRING_INLINE 12 /* string_t::INLINE_LENGTH */
+typedef struct {
+  uint32_t length;
+  uint8_t prefix[4];  /* inline strings continue over ptr's 8 bytes */
+  const uint8_t* ptr; /* length > CUDASP_TF_STRING_INLINE */
+} cudasp_tf_string;
+typedef struct {
+  uint64_t offset;
+  uint64_t length;
+} cudasp_tf_list_entry;
+typedef struct {
+  const void* data;         /* UnifiedVectorFormat::data */
+  const uint32_t* sel;      /* SelectionVector::data() (sel_t), NULL = identity */
+  const uint64_t* validity; /* ValidityMask::GetData(), NULL = all valid */
+} cudasp_tf_vector;
+typedef struct {
+  uint32_t count;
+  cudasp_tf_vector txid;
+  cudasp_tf_vector height;
+  cudasp_tf_vector tweak;
+  cudasp_tf_vector outputs;
+  cudasp_tf_vector child; /* ListVector::GetEntry(outputs) over ListVector::GetListSize rows */
+} cudasp_tf_vectors;
+
+int cudasp_tf_function_vectors(const cudasp_tf_bind_data* b, cudasp_tf_global* g, cudasp_tf_local* l,
+                               const cudasp_tf_vectors* vectors);
+
 /* Columnar input: a run of rows of the same four
  * columns as Arrow arrays, so Parquet/Arrow data (or DuckDB's Arrow export)
  * feeds the batch buffers with bulk copies instead of per-row pointers.

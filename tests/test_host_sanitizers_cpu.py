@@ -66,10 +66,11 @@ CASES = [
     ("0", 12, 2048, "rows", ["--outputs-max", "7"]),
     (",".join(["0"] * 8), 16, 4096, "columns", ["--outputs", "2"]),
     ("0,0,0", 6, 20000, "rows", ["--outputs", "2"]),
+    ("0,0", 8, 4096, "vectors", ["--outputs-max", "5"]),
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=["1feed-rows", "8feeds-columns", "3feeds-rows"])
+@pytest.mark.parametrize("case", CASES, ids=["1feed-rows", "8feeds-columns", "3feeds-rows", "2feeds-vectors"])
 def test_host_feeds_clean_under_sanitizers(sanitized, case):
     name, exe = sanitized
     dmap, threads, batch, inp, outs = case

@@ -20,7 +20,7 @@
 // emitted rows are exactly the planted ones (decoded from the txids).
 //
 //   host_e2e [--rows N] [--threads T] [--batch B] [--labels L --labels-file F]
-//            [--outputs K | --outputs-max KMAX] [--input rows|columns]
+//            [--outputs K | --outputs-max KMAX] [--input rows|columns|vectors]
 //            [--reps R] [--warm-reps W [--warm-ms MS]] [--plant-sample FILE]
 //            [--null-device [--cpu-table]] [--output-count K] [--label-negation]
 //            [--pinned DEVICES [--hbm]] [--table-out FILE | --table-in FILE [--cold-phases]]
@@ -61,6 +61,11 @@
 // median (cold start).  --cold-phases (with --table-in)
 // times a scanner's creation on device 0 before the first query instead
 // (scanner_create_s: the fixed-base table and its fold), as a breakdown.
+// --input vectors hands each 2048-row chunk over as DuckDB holds it
+// (cudasp_tf_function_vectors: string_t txids and tweaks pointing into the
+// table, the heights, list_entry_t lists and the child values in place), the
+// extension's pass-through form; rows builds per-row pointer arrays
+// (cudasp_tf_function), columns Arrow runs (cudasp_tf_function_columns).
 // Label keys: F holds L 64-byte keys (x || y, little-endian, bench.label_keys);
 // without F, L must be 0 or 1 (the SQL test's label, test/sql/cudasp.test:104).
 // Prints one JSON line; exit 0 iff every timed query emitted exactly the
@@ -122,6 +127,7 @@ struct Args {
   int k = 2;     // fixed outputs per row
   int kmax = 0;  // > 0: 1..kmax outputs per row
   bool columnar = false;
+  bool vectors = false;  // --input vectors: DuckDB's vectors (string_t, list_entry_t) through cudasp_tf_function_vectors
   int reps = 1;
   int warm_reps = 0;    // more queries, each right after a busy kernel on every GPU (clock at speed)
   int warm_ms = 30;
@@ -154,7 +160,15 @@ static Args parse(int argc, char** argv) {
     else if (s == "--labels-file") a.labels_file = val();
     else if (s == "--outputs") a.k = atoi(val());
     else if (s == "--outputs-max") a.kmax = atoi(val());
-    else if (s == "--input") a.columnar = std::string(val()) == "columns";
+    else if (s == "--input") {
+      const std::string v = val();
+      a.columnar = v == "columns";
+      a.vectors = v == "vectors";
+      if (!a.columnar && !a.vectors && v != "rows") {
+        fprintf(stderr, "--input rows|columns|vectors\n");
+        exit(1);
+      }
+    }
     else if (s == "--reps") a.reps = std::max(1, atoi(val()));
     else if (s == "--warm-reps") a.warm_reps = std::max(0, atoi(val()));
     else if (s == "--warm-ms") a.warm_ms = std::max(1, atoi(val()));
@@ -513,6 +527,39 @@ static QueryResult run_query(const Args& a, const uint8_t scan[32], const uint8_
           CK(cudasp_tf_function_columns(bd, gs, ls[i], &c));
           t_calls[i] += now_s() - s;
         }
+      } else if (a.vectors) {
+        // DuckDB's side: the chunk's vectors as a flat DataChunk holds them
+        // (txids and tweaks as string_t over the table's bytes, offsets of the
+        // lists relative to the chunk's child vector)
+        std::vector<cudasp_tf_string> txs(CUDASP_TF_VECTOR_SIZE), tws(CUDASP_TF_VECTOR_SIZE);
+        std::vector<cudasp_tf_list_entry> le(CUDASP_TF_VECTOR_SIZE);
+        for (;;) {
+          const uint64_t c0 = next.fetch_add(CUDASP_TF_VECTOR_SIZE);
+          if (c0 >= rows) break;
+          const uint32_t cnt = (uint32_t)std::min<uint64_t>(CUDASP_TF_VECTOR_SIZE, rows - c0);
+          for (uint32_t r = 0; r < cnt; r++) {
+            const uint8_t* tx = t.txids.data() + (c0 + r) * 32;
+            const uint8_t* tk = t.tweaks.data() + (c0 + r) * 64;
+            txs[r].length = 32;
+            memcpy(txs[r].prefix, tx, 4);
+            txs[r].ptr = tx;
+            tws[r].length = 64;
+            memcpy(tws[r].prefix, tk, 4);
+            tws[r].ptr = tk;
+            le[r].offset = t.list_off[c0 + r] - t.list_off[c0];
+            le[r].length = t.list_len[c0 + r];
+          }
+          cudasp_tf_vectors v{};
+          v.count = cnt;
+          v.txid.data = txs.data();
+          v.height.data = t.heights.data() + c0;
+          v.tweak.data = tws.data();
+          v.outputs.data = le.data();
+          v.child.data = t.outputs.data() + t.list_off[c0];
+          const double s = now_s();
+          CK(cudasp_tf_function_vectors(bd, gs, ls[i], &v));
+          t_calls[i] += now_s() - s;
+        }
       } else {
         std::vector<const uint8_t*> txp(CUDASP_TF_VECTOR_SIZE), twp(CUDASP_TF_VECTOR_SIZE);
         std::vector<uint32_t> txs(CUDASP_TF_VECTOR_SIZE, 32), tws(CUDASP_TF_VECTOR_SIZE, 64);
@@ -837,7 +884,7 @@ int main(int argc, char** argv) {
          "\"null_device\": %s, \"host_cpus_online\": %ld, \"host_call_tx_per_s\": %.1f, "
          "\"table_in\": %s, \"hip_init_s\": %.4f, \"first_query_s\": %.5f, \"scanner_create_s\": %.4f, "
          "\"first_query_exact\": %s}\n",
-         a.columnar ? "arrow columns" : "2048-row chunks", (unsigned long long)t.rows, a.threads, (long long)a.batch,
+         a.columnar ? "arrow columns" : (a.vectors ? "2048-row DuckDB vectors" : "2048-row chunks"), (unsigned long long)t.rows, a.threads, (long long)a.batch,
          a.labels,
          a.kmax ? ("\"1.." + std::to_string(a.kmax) + "\"").c_str() : std::to_string(a.k).c_str(),
          (unsigned long long)t.outputs.size(), a.reps, med, all.c_str(), sorted[0], t.rows / med,
