@@ -149,6 +149,23 @@ inline std::vector<uint32_t> fb_window_bases(int bits = FB_BITS) {
   return bases;
 }
 
+// The same bases with their doubles: 32 words per window, 2^(bits i) G then
+// 2^(bits i + 1) G (k_fb_build_runs: the step between consecutive odd
+// multiples).
+inline std::vector<uint32_t> fb_window_bases_doubled(int bits) {
+  const int windows = (256 + bits - 1) / bits;
+  std::vector<uint32_t> out((size_t)windows * 32);
+  HPoint cur = hp_generator();
+  for (int i = 0; i < windows; i++) {
+    const HPoint two = hp_add(cur, cur);
+    hp_words(&out[(size_t)i * 32], cur);
+    hp_words(&out[(size_t)i * 32 + 16], two);
+    cur = two;
+    for (int d = 1; d < bits; d++) cur = hp_add(cur, cur);
+  }
+  return out;
+}
+
 // Overwrite memory that held key material (not optimised away).
 inline void wipe_bytes(void* p, size_t n) {
   volatile uint8_t* v = static_cast<volatile uint8_t*>(p);

@@ -8,4 +8,4 @@ from ._native import CudaspError, load as load_native  # noqa: F401
 from .scanner import HostBuffer, Scanner, ScanStream, StreamBatch  # noqa: F401
 from .pinned import NativePinnedTable, PinnedTable  # noqa: F401
 from .table_function import (BoundScan, assign_gpu, InvalidInputException, cudasp_scan, cudasp_scan_arrow, pool_size,  # noqa: F401
-                             release_pool)
+                             prewarm, release_pool)

@@ -163,6 +163,7 @@ _HOST_SIGNATURES = {
     "cudasp_tf_pool_size": (ctypes.c_uint32, []),
     "cudasp_tf_function": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Chunk)]),
     "cudasp_tf_function_vectors": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Vectors)]),
+    "cudasp_tf_prewarm": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)]),
     "cudasp_tf_final": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Output)]),
     "cudasp_tf_function_columns": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(_Columns)]),
     "cudasp_tf_get_stats": (ctypes.c_int, [_P, ctypes.POINTER(_Stats)]),
@@ -383,6 +384,14 @@ def assign_gpu(ordinal, num_gpus):
 def pool_size():
     """GPU contexts parked in the host's cross-query pool (cudasp_tf_pool_size)."""
     return int(_lib().cudasp_tf_pool_size())
+
+
+def prewarm(batch_size=0):
+    """Build the fixed-base tables and park one ready streaming feed per GPU
+    (cudasp_tf_prewarm); returns the seconds it took."""
+    secs = ctypes.c_double()
+    _native.check(_lib().cudasp_tf_prewarm(int(batch_size), ctypes.byref(secs)))
+    return secs.value
 
 
 def release_pool():

@@ -14,6 +14,7 @@
 #include "cudasp_extension.hpp"
 
 #include <cstdlib>
+#include <thread>
 
 #include "duckdb.hpp"
 #include "duckdb/common/exception.hpp"
@@ -209,6 +210,14 @@ static void LoadInternal(ExtensionLoader &loader) {
 	// No process settings are needed: the host's device feeds size their
 	// streams from the hardware queues the HIP runtime gives the process
 	// (GPU_MAX_HW_QUEUES, 4 by default).
+	// Cold start: build every GPU's fixed-base table and park a ready feed per
+	// GPU in the background, so the session's first cudasp_scan only rebinds
+	// its keys (a query that arrives earlier waits for, or shares, the same
+	// once-per-device work).  CUDASP_PREWARM=0 turns it off.
+	const char *pw = std::getenv("CUDASP_PREWARM");
+	if (!(pw && std::atoi(pw) == 0)) {
+		std::thread([] { (void)cudasp_tf_prewarm(0, nullptr); }).detach();
+	}
 	TableFunction func("cudasp_scan",
 	                   {LogicalType::TABLE, LogicalType::BLOB, LogicalType::BLOB, LogicalType::LIST(LogicalType::BLOB)},
 	                   nullptr, CudaspScanBind, CudaspScanInit, CudaspScanLocalInit);

@@ -324,6 +324,18 @@ int cudasp_stage_match_device(cudasp_scanner* s, const uint32_t* d_t, const int6
                               const uint32_t* d_output_offsets, const uint32_t* d_output_lengths, uint32_t n,
                               uint8_t* d_match_flags, uint32_t* d_match_rows, uint32_t* d_match_count, void* stream);
 
+/* The fixed-base table of `device` at window width `bits` (22, 26 or 7; 0 =
+ * the device's default), built now unless it exists: a scanner created later
+ * finds it ready.  A host that knows its devices calls this at load time (the
+ * DuckDB extension's Load, in the background) so the first query does not
+ * pay the build.  *build_seconds (may be NULL): the build's wall time, 0 when
+ * the table already existed.  Thread-safe (one build per device and width). */
+int cudasp_fixed_base_prepare(int device, int bits, double* build_seconds);
+/* Test hook: every stride-th entry of that table recomputed on its own (a
+ * double-and-add and an inversion per entry) and compared with the built
+ * one; *checked entries, *mismatched of them differ.  Synchronous. */
+int cudasp_debug_fb_check(int device, int bits, uint32_t stride, uint64_t* checked, uint64_t* mismatched);
+
 /* Shader clock of the last k_scan_multi launch on `device` (measurement
  * only): s_memtime ticks over s_memrealtime time of the grid's first wave,
  * in MHz, and that wave's life in seconds (may be NULL).  Synchronizes the

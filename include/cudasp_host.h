@@ -139,6 +139,16 @@ uint32_t cudasp_assign_gpu(uint64_t ordinal, uint32_t num_gpus);
  * reports how many are parked. */
 void cudasp_tf_release_pool(void);
 uint32_t cudasp_tf_pool_size(void);
+/* Cold start (no reference counterpart: the reference initialises each
+ * device inside the first batch, src/cudasp_gpu.cu:474-484): builds every
+ * logical GPU's fixed-base table and parks one ready streaming feed per
+ * logical GPU -- scanner, persistent-kernel stream, all batch slots pinned --
+ * in the pool for queries of this batch_size (0 = 300000), so the first query
+ * of the process only rebinds keys.  The DuckDB extension calls it from a
+ * background thread at LOAD.  Feeds already pooled are kept; *seconds (may
+ * be NULL) receives the wall time.  Streaming-feed configurations only (one
+ * feed per device); otherwise CUDASP_ERR_INVALID_ARG. */
+int cudasp_tf_prewarm(uint64_t batch_size, double* seconds);
 
 /* One input chunk (<= CUDASP_TF_VECTOR_SIZE = 2048 rows; a larger count is
  * rejected with CUDASP_ERR_INVALID_ARG) of the input table, columns by position:

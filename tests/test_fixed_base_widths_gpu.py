@@ -161,3 +161,23 @@ def test_spend_fold_equals_separate_addition(torch):
         assert not s.spend_folded
         s.set_keys(bench.SCAN_KEY, bench.SPEND_KEY, labels)
         assert s.spend_folded
+
+
+@pytest.mark.parametrize("bits,stride", [(22, 1), (26, 7), (7, 1)])
+def test_table_built_in_runs_equals_entries_built_alone(torch, bits, stride):
+    """The fixed-base tables are built in runs of consecutive odd multiples
+    with one batched inversion per run (k_fb_build_runs); every stride-th
+    entry (all of them at 22 and 7 bits; at 26 bits stride 7, which visits
+    every position of a 32-entry run) equals the entry computed on its own
+    by double-and-add and its own inversion (k_fb_check)."""
+    import ctypes
+    from cudasp_amd import _native
+    lib = _native.load()
+    checked, bad = ctypes.c_uint64(), ctypes.c_uint64()
+    _native.check(lib.cudasp_debug_fb_check(0, bits, stride, ctypes.byref(checked), ctypes.byref(bad)))
+    windows, entries = (256 + bits - 1) // bits, 1 << (bits - 1)
+    assert checked.value == -(-windows * entries // stride)
+    assert bad.value == 0, (bits, bad.value)
+    secs = ctypes.c_double(-1)
+    _native.check(lib.cudasp_fixed_base_prepare(0, bits, ctypes.byref(secs)))
+    assert secs.value == 0  # already built: nothing to do

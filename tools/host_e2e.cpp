@@ -60,7 +60,9 @@
 // object load -- and is reported as first_query_s beside the warm queries'
 // median (cold start).  --cold-phases (with --table-in)
 // times a scanner's creation on device 0 before the first query instead
-// (scanner_create_s: the fixed-base table and its fold), as a breakdown.
+// (scanner_create_s: the fixed-base table and its fold), as a breakdown;
+// --prewarm calls cudasp_tf_prewarm first, as the DuckDB extension does at
+// LOAD (prewarm_s), so first_query_s is then the first query after it.
 // --input vectors hands each 2048-row chunk over as DuckDB holds it
 // (cudasp_tf_function_vectors: string_t txids and tweaks pointing into the
 // table, the heights, list_entry_t lists and the child values in place), the
@@ -140,6 +142,7 @@ struct Args {
   bool hbm = false;             // --hbm: CUDASP_TABLE_HBM placement
   std::string table_out, table_in;  // --table-out / --table-in FILE
   bool cold_phases = false;     // --cold-phases: time a scanner's creation before the first query
+  bool prewarm = false;         // --prewarm: cudasp_tf_prewarm before the first query (the extension's LOAD)
 };
 
 static Args parse(int argc, char** argv) {
@@ -181,6 +184,7 @@ static Args parse(int argc, char** argv) {
     else if (s == "--table-out") a.table_out = val();
     else if (s == "--table-in") a.table_in = val();
     else if (s == "--cold-phases") a.cold_phases = true;
+    else if (s == "--prewarm") a.prewarm = true;
     else if (s == "--pinned") {
       std::string v = val();
       for (size_t p = 0; p <= v.size();) {
@@ -799,7 +803,7 @@ int main(int argc, char** argv) {
   };
   const auto g0 = std::chrono::steady_clock::now();
   Table t;
-  double hip_init_s = 0, scanner_create_s = 0;
+  double hip_init_s = 0, scanner_create_s = 0, prewarm_s = 0;
   if (!a.table_in.empty()) {
     if (!read_table(a.table_in, t) || t.rows != a.rows) {
       fprintf(stderr, "cannot read a %llu-row table from %s\n", (unsigned long long)a.rows, a.table_in.c_str());
@@ -835,6 +839,7 @@ int main(int argc, char** argv) {
       cudasp_scanner_destroy(sc);
     }
   }
+  if (a.prewarm) CK(cudasp_tf_prewarm((uint64_t)a.batch, &prewarm_s));
   if (!a.pinned.empty()) return run_pinned(a, scan, spend, labels, t, gen_s);
 
   const QueryResult warm = run_query(a, scan, spend, labels, t);  // scanners, slots, tables
@@ -883,7 +888,7 @@ int main(int argc, char** argv) {
          "\"warm_reps\": %d, \"warm_ms\": %d, \"warm_seconds\": %.5f, \"warm_tx_per_s\": %.1f, "
          "\"null_device\": %s, \"host_cpus_online\": %ld, \"host_call_tx_per_s\": %.1f, "
          "\"table_in\": %s, \"hip_init_s\": %.4f, \"first_query_s\": %.5f, \"scanner_create_s\": %.4f, "
-         "\"first_query_exact\": %s}\n",
+         "\"first_query_exact\": %s, \"prewarm_s\": %.4f}\n",
          a.columnar ? "arrow columns" : (a.vectors ? "2048-row DuckDB vectors" : "2048-row chunks"), (unsigned long long)t.rows, a.threads, (long long)a.batch,
          a.labels,
          a.kmax ? ("\"1.." + std::to_string(a.kmax) + "\"").c_str() : std::to_string(a.k).c_str(),
@@ -896,6 +901,6 @@ int main(int argc, char** argv) {
          q.stats.streaming_feeds, q.logical_gpus, a.warm_reps, a.warm_ms, warm_med,
          warm_med > 0 ? t.rows / warm_med : 0.0, a.null_device ? "true" : "false", sysconf(_SC_NPROCESSORS_ONLN),
          q.call_s_mean > 0 ? t.rows / q.call_s_mean : 0.0, a.table_in.empty() ? "false" : "true", hip_init_s,
-         warm.secs, scanner_create_s, warm.exact ? "true" : "false");
+         warm.secs, scanner_create_s, warm.exact ? "true" : "false", prewarm_s);
   return all_exact ? 0 : 2;
 }
