@@ -559,6 +559,62 @@ def pinned_leg(args, labels, world, hbm=False):
     return res
 
 
+def cold_start_leg(args, world, rows=1_000_000):
+    """Cold start: config 2's 1M-row table written once
+    by one tools/host_e2e child (--table-out), then fresh children whose first
+    GPU work is the first query (--table-in; the process has only initialised
+    the HIP runtime): `first_query_s` builds the fixed-base table, the feed
+    and its pinned slots inside the query; `first_query_prewarmed_s` runs
+    after cudasp_tf_prewarm (what the DuckDB extension starts at LOAD,
+    `prewarm_s`).  Both against the same process's warm queries' median;
+    every query must emit exactly the planted rows."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "tools", "host_e2e")
+    if not os.path.exists(exe):
+        return dict(error="tools/host_e2e not built (make -C duckdb-cudasp-extension_amd)")
+    threads = max(1, min(8 * world, host_cores()[0]))
+    fd, path = tempfile.mkstemp(prefix="cudasp_cold_", suffix=".bin")
+    os.close(fd)
+    base = [exe, "--rows", str(rows), "--threads", str(threads), "--batch", str(args.batch_size), "--outputs", "2"]
+
+    def child(extra):
+        try:
+            r = subprocess.run(base + extra, capture_output=True, text=True, timeout=args.e2e_timeout)
+        except subprocess.TimeoutExpired:
+            return dict(error="timed out")
+        try:
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+        except (ValueError, IndexError):
+            return dict(error="exit %d: %s" % (r.returncode, (r.stderr or r.stdout)[-300:]))
+        d["exit_code"] = r.returncode
+        return d
+
+    try:
+        gen = child(["--table-out", path])
+        if "error" in gen:
+            return dict(error="table: " + gen["error"])
+        cold = child(["--table-in", path, "--reps", "5"])
+        pw = child(["--table-in", path, "--reps", "5", "--prewarm"])
+    finally:
+        os.unlink(path)
+    out = dict(rows=rows, threads=threads, batch_size=args.batch_size,
+               note="fresh tools/host_e2e processes, first GPU work = the first query (HIP runtime initialised "
+                    "before: hip_init_s); warm = the same process's next 5 queries' median")
+    for name, d in (("cold", cold), ("prewarmed", pw)):
+        if "error" in d:
+            out[name + "_error"] = d["error"]
+            continue
+        out[name] = dict(first_query_s=d.get("first_query_s"), warm_query_s=d.get("seconds"),
+                         ratio=(d["first_query_s"] / d["seconds"]) if d.get("seconds") else None,
+                         hip_init_s=d.get("hip_init_s"), prewarm_s=d.get("prewarm_s"),
+                         exact=bool(d.get("first_query_exact") and d.get("emitted_equal_planted")),
+                         exit_code=d.get("exit_code"))
+    out["first_query_s"] = out.get("cold", {}).get("first_query_s")
+    out["first_query_prewarmed_s"] = out.get("prewarmed", {}).get("first_query_s")
+    return out
+
+
 def e2e_leg(args, labels, world, fb_bits, mode=None):
     """PCIe-inclusive end-to-end rate through the table-function host
     (include/cudasp_host.h, the calls DuckDB's executor makes) over all
@@ -973,6 +1029,8 @@ def main():
                     help="also run the pinned and resident table legs (cudasp_pinned_*, tools/host_e2e --pinned; "
                          "an API beside the reference's interface, off by default)")
     ap.add_argument("--no-pinned", action="store_true", help=argparse.SUPPRESS)  # the default since round 6
+    ap.add_argument("--no-cold-start", action="store_true",
+                    help="skip the cold-start leg (fresh processes' first 1M-row query, with and without prewarm)")
     ap.add_argument("--no-e2e-launch", action="store_true",
                     help="skip the second end-to-end leg with the host's per-slot launches (CUDASP_TF_MODE=launch)")
     ap.add_argument("--e2e-threads", type=int, default=0,
@@ -1283,6 +1341,8 @@ def main():
                 el = e2e_leg(args, labels, world, args.fb_bits, mode="launch")
                 result["e2e_launch"] = el
                 result["e2e_launch_tx_s"] = el.get("tx_per_s")
+            if not args.no_cold_start and args.fb_bits == product_fb_bits:
+                result["cold_start"] = cold_start_leg(args, world)
             if args.pinned and args.fb_bits in (0, 26) and args.rows <= 40_000_000:
                 # (the child rebuilds the table in host memory: bounded to config-4 sizes)
                 # the table pinned once and scanned in place: no host copy per query

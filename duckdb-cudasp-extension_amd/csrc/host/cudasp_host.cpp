@@ -53,6 +53,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../../include/cudasp_abi.h"
@@ -117,6 +118,7 @@ double now_s() {
 
 }  // namespace
 
+extern "C" void cudasp_internal_scanner_park(cudasp_scanner* s);
 extern "C" void cudasp_internal_set_error(const char* msg);
 extern "C" void* cudasp_internal_scanner_stream(cudasp_scanner* s);
 extern "C" void cudasp_internal_clear_key_cache(void);
@@ -326,6 +328,9 @@ FeedRes* pool_take(int device, uint32_t cap_rows, int nstreams, uint32_t stream_
 }
 
 void pool_put(FeedRes* r) {
+  // parked scanners hold no spend-key fold table (cudasp_internal_scanner_park)
+  for (int k = 0; k < r->nstreams; k++)
+    if (r->scanners[k]) cudasp_internal_scanner_park(r->scanners[k]);
   {
     std::lock_guard<std::mutex> lock(g_pool_mu);
     if (g_pool.size() < POOL_MAX) {
@@ -1926,39 +1931,51 @@ int cudasp_tf_prewarm(uint64_t batch_size, double* seconds) {
   memcpy(spend, gx, 32);
   memcpy(spend + 32, gy, 32);
   const uint32_t cap_rows = (uint32_t)(batch_size + CUDASP_TF_VECTOR_SIZE);
-  for (size_t lg = 0; lg < map.size(); lg++) {
+  // the logical GPUs' feeds in parallel (each device's table build, scanner,
+  // stream and pinned slots are independent)
+  std::vector<int> rcs(map.size(), CUDASP_OK);
+  std::vector<std::string> msgs(map.size());
+  auto warm_one = [&](size_t lg) {
     const int device = map[lg];
     const uint32_t blocks = stream_blocks_for(device, map);
     {
       std::lock_guard<std::mutex> lock(g_pool_mu);
-      bool have = false;
       for (FeedRes* r : g_pool)
-        have |= r->device == device && r->cap_rows == cap_rows && r->nstreams == 1 && r->stream &&
-                r->stream_blocks == blocks;
-      if (have) continue;  // already warm
+        if (r->device == device && r->cap_rows == cap_rows && r->nstreams == 1 && r->stream &&
+            r->stream_blocks == blocks)
+          return;  // already warm
     }
     DeviceSet dg(device);
     auto* r = new FeedRes();
     r->device = device;
     r->cap_rows = cap_rows;
     r->nstreams = 1;
-    rc = cudasp_scanner_create(device, scan, spend, nullptr, 0, cap_rows, &r->scanners[0]);
-    if (rc == CUDASP_OK) rc = cudasp_stream_create(r->scanners[0], blocks, &r->stream);
-    if (rc == CUDASP_OK) {
+    int e = cudasp_scanner_create(device, scan, spend, nullptr, 0, cap_rows, &r->scanners[0]);
+    if (e == CUDASP_OK) e = cudasp_stream_create(r->scanners[0], blocks, &r->stream);
+    if (e == CUDASP_OK) {
       r->stream_blocks = blocks;
       r->stream_slots = feed_stream_slots();
       // every slot with the capacity a first query opens it with (2 outputs
       // and 32 txid bytes per row; grown later like any slot)
-      for (int k = 0; k < r->stream_slots && rc == CUDASP_OK; k++)
-        rc = prepare_slot_streaming(*r, r->slots[k], (size_t)cap_rows * 2, (size_t)cap_rows * 32);
+      for (int k = 0; k < r->stream_slots && e == CUDASP_OK; k++)
+        e = prepare_slot_streaming(*r, r->slots[k], (size_t)cap_rows * 2, (size_t)cap_rows * 32);
     }
-    if (rc != CUDASP_OK) {
-      const std::string msg = cudasp_last_error();
+    if (e != CUDASP_OK) {
+      rcs[lg] = e;
+      msgs[lg] = cudasp_last_error();
       release_res(r);
-      return host_fail(rc, "prewarm of GPU %zu (device %d): %s", lg, device, msg.c_str());
+      return;
     }
     pool_put(r);
+  };
+  {
+    std::vector<std::thread> th;
+    for (size_t lg = 0; lg < map.size(); lg++) th.emplace_back(warm_one, lg);
+    for (auto& t : th) t.join();
   }
+  for (size_t lg = 0; lg < map.size(); lg++)
+    if (rcs[lg] != CUDASP_OK)
+      return host_fail(rcs[lg], "prewarm of GPU %zu (device %d): %s", lg, map[lg], msgs[lg].c_str());
   // One placeholder row through every parked feed, as a query would send it
   // (bind, a feed taken from the pool, its keys rebound, a batch published to
   // its streaming kernel, harvest, the feed parked again): the launch path's

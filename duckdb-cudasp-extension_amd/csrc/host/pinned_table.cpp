@@ -208,16 +208,24 @@ int seal_hbm(cudasp_pinned_table& t, Batch& b, size_t wb) {
   std::vector<uint32_t> lens(n);
   for (uint64_t r = 0; r < n; r++) lens[r] = s.offsets[r + 1] - s.offsets[r];
   uint8_t* d_tmp = nullptr;
-  bool ok = hipMalloc((void**)&b.d_x, n * 32) == hipSuccess && hipMalloc((void**)&b.d_y, n * 32) == hipSuccess &&
+  // the uploads and the transpose on a private non-blocking stream, waited
+  // for alone: an append does not wait for other work on the device (another
+  // table's or query's persistent streaming kernel runs until its close)
+  hipStream_t st = nullptr;
+  bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+            hipMalloc((void**)&b.d_x, n * 32) == hipSuccess && hipMalloc((void**)&b.d_y, n * 32) == hipSuccess &&
             hipMalloc((void**)&b.d_out, wb) == hipSuccess && hipMalloc((void**)&b.d_offs, n * 4) == hipSuccess &&
             hipMalloc((void**)&b.d_lens, n * 4) == hipSuccess && hipMalloc((void**)&b.d_flags, n) == hipSuccess &&
             hipMalloc((void**)&b.d_rows, n * 4) == hipSuccess && hipMalloc((void**)&d_tmp, n * TWEAK_KEY_SIZE) == hipSuccess;
-  ok = ok && hipMemcpy(d_tmp, s.rows.data(), n * TWEAK_KEY_SIZE, hipMemcpyHostToDevice) == hipSuccess &&
-       (b.words == 0 || hipMemcpy(b.d_out, s.outputs.data(), b.words * 8, hipMemcpyHostToDevice) == hipSuccess) &&
-       hipMemcpy(b.d_offs, s.offsets.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemcpy(b.d_lens, lens.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess;
-  if (ok) ok = cudasp_tweaks_to_columns(d_tmp, (uint32_t)n, b.d_x, b.d_y, nullptr) == CUDASP_OK;
-  if (ok) ok = hipDeviceSynchronize() == hipSuccess;
+  ok = ok && hipMemcpyAsync(d_tmp, s.rows.data(), n * TWEAK_KEY_SIZE, hipMemcpyHostToDevice, st) == hipSuccess &&
+       (b.words == 0 || hipMemcpyAsync(b.d_out, s.outputs.data(), b.words * 8, hipMemcpyHostToDevice, st) == hipSuccess) &&
+       hipMemcpyAsync(b.d_offs, s.offsets.data(), n * 4, hipMemcpyHostToDevice, st) == hipSuccess &&
+       hipMemcpyAsync(b.d_lens, lens.data(), n * 4, hipMemcpyHostToDevice, st) == hipSuccess;
+  if (ok) ok = cudasp_tweaks_to_columns(d_tmp, (uint32_t)n, b.d_x, b.d_y, st) == CUDASP_OK;
+  if (st) {
+    ok = hipStreamSynchronize(st) == hipSuccess && ok;  // the pageable sources stay alive until here
+    (void)hipStreamDestroy(st);
+  }
   if (d_tmp) (void)hipFree(d_tmp);
   if (!ok) {
     free_batch(b);

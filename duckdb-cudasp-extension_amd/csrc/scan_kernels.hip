@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1505,7 +1506,14 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
     if constexpr (wide) {
       // K > MULTI_RMAX: the piece (count rows, rmax 1: one) is finished here,
       // its indices in groups of g <= MULTI_RMAX F points with one inversion
-      // each (the S points were inverted above, alone: P and Q stay empty)
+      // each (the S points were inverted above, alone: P and Q stay empty).
+      // Its rows' output mirrors were written in this iteration, lane-strided
+      // by stream_prefetch (agent-scope write-through stores): wait for those
+      // stores and drop this CU's L1 before any lane reads them (the
+      // pipelined path reads a mirror one iteration later, after the next
+      // iteration's system-scope acquire).
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const StreamWr* wn = wrs[wid][pn];
       const int meta_n = META + 2 * MULTI_RMAX * pn;
       uint32_t hits = 0;
@@ -2120,8 +2128,10 @@ struct FoldTable {
   uint32_t* table = nullptr;  // nullptr: exceptional (or failed) -- no fold for this key
   int refs = 0;
   uint64_t last_release = 0;
+  bool building = false;  // fold_acquire is building it (outside g_fold_mu)
 };
 std::mutex g_fold_mu;
+std::condition_variable g_fold_cv;
 std::map<FoldKey, FoldTable> g_folds;
 uint64_t g_fold_clock = 0;
 constexpr int FOLD_CACHED_PER_DEVICE = 4;
@@ -2159,48 +2169,59 @@ void fold_trim_locked(int device) {
   }
 }
 
-// A reference to the fold table of (device, bits, spend), built on first use
-// (synchronously, on a stream of its own).  *table = nullptr when the key
-// cannot be folded (exceptional sums) or the allocation failed.
-int fold_acquire(const FoldKey& key, const uint32_t* d_fb, const uint32_t** table) {
-  std::lock_guard<std::mutex> lk(g_fold_mu);
-  auto it = g_folds.find(key);
-  if (it != g_folds.end()) {
-    it->second.refs++;
-    *table = it->second.table;
-    return CUDASP_OK;
-  }
-  FoldTable ft;
+// The fold table of `key` built on a stream of its own: the table, or nullptr
+// when the key cannot be folded (exceptional sums) or anything failed (the
+// scanner then adds B on its own; every partial allocation is freed).
+uint32_t* fold_build(const FoldKey& key, const uint32_t* d_fb) {
   DeviceGuard g(key.device);
   uint32_t* d = nullptr;
   uint32_t* d_bad = nullptr;
-  if (hipMalloc(&d, fold_table_bytes(key.bits)) != hipSuccess || hipMalloc(&d_bad, 4) != hipSuccess) {
-    (void)hipGetLastError();
-    if (d) (void)hipFree(d);
-    d = nullptr;
-  } else {
-    hipStream_t st = nullptr;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    HIP_TRY(hipMemsetAsync(d_bad, 0, 4, st));
+  hipStream_t st = nullptr;
+  uint32_t bad = 1;
+  bool ok = hipMalloc(&d, fold_table_bytes(key.bits)) == hipSuccess && hipMalloc(&d_bad, 4) == hipSuccess &&
+            hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+            hipMemsetAsync(d_bad, 0, 4, st) == hipSuccess;
+  if (ok) {
     SpendWords sw;
     memcpy(sw.w, key.spend, sizeof(sw.w));
     const uint32_t top = key.bits == 26 ? FbWidth<26>::TOP_ENTRIES : FbWidth<22>::TOP_ENTRIES;
     auto kf = key.bits == 26 ? k_fb_fold<26> : k_fb_fold<22>;
     hipLaunchKernelGGL(kf, dim3((top + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, d_fb, sw, d, d_bad);
-    HIP_TRY(hipGetLastError());
-    uint32_t bad = 1;
-    HIP_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    HIP_TRY(hipStreamDestroy(st));
-    if (bad) {
-      (void)hipFree(d);
-      d = nullptr;
-    }
+    ok = hipGetLastError() == hipSuccess && hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipStreamSynchronize(st) == hipSuccess;
   }
+  (void)hipGetLastError();
+  if (st) (void)hipStreamDestroy(st);
   if (d_bad) (void)hipFree(d_bad);
-  ft.table = d;
-  ft.refs = 1;
-  g_folds[key] = ft;
+  if (!ok || bad) {
+    if (d) (void)hipFree(d);
+    d = nullptr;
+  }
+  return d;
+}
+
+// A reference to the fold table of (device, bits, spend), built on first use.
+// The build runs outside g_fold_mu (an entry marked `building` holds its
+// place; other scanners of the same key wait for it, other keys and devices
+// go ahead).  *table = nullptr when the key cannot be folded.
+int fold_acquire(const FoldKey& key, const uint32_t* d_fb, const uint32_t** table) {
+  std::unique_lock<std::mutex> lk(g_fold_mu);
+  auto it = g_folds.find(key);
+  if (it != g_folds.end()) {
+    it->second.refs++;  // a referenced entry is never trimmed: `it` stays valid
+    g_fold_cv.wait(lk, [&] { return !it->second.building; });
+    *table = it->second.table;
+    return CUDASP_OK;
+  }
+  it = g_folds.emplace(key, FoldTable()).first;
+  it->second.refs = 1;
+  it->second.building = true;
+  lk.unlock();
+  uint32_t* d = fold_build(key, d_fb);
+  lk.lock();
+  it->second.table = d;
+  it->second.building = false;
+  g_fold_cv.notify_all();
   *table = d;
   return CUDASP_OK;
 }
@@ -2751,6 +2772,21 @@ void cudasp_internal_set_error(const char* msg) { g_last_error = msg ? msg : "";
 // The table-function host's device feeds launch each batch's copies and
 // kernels on the stream of the scanner that scans it; not public either.
 void* cudasp_internal_scanner_stream(cudasp_scanner* s) { return s ? (void*)s->stream : nullptr; }
+// A scanner parked in the table-function host's pool: its spend key's fold
+// table is released (so parked scanners do not keep old wallets' 268 MB
+// tables alive; at most FOLD_CACHED_PER_DEVICE unreferenced ones stay cached),
+// and its next cudasp_scanner_set_keys prepares again, even for the same
+// keys, taking the fold table back.  No work of the scanner may be in flight.
+void cudasp_internal_scanner_park(cudasp_scanner* s) {
+  if (!s) return;
+  if (s->fold_held) {
+    fold_release(s->fold_key);
+    s->fold_held = false;
+    s->fold_table = nullptr;
+  }
+  s->consts.fb_top = nullptr;
+  s->prepared = false;
+}
 // Wipe the process-wide scan-key digit cache (cudasp_tf_release_pool).
 void cudasp_internal_clear_key_cache(void) { scan_digits_cache_clear(); }
 

@@ -307,7 +307,8 @@ def test_host_e2e_eight_logical_gpus_config4():
 @pytest.mark.parametrize("labels,threads,batch,rows,outs", [(2, 16, 1, 65536, ["--outputs", "2"]),
                                                              (0, 1, 2048, 65536, ["--outputs", "2"]),
                                                              (1, 3, 2048, 300001, ["--outputs-max", "15"]),
-                                                             (0, 1, 2048, 300001, ["--outputs", "8"])])
+                                                             (0, 1, 2048, 300001, ["--outputs", "8"]),
+                                                             (1, 4, 2048, 65536, ["--outputs", "2", "--output-count", "8"])])
 def test_host_stream_slot_reuse_reads_fresh_rows(labels, threads, batch, rows, outs):
     """A streaming feed with 4 slots (CUDASP_TF_STREAM_SLOTS=4) and 2048-row
     batches: every slot -- its pinned rows and its device mirror of the
@@ -316,7 +317,10 @@ def test_host_stream_slot_reuse_reads_fresh_rows(labels, threads, batch, rows, o
     follow a system-scope acquire and the mirror is written through, so no
     row is scanned with a stale tweak or compared with a stale outputs list
     (without the acquire 8-25% of the planted matches were lost, without the
-    write-through 1-3 per query; profiles/r05_stream_acquire.txt).  Every
+    write-through 1-3 per query; profiles/r05_stream_acquire.txt).  The last
+    case streams output_count 8 through the WIDE instance, which reads a
+    piece's mirrors in the iteration that wrote them (after a vmcnt wait and an
+    agent-scope acquire).  Every
     query emits exactly the planted rows; the oracle recomputes the run's
     sample."""
     import json
