@@ -60,7 +60,11 @@ __global__ __launch_bounds__(256) void loop(uint32_t* out, int iters, uint32_t s
   seed_fe(Q.x, s + 3);
   seed_fe(Q.y, s + 4);
   for (int it = 0; it < iters; ++it) {
-    if constexpr (OP == 0) {
+    if constexpr (OP == 20) {
+      gej_double_neg_yh(R, R);  // the stage-A ladder's doubling (Yh form)
+    } else if constexpr (OP == 21) {
+      gej_add_ge_yh(R, R, Q);  // the stage-A ladder's mixed addition (Yh form)
+    } else if constexpr (OP == 0) {
       gej_double(R, R);
     } else if constexpr (OP == 1) {
       gej_add_ge(R, R, Q);
@@ -126,6 +130,8 @@ int main() {
   for (int w : {1, 2, 3, 4}) run<3>("sqr", w, d, cus, 2);
   for (int w : {3}) run<0>("dbl", w, d, cus, 1);
   for (int w : {3}) run<10>("dbl0", w, d, cus, 1);
+  for (int w : {2, 3, 4}) run<20>("ydbl", w, d, cus, 1);
+  for (int w : {2, 3, 4}) run<21>("yadd", w, d, cus, 1);
   CHK(hipFree(d));
   return 0;
 }

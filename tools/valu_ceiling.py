@@ -128,7 +128,8 @@ def main():
     out["one_opcode_loops"] = {k: dict(U=r["U"], clock_hz=r.get("clock_hz")) for k, r in mb.items()}
     go = analyse(counters(d + "/go_sq/*counter_collection.csv"), counters(d + "/go_grbm/*counter_collection.csv"),
                  durations(d + "/go_kt/*kernel_trace.csv"), skip_first=False)
-    names = {"void loop<0>": "dbl", "void loop<1>": "madd", "void loop<2>": "mul", "void loop<3>": "sqr"}
+    names = {"void loop<0>": "dbl", "void loop<1>": "madd", "void loop<2>": "mul", "void loop<3>": "sqr",
+             "void loop<20>": "ydbl", "void loop<21>": "yadd"}
     print("group-operation loops (group_ops: register-resident, issue-bound; by waves per SIMD):")
     gu = {}
     for k, r in sorted(go.items()):
@@ -140,10 +141,14 @@ def main():
               % (nm, w, r["U"], r.get("int64", 0) / r["valu"] if r.get("int64") else 0, r.get("clock_hz", 0) / 1e9))
     out["group_op_loops"] = {"%s_w%d" % k: v for k, v in gu.items()}
     u_ladder = None
-    if ("dbl", 3) in gu and ("madd", 3) in gu:
+    # the ladder's own operations (gej_double_neg_yh / gej_add_ge_yh, the Yh
+    # form k_scan_multi runs) when measured, else the plain forms
+    dbl, add = ("ydbl", "yadd") if ("ydbl", 3) in gu and ("yadd", 3) in gu else ("dbl", "madd")
+    if (dbl, 3) in gu and (add, 3) in gu:
         tot = sum(n for n, _ in LADDER)
-        u_ladder = tot / sum(n / gu[(op, 3)] for n, op in LADDER)
-        print("ladder mix at 3 waves/SIMD (126 dbl x 893 + 39 madd x 1576 VALU): U %.3f" % u_ladder)
+        u_ladder = tot / sum(n / gu[(dbl if op == "dbl" else add, 3)] for n, op in LADDER)
+        print("ladder mix at 3 waves/SIMD (126 %s x 893 + 39 %s x 1576 VALU): U %.3f" % (dbl, add, u_ladder))
+    out["ladder_ops"] = [dbl, add]
     out["ladder_mix_U"] = u_ladder
     for L in (0, 1, 16):
         sc = analyse(counters(d + "/scan_sq_L%d/*counter_collection.csv" % L),
