@@ -888,7 +888,7 @@ def sq_profile_name(args):
     return name
 
 
-def alu_roofline(sq, path, value_per_gpu, multi=False, clock_mhz=None, stamp=None):
+def alu_roofline(sq, path, value_per_gpu, multi=False, clock_mhz=None, stamp=None, labels=0):
     """Integer-VALU roofline of the whole path: VALU wave-instructions per row
     (rocprofv3 SQ_INSTS_VALU of a run of the same shape on the same machine
     code, profiles/: k_scan_multi per row with --launch multi, both stage
@@ -922,38 +922,46 @@ def alu_roofline(sq, path, value_per_gpu, multi=False, clock_mhz=None, stamp=Non
                valu_wave_instr_per_64_rows=per64, kernel_U_profiled=kernel_u,
                source=os.path.relpath(path, ROOT), code_stamp=stamp,
                note="SQ_INSTS_VALU per row of a run of this shape on this machine code (%s); peak = nominal VALU "
-                    "issue rate; VOP3 integer ops issue at about half of it on gfx950 (the measured rate is at "
-                    "2.4 GHz)" % sq.get("shape", "see source"))
+                    "issue rate; measured_vop3_issue_rate = 8-byte-encoded (VOP3) integer ops alone at 2.4 GHz, "
+                    "about half of it -- the kernel's 4-byte VOP2 ops issue faster, so it can exceed 1; "
+                    "mix_ceiling is the bound of the kernel's own mix" % sq.get("shape", "see source"))
     if multi:
-        mix = mix_ceiling(achieved_wi, clock_mhz, stamp, kernel_u)
+        mix = mix_ceiling(achieved_wi, clock_mhz, stamp, kernel_u, labels)
         if mix:
             out["mix_ceiling"] = mix
     return out
 
 
-def mix_ceiling(achieved_wi, clock_mhz, stamp, kernel_u):
+def mix_ceiling(achieved_wi, clock_mhz, stamp, kernel_u, labels=0):
     """The issue ceiling of the scan's own instruction mix (tools/valu_ceiling.py,
-    profiles/r0N_valu_ceiling.json, stamped like the counters): the kernel's
-    stage-A ladder (~88% of its VALU) run as register-resident loops at the
-    kernel's 3 waves per SIMD issues U_ladder VALU wave-instructions per 4
-    SIMD cycles; x 1024 SIMDs x f / 4 is the rate this mix sustains at clock f
-    when nothing else limits it.  f is the timed launch's own shader clock
-    (`clock`), else the 2.4 GHz peak.  The clock-free form is the profiled
-    launch's U over U_ladder."""
+    profiles/r0N_valu_ceiling.json, stamped like the counters).  The stage-A
+    ladder's own operations (the Yh-form doubling and addition), run as
+    register-resident loops at the kernel's 3 waves per SIMD, issue U_ladder
+    VALU wave-instructions per 4 SIMD cycles; they are the ladder's share of
+    the kernel's VALU per row (82% at 0 labels, the bench key's 126 doublings
+    and 39 additions); the rest issues at most at the 4-byte VOP2 rate (the
+    fastest one-opcode loop).  U_max = 1 / (share / U_ladder + (1 - share) /
+    U_vop2) bounds the whole mix, and U_max x 1024 SIMDs x f / 4 is the rate
+    at clock f -- the timed launch's own shader clock (`clock`), else the
+    2.4 GHz peak.  The clock-free form is the profiled launch's U over U_max."""
     path, vc, why = stamped_summary("valu_ceiling", "k_scan_multi", stamp)
     if vc is None:
         return dict(error=why)
-    u = vc.get("ladder_mix_U")
-    if not u:
-        return dict(error="%s has no ladder_mix_U" % os.path.relpath(path, ROOT))
+    shape = vc.get("k_scan_multi_L%d" % labels) or {}
+    u_max = shape.get("mix_U_upper_bound")
+    if not u_max:
+        return dict(error="%s has no mix bound for %d labels" % (os.path.relpath(path, ROOT), labels))
     f = clock_mhz * 1e6 if clock_mhz else 2.4e9
-    ceiling = u * 1024 * f / 4
-    return dict(ladder_mix_U=u, clock_hz=f, clock_source="timed launch" if clock_mhz else "peak (no clock read)",
+    ceiling = u_max * 1024 * f / 4
+    return dict(mix_U_upper_bound=u_max, ladder_U=vc.get("ladder_mix_U"), ladder_ops=vc.get("ladder_ops"),
+                ladder_share=shape.get("ladder_share"), vop2_U=vc.get("vop2_U"), clock_hz=f,
+                clock_source="timed launch" if clock_mhz else "peak (no clock read)",
                 ceiling_wave_instr_per_s=ceiling, frac=achieved_wi / ceiling,
-                kernel_frac_of_ladder_mix_profiled=(kernel_u / u) if kernel_u else None,
+                kernel_U_profiled=kernel_u, kernel_frac_of_mix_bound_profiled=(kernel_u / u_max) if kernel_u else None,
                 source=os.path.relpath(path, ROOT),
-                note="U = VALU wave-instructions per 4 SIMD cycles (PMC); frac = achieved / (U_ladder x SIMDs x "
-                     "clock / 4); kernel_frac_of_ladder_mix_profiled = the profiled launch's U / U_ladder")
+                note="U = VALU wave-instructions per 4 SIMD cycles (PMC); U_max = 1 / (share / U_ladder + (1 - share) "
+                     "/ U_vop2): the ladder's ops at their measured loop rate, the rest at most at the VOP2 rate; frac "
+                     "= achieved / (U_max x SIMDs x clock / 4)")
 
 
 def timed_steps(step, steps, warmup, device, barrier, counter=None):
@@ -1209,7 +1217,8 @@ def main():
     if sq is None:
         alu = dict(bound="valu", error=sq_why, code_stamp=stamp)
     else:
-        alu = alu_roofline(sq, sq_path, value / world, multi, clock["shader_mhz"] if clock else None, stamp)
+        alu = alu_roofline(sq, sq_path, value / world, multi, clock["shader_mhz"] if clock else None, stamp,
+                           args.labels)
 
     result = dict(
         metric=METRIC, value=value, unit="tx/s", n_gpus=world, steps=args.steps, warmup=args.warmup,

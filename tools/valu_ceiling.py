@@ -108,6 +108,8 @@ def analyse(sq, grbm, kt, skip_first):
 # doublings and 39 mixed additions of 893 and 1576 VALU;
 # ~88% of k_scan_multi's instructions.
 LADDER = ((126 * 893, "dbl"), (39 * 1576, "madd"))
+# rows of one k_scan_multi launch in tools/recipes/pmc.sh's scan passes, by label count
+ROWS = {0: 32_700_000, 1: 9_400_000, 16: 3_000_000}
 
 
 def main():
@@ -149,6 +151,14 @@ def main():
         u_ladder = tot / sum(n / gu[(dbl if op == "dbl" else add, 3)] for n, op in LADDER)
         print("ladder mix at 3 waves/SIMD (126 %s x 893 + 39 %s x 1576 VALU): U %.3f" % (dbl, add, u_ladder))
     out["ladder_ops"] = [dbl, add]
+    # The kernel's other instructions (inversions' divsteps, SHA-256, stage B,
+    # compares) issue at most at the 4-byte-encoded VOP2 rate (v_add_u32,
+    # the fastest one-opcode loop); with the ladder's share of the kernel's
+    # per-row VALU (the bench key's 126 doublings and 39 additions over the
+    # measured count), 1 / (share / U_ladder + (1 - share) / U_vop2) bounds
+    # the issue rate of the whole mix from above.
+    u_vop2 = max((r["U"] for r in mb.values()), default=None)
+    out["vop2_U"] = u_vop2
     out["ladder_mix_U"] = u_ladder
     for L in (0, 1, 16):
         sc = analyse(counters(d + "/scan_sq_L%d/*counter_collection.csv" % L),
@@ -165,7 +175,15 @@ def main():
               "ceiling %s; ceiling %s wave-instr/s at this clock, %s at 2.4 GHz"
               % (L, r["U"], (f or 0) / 1e9, ach or 0, "%.3f" % frac if frac else "-",
                  "%.3e" % ceiling if ceiling else "-", "%.3e" % (ceiling * PEAK_HZ / f) if (ceiling and f) else "-"))
+        per_row = r["valu"] * 64.0 / ROWS.get(L, 1) if ROWS.get(L) else None
+        share = sum(n for n, _ in LADDER) / per_row if per_row else None
+        bound = (1.0 / (share / u_ladder + (1 - share) / u_vop2)) if (share and u_ladder and u_vop2) else None
+        if bound:
+            print("  ladder share of its VALU %.3f (of %.0f per row); mix upper bound U %.3f; kernel at %.3f of it"
+                  % (share, per_row, bound, r["U"] / bound))
         out["k_scan_multi_L%d" % L] = dict(U=r["U"], clock_hz=f, achieved_wave_instr_per_s=ach,
+                                           valu_per_row=per_row, ladder_share=share, mix_U_upper_bound=bound,
+                                           frac_of_mix_upper_bound=(r["U"] / bound) if bound else None,
                                            frac_of_ladder_mix_ceiling=frac,
                                            mix_ceiling_wave_instr_per_s=ceiling,
                                            mix_ceiling_at_peak_clock=(ceiling * PEAK_HZ / f) if (ceiling and f) else None,
