@@ -1184,6 +1184,11 @@ def main():
         return stamped_summary(name, skey, stamp)
 
     hbm_path, pmc, traffic_why = summary(args.pmc_summary, "pmc_hbm_multi" if multi else "pmc_hbm_k_shared_secret")
+    if pmc and not args.pmc_summary and (args.labels or args.outputs_max or args.outputs_per_row != 2 or
+                                         args.output_count != 1 or args.label_negation):
+        # the HBM passes profile config 4's row shape (0 labels, 2 outputs per row)
+        hbm_path, pmc, traffic_why = None, None, "HBM counters are measured at config 4's row shape only " \
+                                                 "(0 labels, 2 outputs/row)"
     pmc = pmc or {}
     traffic = None
     if multi:
