@@ -2033,6 +2033,27 @@ size_t fb_table_bytes(int bits) {
   return windows * ((size_t)1 << (bits - 1)) * FB_WORDS * 4;
 }
 
+// One non-blocking stream per device for the library's one-off builds (the
+// fixed-base tables, the spend-key folds), created once and kept: creating
+// and destroying a stream costs ~3 + 1.5 ms, paid by a query's first key
+// otherwise (profiles/r06_cold_prewarm_hip_api_stats.csv).  The caller has
+// the device current.  Work on it is waited for with hipStreamSynchronize,
+// so it never holds up other streams.
+std::mutex g_util_mu;
+std::map<int, hipStream_t> g_util_streams;
+hipStream_t util_stream(int device) {
+  std::lock_guard<std::mutex> lk(g_util_mu);
+  auto it = g_util_streams.find(device);
+  if (it != g_util_streams.end()) return it->second;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  g_util_streams[device] = st;
+  return st;
+}
+
 int ensure_device_table(int device, int bits, const uint32_t** out, bool* built = nullptr) {
   if (!fb_bits_supported(bits))
     return set_error(CUDASP_ERR_INVALID_ARG, "fixed-base window width %d not supported (22, 26, or 7 = LDS)", bits);
@@ -2068,16 +2089,15 @@ int ensure_device_table(int device, int bits, const uint32_t** out, bool* built 
   uint32_t* d_scratch = nullptr;
   hipStream_t st = nullptr;
   auto cleanup = [&](bool keep_table) {
-    if (st) (void)hipStreamDestroy(st);
     if (d_bases) (void)hipFree(d_bases);
     if (d_scratch) (void)hipFree(d_scratch);
     if (!keep_table) (void)hipFree(d_table);
   };
-  // The build runs on a stream of its own, so other threads' work on the
-  // device is not serialized behind it (no device-wide synchronize).
+  // The build runs on the device's utility stream, so other threads' work on
+  // the device is not serialized behind it (no device-wide synchronize).
   if (hipMalloc(&d_bases, bases2.size() * 4) != hipSuccess ||
       hipMalloc(&d_scratch, (size_t)FB_RUN_WORDS * blocks * BLOCK * 4) != hipSuccess ||
-      hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+      (st = util_stream(device)) == nullptr ||
       hipMemcpyAsync(d_bases, bases2.data(), bases2.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
     (void)hipGetLastError();
     cleanup(false);
@@ -2169,7 +2189,7 @@ void fold_trim_locked(int device) {
   }
 }
 
-// The fold table of `key` built on a stream of its own: the table, or nullptr
+// The fold table of `key` built on the device's utility stream: the table, or nullptr
 // when the key cannot be folded (exceptional sums) or anything failed (the
 // scanner then adds B on its own; every partial allocation is freed).
 uint32_t* fold_build(const FoldKey& key, const uint32_t* d_fb) {
@@ -2179,8 +2199,7 @@ uint32_t* fold_build(const FoldKey& key, const uint32_t* d_fb) {
   hipStream_t st = nullptr;
   uint32_t bad = 1;
   bool ok = hipMalloc(&d, fold_table_bytes(key.bits)) == hipSuccess && hipMalloc(&d_bad, 4) == hipSuccess &&
-            hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
-            hipMemsetAsync(d_bad, 0, 4, st) == hipSuccess;
+            (st = util_stream(key.device)) != nullptr && hipMemsetAsync(d_bad, 0, 4, st) == hipSuccess;
   if (ok) {
     SpendWords sw;
     memcpy(sw.w, key.spend, sizeof(sw.w));
@@ -2191,7 +2210,6 @@ uint32_t* fold_build(const FoldKey& key, const uint32_t* d_fb) {
          hipStreamSynchronize(st) == hipSuccess;
   }
   (void)hipGetLastError();
-  if (st) (void)hipStreamDestroy(st);
   if (d_bad) (void)hipFree(d_bad);
   if (!ok || bad) {
     if (d) (void)hipFree(d);
