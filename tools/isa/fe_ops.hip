@@ -33,3 +33,12 @@ extern "C" __global__ __launch_bounds__(256, 2) void probe_inv(const uint32_t* i
 extern "C" __global__ __launch_bounds__(256, 2) void probe_loadstore(const uint32_t* in, uint32_t* out) {
   fe a; ld(a, in); st(out, a);
 }
+extern "C" __global__ __launch_bounds__(256, 2) void probe_ydbl(const uint32_t* in, uint32_t* out) {
+  gej p, r; ld(p.x, in); ld(p.y, in + 655360); ld(p.z, in + 2 * 655360);
+  gej_double_neg_yh(r, p); st(out, r.x); st(out + 655360, r.y); st(out + 2 * 655360, r.z);
+}
+extern "C" __global__ __launch_bounds__(256, 2) void probe_yadd(const uint32_t* in, uint32_t* out) {
+  gej p, r; ge q; ld(p.x, in); ld(p.y, in + 655360); ld(p.z, in + 2 * 655360);
+  ld(q.x, in + 3 * 655360); ld(q.y, in + 4 * 655360);
+  gej_add_ge_yh(r, p, q); st(out, r.x); st(out + 655360, r.y); st(out + 2 * 655360, r.z);
+}
