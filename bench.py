@@ -1044,7 +1044,9 @@ def main():
     ap.add_argument("--e2e-threads", type=int, default=0,
                     help="executor threads of the e2e leg; 0 = 8 per GPU, at most the allotted host cores")
     ap.add_argument("--e2e-reps", type=int, default=0, help="timed e2e queries (median); 0 = by table size")
-    ap.add_argument("--e2e-input", choices=["rows", "columns"], default="rows")
+    ap.add_argument("--e2e-input", choices=["rows", "columns", "vectors"], default="rows",
+                    help="how the e2e child hands chunks to the host: per-row pointers, Arrow columns, or DuckDB vectors "
+                         "(the extension's pass-through form)")
     ap.add_argument("--e2e-hw-queues", type=int, default=0,
                     help="GPU_MAX_HW_QUEUES for the e2e child; 0 = the environment's (HIP default 4)")
     ap.add_argument("--e2e-timeout", type=int, default=600)

@@ -4,7 +4,7 @@ two rounds of the fixed tests and were found by tools/soak_host.py).
 
 Streaming feeds with 4 slots (every slot rewritten many times while the
 persistent kernel runs), random threads (1..32), batch sizes down to 1 row,
-row chunks or Arrow columns, 0/1/2/16 labels, 1/3/8 logical GPUs, idle exits,
+row chunks, DuckDB vectors or Arrow columns, 0/1/2/16 labels, 1/3/8 logical GPUs, idle exits,
 protocol variants (output_count up to 13, label negation), fold on/off.  Every
 query must emit exactly its planted rows and each run's 512-row sample must
 equal the C oracle (checker use of oracle/).  Hard deadline: the soak stops

@@ -3,7 +3,7 @@ a shortened seeded form runs in the GPU suite, tests/test_soak_gpu.py).
 
 For a wall-clock budget it runs tools/host_e2e on seeded random query shapes:
 table size, executor threads, batch_size (down to a few rows: many slots and
-ring wraps), row chunks or Arrow columns, 0 / 1 / 2 / 16 label keys, fixed or
+ring wraps), row chunks, DuckDB vectors or Arrow columns, 0 / 1 / 2 / 16 label keys, fixed or
 ragged output lists, 1 / 3 / 8 logical GPUs on the one card, streaming feeds or
 per-slot launches, the streaming slot count, plain or non-temporal slot copies,
 the spend-key fold on or off, streaming kernels that leave after 1-3 ms idle
@@ -39,7 +39,7 @@ def shape(rng):
         rows=rows,
         threads=rng.choice([1, 2, 3, 8, 16, 32]),
         batch=rng.choice([1, 7, 2048, 5000, 65536, 300000]),
-        input=rng.choice(["rows", "columns"]),
+        input=rng.choice(["rows", "columns", "vectors"]),
         labels=labels,
         outputs=rng.choice([["--outputs", "1"], ["--outputs", "2"], ["--outputs", "8"], ["--outputs-max", "15"]]),
         device_map=rng.choice(["0", "0", "0,0,0", ",".join(["0"] * 8)]),
