@@ -2033,28 +2033,35 @@ size_t fb_table_bytes(int bits) {
   return windows * ((size_t)1 << (bits - 1)) * FB_WORDS * 4;
 }
 
-// One non-blocking stream per device for the library's one-off builds (the
-// fixed-base tables, the spend-key folds), created once and kept: creating
-// and destroying a stream costs ~3 + 1.5 ms, paid by a query's first key
-// otherwise (profiles/r06_cold_prewarm_hip_api_stats.csv).  The caller has
-// the device current.  Work on it is waited for with hipStreamSynchronize,
-// so it never holds up other streams.
-std::mutex g_util_mu;
-std::map<int, hipStream_t> g_util_streams;
-hipStream_t util_stream(int device) {
-  std::lock_guard<std::mutex> lk(g_util_mu);
-  auto it = g_util_streams.find(device);
-  if (it != g_util_streams.end()) return it->second;
+// The library's one-off builds (the fixed-base tables, the spend-key folds)
+// run on the stream of the scanner that needs them, or on a temporary stream
+// when there is none (cudasp_fixed_base_prepare, the synthetic tables).  Not
+// on a stream kept for the purpose: every stream a process keeps takes one of
+// the GPU_MAX_HW_QUEUES hardware queues, and the host's per-slot launch feeds
+// size their streams to the queues left (a kept build stream made two of
+// their three streams share a queue: 167 -> 107 M tx/s end to end).  A
+// temporary stream costs ~3 ms to create and ~1.5 ms to destroy, which a new
+// key's fold paid inside the query before it took the scanner's stream.
+struct BuildStream {
   hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
+  bool owned = false;
+  explicit BuildStream(hipStream_t given) : st(given) {
+    if (!st) {
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        st = nullptr;
+      } else {
+        owned = true;
+      }
+    }
   }
-  g_util_streams[device] = st;
-  return st;
-}
+  ~BuildStream() {
+    if (owned) (void)hipStreamDestroy(st);
+  }
+};
 
-int ensure_device_table(int device, int bits, const uint32_t** out, bool* built = nullptr) {
+int ensure_device_table(int device, int bits, const uint32_t** out, bool* built = nullptr,
+                        hipStream_t stream = nullptr) {
   if (!fb_bits_supported(bits))
     return set_error(CUDASP_ERR_INVALID_ARG, "fixed-base window width %d not supported (22, 26, or 7 = LDS)", bits);
   DeviceTable* dt;
@@ -2093,11 +2100,12 @@ int ensure_device_table(int device, int bits, const uint32_t** out, bool* built 
     if (d_scratch) (void)hipFree(d_scratch);
     if (!keep_table) (void)hipFree(d_table);
   };
-  // The build runs on the device's utility stream, so other threads' work on
-  // the device is not serialized behind it (no device-wide synchronize).
+  // The build runs on the caller's (or a temporary) stream, so other threads'
+  // work on the device is not serialized behind it (no device-wide synchronize).
+  BuildStream bst(stream);
   if (hipMalloc(&d_bases, bases2.size() * 4) != hipSuccess ||
       hipMalloc(&d_scratch, (size_t)FB_RUN_WORDS * blocks * BLOCK * 4) != hipSuccess ||
-      (st = util_stream(device)) == nullptr ||
+      (st = bst.st) == nullptr ||
       hipMemcpyAsync(d_bases, bases2.data(), bases2.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
     (void)hipGetLastError();
     cleanup(false);
@@ -2189,17 +2197,18 @@ void fold_trim_locked(int device) {
   }
 }
 
-// The fold table of `key` built on the device's utility stream: the table, or nullptr
+// The fold table of `key` built on `stream` (or a temporary one): the table, or nullptr
 // when the key cannot be folded (exceptional sums) or anything failed (the
 // scanner then adds B on its own; every partial allocation is freed).
-uint32_t* fold_build(const FoldKey& key, const uint32_t* d_fb) {
+uint32_t* fold_build(const FoldKey& key, const uint32_t* d_fb, hipStream_t stream) {
   DeviceGuard g(key.device);
+  BuildStream bst(stream);
   uint32_t* d = nullptr;
   uint32_t* d_bad = nullptr;
   hipStream_t st = nullptr;
   uint32_t bad = 1;
   bool ok = hipMalloc(&d, fold_table_bytes(key.bits)) == hipSuccess && hipMalloc(&d_bad, 4) == hipSuccess &&
-            (st = util_stream(key.device)) != nullptr && hipMemsetAsync(d_bad, 0, 4, st) == hipSuccess;
+            (st = bst.st) != nullptr && hipMemsetAsync(d_bad, 0, 4, st) == hipSuccess;
   if (ok) {
     SpendWords sw;
     memcpy(sw.w, key.spend, sizeof(sw.w));
@@ -2222,7 +2231,7 @@ uint32_t* fold_build(const FoldKey& key, const uint32_t* d_fb) {
 // The build runs outside g_fold_mu (an entry marked `building` holds its
 // place; other scanners of the same key wait for it, other keys and devices
 // go ahead).  *table = nullptr when the key cannot be folded.
-int fold_acquire(const FoldKey& key, const uint32_t* d_fb, const uint32_t** table) {
+int fold_acquire(const FoldKey& key, const uint32_t* d_fb, const uint32_t** table, hipStream_t stream) {
   std::unique_lock<std::mutex> lk(g_fold_mu);
   auto it = g_folds.find(key);
   if (it != g_folds.end()) {
@@ -2235,7 +2244,7 @@ int fold_acquire(const FoldKey& key, const uint32_t* d_fb, const uint32_t** tabl
   it->second.refs = 1;
   it->second.building = true;
   lk.unlock();
-  uint32_t* d = fold_build(key, d_fb);
+  uint32_t* d = fold_build(key, d_fb, stream);
   lk.lock();
   it->second.table = d;
   it->second.building = false;
@@ -2428,7 +2437,7 @@ int scanner_update_fold(cudasp_scanner* s) {
   s->consts.fb_top = nullptr;
   if (!want) return CUDASP_OK;
   const uint32_t* t = nullptr;
-  const int rc = fold_acquire(key, s->d_fb, &t);
+  const int rc = fold_acquire(key, s->d_fb, &t, s->stream);  // no work of the scanner in flight
   if (rc != CUDASP_OK) return rc;
   s->fold_held = true;
   s->fold_key = key;
@@ -2850,9 +2859,17 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
   // --- device state --------------------------------------------------------
   DeviceGuard g(device);
   s->fb_bits = default_fb_bits(device);
-  int rc = ensure_device_table(device, s->fb_bits, &s->d_fb);
+  // the scanner's stream first: a first scanner builds the device's
+  // fixed-base table on it
+  hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    s->stream = nullptr;
+    free_scanner(s);
+    return set_error(CUDASP_ERR_HIP, "hipStreamCreate failed: %s", hipGetErrorString(e));
+  }
+  int rc = ensure_device_table(device, s->fb_bits, &s->d_fb, nullptr, s->stream);
   if (rc != CUDASP_OK) {
-    delete s;
+    free_scanner(s);
     return rc;
   }
   // One scratch slot per thread of the largest launch; each scratch buffer is
@@ -2903,11 +2920,6 @@ int cudasp_scanner_create(int device, const uint8_t scan_private_key[32], const 
   ALLOC(s->d_labels, labels.size() * 4);
 #undef ALLOC
   // d_t / d_vscratch / d_lscratch: on first stage-kernel use (ensure_stage_buffers)
-  hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
-  if (e != hipSuccess) {
-    free_scanner(s);
-    return set_error(CUDASP_ERR_HIP, "hipStreamCreate failed: %s", hipGetErrorString(e));
-  }
   e = hipMemcpy(s->d_naf, naf.data(), naf.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_labels, labels.data(), labels.size() * 4, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -3092,7 +3104,7 @@ int cudasp_scanner_set_fixed_base_bits(cudasp_scanner* s, int bits) {
   DeviceGuard g(s->device);
   HIP_TRY(hipStreamSynchronize(s->stream));
   const uint32_t* fb = nullptr;
-  int rc = ensure_device_table(s->device, bits, &fb);
+  int rc = ensure_device_table(s->device, bits, &fb, nullptr, s->stream);
   if (rc != CUDASP_OK) return rc;
   s->d_fb = fb;
   s->fb_bits = bits;
