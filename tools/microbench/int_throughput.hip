@@ -16,6 +16,8 @@ __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t 
   uint32_t a[8], b[8];
   uint64_t acc[8];
   double f[8];
+  uint32_t smask;
+  asm volatile("s_mov_b32 %0, 0x1fffffff" : "=s"(smask));
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     a[i] = seed * (threadIdx.x + 3 * i + 1) + blockIdx.x;
@@ -55,6 +57,46 @@ __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t 
           asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(a[k]) : "v"(b[k]));
         } else if constexpr (OP == 11) {  // 64-bit add via v_lshl_add_u64 (gfx940+)
           asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(acc[k]) : "v"(acc[(k+1)&7]));
+        } else if constexpr (OP == 12) {  // VOP2 with a 32-bit literal (8 bytes)
+          asm volatile("v_and_b32_e32 %0, 0x1fffffff, %0" : "+v"(a[k]));
+        } else if constexpr (OP == 13) {  // the same with the mask in an SGPR (4 bytes)
+          asm volatile("v_and_b32_e32 %0, %1, %0" : "+v"(a[k]) : "s"(smask));
+        } else if constexpr (OP == 14) {  // the same op in the VOP3 encoding (8 bytes)
+          asm volatile("v_and_b32_e64 %0, %1, %0" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 15) {  // VOP2 subtract from a literal (fe_negate's form)
+          asm volatile("v_sub_u32_e32 %0, 0x3ffffffe, %0" : "+v"(a[k]));
+        } else if constexpr (OP == 16) {  // the same from an SGPR
+          asm volatile("v_sub_u32_e32 %0, %1, %0" : "+v"(a[k]) : "s"(smask));
+        } else if constexpr (OP == 17) {  // 64-bit shift (the reductions' carry)
+          asm volatile("v_lshrrev_b64 %0, 29, %0" : "+v"(acc[k]));
+        } else if constexpr (OP == 18) {  // one mad + one literal and (a reduction's pair)
+          asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_and_b32_e32 %1, 0x1fffffff, %1"
+                       : "+v"(acc[k]), "+v"(a[k]) : "v"(b[k]), "v"(b[(k + 1) & 7]) : "vcc");
+        } else if constexpr (OP == 19) {  // one mad + one SGPR-mask and
+          asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_and_b32_e32 %1, %4, %1"
+                       : "+v"(acc[k]), "+v"(a[k]) : "v"(b[k]), "v"(b[(k + 1) & 7]), "s"(smask) : "vcc");
+        } else if constexpr (OP == 20) {  // four mads + one literal and (~the ladder's ratio)
+          asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_mad_u64_u32 %0, vcc, %3, %2, %0\n\t"
+                       "v_mad_u64_u32 %0, vcc, %2, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %3, %0\n\t"
+                       "v_and_b32_e32 %1, 0x1fffffff, %1"
+                       : "+v"(acc[k]), "+v"(a[k]) : "v"(b[k]), "v"(b[(k + 1) & 7]) : "vcc");
+        } else if constexpr (OP == 21) {  // four mads + one SGPR-mask and
+          asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_mad_u64_u32 %0, vcc, %3, %2, %0\n\t"
+                       "v_mad_u64_u32 %0, vcc, %2, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %3, %0\n\t"
+                       "v_and_b32_e32 %1, %4, %1"
+                       : "+v"(acc[k]), "+v"(a[k]) : "v"(b[k]), "v"(b[(k + 1) & 7]), "s"(smask) : "vcc");
+        } else if constexpr (OP == 22) {  // four mads alone (the base of 20/21)
+          asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0\n\tv_mad_u64_u32 %0, vcc, %2, %1, %0\n\t"
+                       "v_mad_u64_u32 %0, vcc, %1, %1, %0\n\tv_mad_u64_u32 %0, vcc, %2, %2, %0"
+                       : "+v"(acc[k]) : "v"(b[k]), "v"(b[(k + 1) & 7]) : "vcc");
+        } else if constexpr (OP == 23) {  // mad with an SGPR multiplier (the reductions' fold terms)
+          asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc[k]) : "v"(b[k]), "s"(smask) : "vcc");
+        } else if constexpr (OP == 24) {  // mad with an inline-constant multiplier
+          asm volatile("v_mad_u64_u32 %0, vcc, %1, 8, %0" : "+v"(acc[k]) : "v"(b[k]) : "vcc");
+        } else if constexpr (OP == 25) {  // VOP2 add of two VGPRs in the VOP3 encoding
+          asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 26) {  // VOP2 shift by an inline constant
+          asm volatile("v_lshlrev_b32_e32 %0, 1, %0" : "+v"(a[k]));
         }
       }
     }
@@ -111,6 +153,22 @@ int main() {
   run<6>("v_mad_u32_u24", 1, blocks, d);
   run<7>("v_mul_hi_u32_u24", 1, blocks, d);
   run<5>("v_fma_f64", 1, blocks, d);
+  // encodings: a VOP2 op with a literal, with an SGPR, in VOP3 form; mixes
+  run<12>("v_and_b32 literal (8 B)", 1, blocks, d);
+  run<13>("v_and_b32 sgpr (4 B)", 1, blocks, d);
+  run<14>("v_and_b32_e64 (8 B)", 1, blocks, d);
+  run<15>("v_sub_u32 literal (8 B)", 1, blocks, d);
+  run<16>("v_sub_u32 sgpr (4 B)", 1, blocks, d);
+  run<17>("v_lshrrev_b64", 1, blocks, d);
+  run<18>("mad + and literal (2 ins)", 2, blocks, d);
+  run<19>("mad + and sgpr (2 ins)", 2, blocks, d);
+  run<20>("4 mad + and literal (5 ins)", 5, blocks, d);
+  run<21>("4 mad + and sgpr (5 ins)", 5, blocks, d);
+  run<22>("4 mad (4 ins)", 4, blocks, d);
+  run<23>("v_mad_u64_u32 sgpr operand", 1, blocks, d);
+  run<24>("v_mad_u64_u32 inline const", 1, blocks, d);
+  run<25>("v_add_u32_e64 (8 B)", 1, blocks, d);
+  run<26>("v_lshlrev_b32 inline (4 B)", 1, blocks, d);
   CHK(hipFree(d));
   return 0;
 }
