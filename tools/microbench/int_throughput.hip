@@ -97,6 +97,32 @@ __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t 
           asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(a[k]) : "v"(b[k]));
         } else if constexpr (OP == 26) {  // VOP2 shift by an inline constant
           asm volatile("v_lshlrev_b32_e32 %0, 1, %0" : "+v"(a[k]));
+        } else if constexpr (OP == 27) {  // doubling as an add of the same VGPR twice
+          asm volatile("v_add_u32_e32 %0, %0, %0" : "+v"(a[k]));
+        } else if constexpr (OP == 28) {  // VOP2 and with an inline constant
+          asm volatile("v_and_b32_e32 %0, 1, %0" : "+v"(a[k]));
+        } else if constexpr (OP == 29) {  // VOP2 shift right by an inline constant
+          asm volatile("v_lshrrev_b32_e32 %0, 29, %0" : "+v"(a[k]));
+        } else if constexpr (OP == 30) {  // VOP2 add of a literal
+          asm volatile("v_add_u32_e32 %0, 0x3ffffffe, %0" : "+v"(a[k]));
+        } else if constexpr (OP == 31) {  // VOP2 shift by a VGPR amount
+          asm volatile("v_lshlrev_b32_e32 %0, %1, %0" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 32) {  // VOP1 move of a VGPR
+          asm volatile("v_mov_b32_e32 %0, %1" : "=v"(a[k]) : "v"(b[(k + 1) & 7]));
+        } else if constexpr (OP == 33) {  // VOP2 and of two VGPRs
+          asm volatile("v_and_b32_e32 %0, %0, %1" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 34) {  // VOP2 sub of two VGPRs
+          asm volatile("v_sub_u32_e32 %0, %1, %0" : "+v"(a[k]) : "v"(b[k]));
+        } else if constexpr (OP == 35) {  // 4 mads + 1 shift by inline constant (the sqr prologue's form)
+          asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_mad_u64_u32 %0, vcc, %3, %2, %0\n\t"
+                       "v_mad_u64_u32 %0, vcc, %2, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %3, %0\n\t"
+                       "v_lshlrev_b32_e32 %1, 1, %1"
+                       : "+v"(acc[k]), "+v"(a[k]) : "v"(b[k]), "v"(b[(k + 1) & 7]) : "vcc");
+        } else if constexpr (OP == 36) {  // 4 mads + 1 doubling add
+          asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_mad_u64_u32 %0, vcc, %3, %2, %0\n\t"
+                       "v_mad_u64_u32 %0, vcc, %2, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %3, %0\n\t"
+                       "v_add_u32_e32 %1, %1, %1"
+                       : "+v"(acc[k]), "+v"(a[k]) : "v"(b[k]), "v"(b[(k + 1) & 7]) : "vcc");
         }
       }
     }
@@ -169,6 +195,16 @@ int main() {
   run<24>("v_mad_u64_u32 inline const", 1, blocks, d);
   run<25>("v_add_u32_e64 (8 B)", 1, blocks, d);
   run<26>("v_lshlrev_b32 inline (4 B)", 1, blocks, d);
+  run<27>("v_add_u32 x, x (doubling)", 1, blocks, d);
+  run<28>("v_and_b32 inline const", 1, blocks, d);
+  run<29>("v_lshrrev_b32 inline", 1, blocks, d);
+  run<30>("v_add_u32 literal", 1, blocks, d);
+  run<31>("v_lshlrev_b32 vgpr amount", 1, blocks, d);
+  run<32>("v_mov_b32 vgpr", 1, blocks, d);
+  run<33>("v_and_b32 vgpr, vgpr", 1, blocks, d);
+  run<34>("v_sub_u32 vgpr, vgpr", 1, blocks, d);
+  run<35>("4 mad + lshl inline (5 ins)", 5, blocks, d);
+  run<36>("4 mad + add x,x (5 ins)", 5, blocks, d);
   CHK(hipFree(d));
   return 0;
 }
