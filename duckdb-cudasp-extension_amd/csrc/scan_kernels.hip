@@ -525,6 +525,19 @@ struct MultiTick {
 // start and end (it is its SIMD's oldest wave and runs until the drain).
 __device__ uint64_t g_multi_clock[4];
 
+// The odd-multiple table's y of entries 0 .. N-1 in LDS (LdsY, scan_rows.hpp;
+// 0: all in scratch).  Three blocks per CU leave room for 5 (45 KB of the 53 KB
+// a block may have; k_scan_stream's prefetch transpose shares the area).  The
+// scratch traffic they take off (~25%) is energy under the power cap: +0.9%
+// config 4 device-resident (k_scan_multi, at a higher clock), +1.0% end to end
+// (k_scan_stream; profiles/r06_lds_y_ab.txt).
+#ifndef CUDASP_MULTI_LDS_Y
+#define CUDASP_MULTI_LDS_Y 5
+#endif
+#ifndef CUDASP_STREAM_LDS_Y
+#define CUDASP_STREAM_LDS_Y 5
+#endif
+
 template <int FBB, bool PIPE>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const MultiBatch* __restrict__ bd, uint32_t nb,
                                                                    uint32_t total_wr, const int8_t* __restrict__ naf,
@@ -537,6 +550,11 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const Scratch sc = make_scratch(scr, gridDim.x * blockDim.x, slot);
   const uint32_t lane = threadIdx.x & 63u;
+#if CUDASP_MULTI_LDS_Y
+  // the y of odd multiples 0 .. CUDASP_MULTI_LDS_Y - 1 (LdsY): 45 KB per block
+  // at 5, so three blocks per CU fit the 160 KB
+  __shared__ uint32_t ytab[CUDASP_MULTI_LDS_Y * FW][BLOCK];
+#endif
   constexpr int PB = VB_SCRATCH_WORDS;                             // pending rows
   constexpr int LB = VB_SCRATCH_WORDS + PEND_WORDS * multi_pend_slots(PIPE);  // label prefix products
   const int QF = LB + FW * (int)k.label_count * MULTI_RMAX;  // PIPE: piece Q's affine F (x, y per row)
@@ -612,8 +630,13 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const Mult
         y[q] = b.ty[(size_t)q * b.n + r];
       }
       gej P;
+#if CUDASP_MULTI_LDS_Y
+      row_shared_secret_point_t(P, x, y, naf, k.naf_len, sc, MultiTick{counter, total_wr, &out, drain_level},
+                                LdsY<CUDASP_MULTI_LDS_Y>{&ytab[0][threadIdx.x], BLOCK});
+#else
       row_shared_secret_point_t(P, x, y, naf, k.naf_len, sc,
                                 MultiTick{counter, total_wr, &out, drain_level});
+#endif
       pend_store(sc, PB, count_p + j, P);
     }
 #if CUDASP_MULTI_TRACE
@@ -1318,8 +1341,20 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
   __shared__ StreamWave waves[BLOCK / 64];
   __shared__ StreamWr wrs[BLOCK / 64][3][MULTI_RMAX];
   __shared__ StreamPf pfs[BLOCK / 64][MULTI_RMAX];
-  __shared__ uint4 pftr[BLOCK / 64][256];  // the row blobs' transpose (stream_prefetch, coal)
   const uint32_t wid = threadIdx.x >> 6;
+#if CUDASP_STREAM_LDS_Y
+  // LdsY as in k_scan_multi, wave-major (a wave's y entries are one contiguous
+  // area, 11.25 KB at 5), whose first 4 KB double as the prefetch's transpose
+  // buffer: the prefetch runs between pieces, when no row's table is live, and a
+  // wave's LDS operations complete in order
+  constexpr int YW = CUDASP_STREAM_LDS_Y * FW * 64 > 1024 ? CUDASP_STREAM_LDS_Y * FW * 64 : 1024;
+  __shared__ uint4 ywave[BLOCK / 64][YW / 4];
+  uint4* const pftr_w = ywave[wid];  // the row blobs' transpose (stream_prefetch, coal)
+  const LdsY<CUDASP_STREAM_LDS_Y> ytab{reinterpret_cast<uint32_t*>(ywave[wid]) + lane, 64};
+#else
+  __shared__ uint4 pftr[BLOCK / 64][256];  // the row blobs' transpose (stream_prefetch, coal)
+  uint4* const pftr_w = pftr[wid];
+#endif
   volatile StreamWave& me = waves[wid];
   if (lane == 0) {
     // the first ticket: one wave-row, worker w's at first_wr + w (k_stream_start)
@@ -1423,7 +1458,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
 #endif
     StreamWr* const wn = wrs[wid][pn];
     const int meta_n = META + 2 * MULTI_RMAX * pn;
-    if (count) stream_prefetch(dev, hint, base, count, lane, wn, pfs[wid], sc, STG, meta_n, ow, pf_coal != 0, pftr[wid]);
+    if (count) stream_prefetch(dev, hint, base, count, lane, wn, pfs[wid], sc, STG, meta_n, ow, pf_coal != 0, pftr_w);
     const int np = count_p * K;  // F points of piece P in pending slots 0 .. np - 1
     // stage A: S = d T of the new piece's rows (staged by the prefetch)
 #pragma unroll 1
@@ -1432,7 +1467,11 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
 #pragma unroll
       for (int q = 0; q < 16; q++) w[q] = scr_load_w(sc, STG + 16 * j + q);
       gej P;
+#if CUDASP_STREAM_LDS_Y
+      row_shared_secret_point_t(P, w, w + 8, naf, k.naf_len, sc, tick, ytab);
+#else
       row_shared_secret_point_t(P, w, w + 8, naf, k.naf_len, sc, tick);
+#endif
       pend_store(sc, PB, np + j, P);
     }
     // one inversion: the new S points, piece P's F points, piece Q's label product

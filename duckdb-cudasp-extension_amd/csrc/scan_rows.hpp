@@ -156,6 +156,45 @@ CUDASP_HD int8_t uniform_digit(const int8_t* p, int i) {
 #endif
 }
 
+// Where the odd-multiple table's y coordinates live (row_shared_secret_point_t).
+// ScrY: all in scratch.  LdsY<N>: entries 0 .. N-1 in the workgroup's LDS
+// (word w of this thread at p[w * stride], stride = the block's threads, so a
+// wave's accesses are conflict-free), the rest in scratch: y is read by every
+// addition (x only by its half's), so an LDS word of y saves the most
+// scratch traffic, which costs clock under the power cap.
+struct ScrY {
+  CUDASP_HD bool has(int) const { return false; }
+  CUDASP_HD void store(int, const fe&) const {}
+  CUDASP_HD void load(fe&, int) const {}
+};
+
+template <int N>
+struct LdsY {
+  uint32_t* p;
+  uint32_t stride;
+  CUDASP_HD bool has(int e) const { return e < N; }
+  CUDASP_HD void store(int e, const fe& a) const {
+#pragma unroll
+    for (int l = 0; l < FE_LIMBS; l++) p[(uint32_t)(e * FE_LIMBS + l) * stride] = a.n[l];
+  }
+  CUDASP_HD void load(fe& a, int e) const {
+#pragma unroll
+    for (int l = 0; l < FE_LIMBS; l++) a.n[l] = p[(uint32_t)(e * FE_LIMBS + l) * stride];
+  }
+};
+
+template <class YTab>
+CUDASP_HD void tab_store_y(const Scratch& sc, const YTab& yt, int e, const fe& a) {
+  if (yt.has(e)) yt.store(e, a);
+  else scr_store(sc, VB_ENTRY_Y(e), a);
+}
+
+template <class YTab>
+CUDASP_HD void tab_load_y(fe& a, const Scratch& sc, const YTab& yt, int e) {
+  if (yt.has(e)) yt.load(a, e);
+  else scr_load(a, sc, VB_ENTRY_Y(e));
+}
+
 // A ladder hook that does nothing (row_shared_secret_point_t).
 struct NoTick {
   CUDASP_HD void ladder(int, uint32_t) const {}
@@ -166,9 +205,10 @@ struct NoTick {
 // layout).  naf: 2 * NAF_MAX digits (GLV half 1, then half 2, signs folded in).
 // tick.ladder(i, naf_len) runs every 16 ladder steps, i the digits still to
 // go (the persistent kernels re-prioritise their waves there).
-template <class Tick>
+template <class Tick, class YTab = ScrY>
 CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uint32_t ty[8], const int8_t* naf,
-                                         uint32_t naf_len, const Scratch& sc, const Tick& tick) {
+                                         uint32_t naf_len, const Scratch& sc, const Tick& tick,
+                                         const YTab& yt = YTab()) {
   ge T;
   fe_from_u32x8(T.x, tx);
   fe_from_u32x8(T.y, ty);
@@ -187,7 +227,7 @@ CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uin
     gej D, acc;
     gej_dblu(D, acc, T);
     scr_store(sc, VB_ENTRY_X(0), acc.x);
-    scr_store(sc, VB_ENTRY_Y(0), acc.y);
+    tab_store_y(sc, yt, 0, acc.y);
     for (int e = 1; e < VB_ENTRIES; e++) {
       fe zr;
       gej nxt;
@@ -206,7 +246,7 @@ CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uin
 #endif
       }
       scr_store(sc, VB_ENTRY_X(e), acc.x);
-      scr_store(sc, VB_ENTRY_Y(e), acc.y);
+      tab_store_y(sc, yt, e, acc.y);
       scr_store(sc, VB_ZR(e - 1), zr);
     }
     scr_store(sc, VB_CZ, acc.z);  // Zg
@@ -217,7 +257,7 @@ CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uin
     for (int e = VB_ENTRIES - 2; e >= 0; e--) {
       fe x, y, r2, r3;
       scr_load(x, sc, VB_ENTRY_X(e));
-      scr_load(y, sc, VB_ENTRY_Y(e));
+      tab_load_y(y, sc, yt, e);
       fe_sqr(r2, ratio);
       fe_mul(r3, r2, ratio);
       fe_mul(x, x, r2);
@@ -226,7 +266,7 @@ CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uin
 #endif
       fe_mul(y, y, r3);
       scr_store(sc, VB_ENTRY_X(e), x);
-      scr_store(sc, VB_ENTRY_Y(e), y);
+      tab_store_y(sc, yt, e, y);
 #if CUDASP_PHI_TABLE
       fe_mul(x, x, beta);
       scr_store(sc, VB_ENTRY_XB(e), x);
@@ -258,7 +298,7 @@ CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uin
       const int d = hf ? d1 : d0;
       const int e = (d < 0 ? -d : d) >> 1;
       scr_load(Pn.x, sc, hf ? VB_ENTRY_XB(e) : VB_ENTRY_X(e));
-      scr_load(Pn.y, sc, VB_ENTRY_Y(e));
+      tab_load_y(Pn.y, sc, yt, e);
     }
     if (!inf) {
       gej_double_neg_yh(R, R);
@@ -274,7 +314,7 @@ CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uin
         } else {
           const int e = (d < 0 ? -d : d) >> 1;
           scr_load(P.x, sc, VB_ENTRY_XB(e));
-          scr_load(P.y, sc, VB_ENTRY_Y(e));
+          tab_load_y(P.y, sc, yt, e);
         }
         if ((d < 0) != sgn_neg) fe_negate<2>(P.y, P.y);
         if (inf) {
@@ -310,7 +350,7 @@ CUDASP_HD void row_shared_secret_point_t(gej& R, const uint32_t tx[8], const uin
         scr_load(P.x, sc, VB_ENTRY_X(e));
         if (half) fe_mul(P.x, P.x, beta);
 #endif
-        scr_load(P.y, sc, VB_ENTRY_Y(e));
+        tab_load_y(P.y, sc, yt, e);
 #if LADDER_YH
         if ((d < 0) != sgn_neg) fe_negate<2>(P.y, P.y);
         if (inf) {

@@ -8,10 +8,12 @@
 # bench part alone).
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${MEASURE_TAG:-r06}_enc; mkdir -p $O; cd $R
-timeout -k 10 120 ./tools/microbench/int_throughput > $O/int_throughput.txt 2>&1 || { echo "microbench failed"; cat $O/int_throughput.txt; exit 1; }
-cat $O/int_throughput.txt
+if [ -z "$SKIP_MB" ]; then
+  timeout -k 10 120 ./tools/microbench/int_throughput > $O/int_throughput.txt 2>&1 || { echo "microbench failed"; cat $O/int_throughput.txt; exit 1; }
+  cat $O/int_throughput.txt
+fi
 B="python3 -u bench.py --no-cpu-baseline --no-e2e --no-layout-probe --no-cold-start --idle-samples 0 --exclusive-batches 0"
-for pass in 1 2 3; do
+for pass in $(seq 1 ${PASSES:-3}); do
   for v in ${VARIANTS:-default smask sconst}; do
     lib=duckdb-cudasp-extension_amd/libcudasp_amd.so; [ $v != default ] && lib=ab/$v/libcudasp_amd.so
     f=$O/${v}_$pass.json
