@@ -125,6 +125,20 @@ __device__ __forceinline__ void store_t(uint32_t* __restrict__ t_out, uint32_t n
   }
 }
 
+// The odd-multiple table's y of entries 0 .. N-1 in LDS (LdsY, scan_rows.hpp;
+// 0: all in scratch).  Three blocks per CU leave room for 5 (45 KB of the 53 KB
+// a block may have; k_scan_stream's prefetch transpose shares the area).  The
+// scratch traffic they take off (~25%) is energy under the power cap: +0.9%
+// config 4 device-resident (k_scan_multi, at a higher clock), +1.0% end to end
+// (k_scan_stream; profiles/r06_lds_y_ab.txt).  k_shared_secret (the per-slot
+// launches' stage A) uses CUDASP_MULTI_LDS_Y too.
+#ifndef CUDASP_MULTI_LDS_Y
+#define CUDASP_MULTI_LDS_Y 5
+#endif
+#ifndef CUDASP_STREAM_LDS_Y
+#define CUDASP_STREAM_LDS_Y 5
+#endif
+
 // Stage A: thread `slot` takes the rows g, g + G, ... (G = ceil(n / R)) of
 // each of its groups g, so every row access stays coalesced.  R = ROWS_A rows
 // per thread share one inversion; launches too small to fill the GPU use 2 or
@@ -148,6 +162,12 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
   const Scratch& sc_tab = sc;
   const Scratch& sc_pend = sc;
 #endif
+#if CUDASP_MULTI_LDS_Y
+  __shared__ uint32_t ytab[CUDASP_MULTI_LDS_Y * FW][BLOCK];
+  const LdsY<CUDASP_MULTI_LDS_Y> yt{&ytab[0][threadIdx.x], BLOCK};
+#else
+  const ScrY yt;
+#endif
   if constexpr (R == 1) {
     for (uint32_t row = slot; row < n; row += stride) {
       uint32_t x[8], y[8];
@@ -157,7 +177,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
         y[w] = ty[(size_t)w * n + row];
       }
       gej P;
-      row_shared_secret_point(P, x, y, naf, k.naf_len, sc);
+      row_shared_secret_point_t(P, x, y, naf, k.naf_len, sc, NoTick(), yt);
       fe zi;
       fe_inv(zi, P.z);
       uint32_t sx[8];
@@ -181,7 +201,7 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_shared_secret(const u
         y[w] = ty[(size_t)w * n + row];
       }
       gej P;
-      row_shared_secret_point(P, x, y, naf, k.naf_len, sc_tab);
+      row_shared_secret_point_t(P, x, y, naf, k.naf_len, sc_tab, NoTick(), yt);
       pend_store(sc_pend, PB, j, P);
       count = j + 1;
     }
@@ -525,18 +545,6 @@ struct MultiTick {
 // start and end (it is its SIMD's oldest wave and runs until the drain).
 __device__ uint64_t g_multi_clock[4];
 
-// The odd-multiple table's y of entries 0 .. N-1 in LDS (LdsY, scan_rows.hpp;
-// 0: all in scratch).  Three blocks per CU leave room for 5 (45 KB of the 53 KB
-// a block may have; k_scan_stream's prefetch transpose shares the area).  The
-// scratch traffic they take off (~25%) is energy under the power cap: +0.9%
-// config 4 device-resident (k_scan_multi, at a higher clock), +1.0% end to end
-// (k_scan_stream; profiles/r06_lds_y_ab.txt).
-#ifndef CUDASP_MULTI_LDS_Y
-#define CUDASP_MULTI_LDS_Y 5
-#endif
-#ifndef CUDASP_STREAM_LDS_Y
-#define CUDASP_STREAM_LDS_Y 5
-#endif
 
 template <int FBB, bool PIPE>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const MultiBatch* __restrict__ bd, uint32_t nb,
