@@ -101,3 +101,31 @@ def test_committed_multi_profiles_have_bench_keys():
     assert k["SQ_INSTS_VALU"] > 0 and k["GRBM_GUI_ACTIVE"] > 0 and sq["multi_rows_per_launch"] == 32_700_000
     hbm = json.load(open(os.path.join(ROOT, "profiles", "r06_pmc_hbm_multi.json")))
     assert hbm["multi_hbm_bytes_per_row"] > 0 and hbm["probe_hbm_bytes_per_row"] > 0
+
+
+def test_stage_a_kernels_keep_three_blocks_per_cu():
+    """The stage-A kernels run three 256-thread blocks per CU (CUDASP_WAVES_A,
+    the persistent grids are sized for it): each block's LDS (the odd-multiple
+    table's y, LdsY; the stream kernel's own) must fit a third of gfx950's
+    160 KB, and its VGPRs a third of 512 per SIMD lane.  Read from the built
+    code object's kernel descriptors, so a larger CUDASP_*_LDS_Y cannot lower
+    the occupancy unnoticed."""
+    import struct
+    import pytest
+    co = _codeobj()
+    if not os.path.exists(_lib_path()):
+        pytest.skip("library not built")
+    elf = co.code_objects(_lib_path())[0][1]
+    syms, secs = co.symbols(elf)
+    seen = 0
+    for name, (val, size, typ, shndx) in syms.items():
+        if not name.endswith(".kd") or not any(k in name for k in ("k_scan_multi", "k_scan_stream", "k_shared_secret")):
+            continue
+        kd = co._bytes_at(elf, secs, shndx, val, 64)
+        lds, = struct.unpack_from("<I", kd, 0)
+        rsrc1, = struct.unpack_from("<I", kd, 48)
+        vgprs = ((rsrc1 & 0x3F) + 1) * 8  # gfx950: granules of 8, AGPRs included
+        assert 3 * lds <= 160 * 1024, (name, lds)
+        assert 3 * vgprs <= 512, (name, vgprs)
+        seen += 1
+    assert seen >= 8
