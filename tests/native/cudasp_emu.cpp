@@ -333,6 +333,46 @@ int emu_shared_secret(const uint8_t scan[32], const uint8_t* tweaks, uint32_t n,
   return 0;
 }
 
+// Stage A for n rows with the odd-multiple table's y split as the kernels
+// split it (LdsY<5>: entries 0..4 in `lds`, word w at lds[w * lds_stride],
+// standing in for the workgroup's LDS; the rest in scratch): t as 8 LE u32
+// words per row.  lds_stride > 1 leaves the other slots of the column alone,
+// as the other lanes' are in the kernels; the scratch poison catches an entry
+// read from the wrong side.
+int emu_shared_secret_lds_y(const uint8_t scan[32], const uint8_t* tweaks, uint32_t n, uint32_t lds_stride,
+                            uint32_t* t_out) {
+  if (lds_stride == 0) return CUDASP_ERR_INVALID_ARG;
+  host::Big<8> d = host::big_zero<8>();
+  for (int i = 0; i < 32; i++) d.w[i / 4] |= (uint32_t)scan[i] << (8 * (i % 4));
+  d = host::scalar_reduce(d);
+  if (host::big_is_zero(d)) return CUDASP_ERR_INVALID_ARG;
+  std::vector<int8_t> naf(2 * NAF_MAX, 0);
+  uint32_t naf_len = 0;
+  if (host::scan_digits(d, naf.data(), NAF_MAX, &naf_len) != 0) return CUDASP_ERR_INVALID_ARG;
+  uint32_t mid[8];
+  bip352_midstate(mid);
+  std::vector<uint32_t> scratch(VB_SCRATCH_WORDS, 0xA5A5A5A5u);
+  std::vector<uint32_t> lds((size_t)5 * FW * lds_stride, 0x5A5A5A5Au);
+  Scratch sc{scratch.data(), 1, 0};
+  const LdsY<5> yt{lds.data(), lds_stride};
+  for (uint32_t r = 0; r < n; r++) {
+    uint32_t x[8], y[8];
+    words_from_row(x, y, tweaks + 64 * (size_t)r);
+    // entries 0..4 must never touch their scratch y words
+    for (int e = 0; e < 5; e++)
+      for (int l = 0; l < FW; l++) scratch[VB_ENTRY_Y(e) + l] = 0xDEADBEEFu;
+    gej R;
+    row_shared_secret_point_t(R, x, y, naf.data(), naf_len, sc, NoTick(), yt);
+    for (int e = 0; e < 5; e++)
+      for (int l = 0; l < FW; l++)
+        if (scratch[VB_ENTRY_Y(e) + l] != 0xDEADBEEFu) return -1;
+    fe zi;
+    fe_inv(zi, R.z);
+    row_shared_secret_finish(t_out + 8 * (size_t)r, R, zi, mid);
+  }
+  return 0;
+}
+
 // Full pipeline values for n rows: values[r * (1 + L) + j] (j = 0 base, 1.. labels);
 // t_out (optional) 8 words per row; flags (optional) with the outputs CSR.
 int emu_row_values(const uint8_t scan[32], const uint8_t spend[64], const uint8_t* labels_bytes, uint32_t L,

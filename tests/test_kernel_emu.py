@@ -310,6 +310,26 @@ def test_against_oracle_random_keys(emu):
         assert (v == ov).all()
 
 
+def test_lds_y_split_equals_scratch_table(emu):
+    """The kernels keep the y of odd multiples 1T..9T in LDS (LdsY<5>) and the
+    rest in scratch: the same stage A with that split (a host array standing
+    in for the LDS, another lane's slots interleaved) gives the t of the
+    all-scratch table, and never touches those entries' scratch words."""
+    emu.emu_shared_secret_lds_y.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_void_p]
+    rng = random.Random(52)
+    k = golden_io.load("stage_kats.json")[0]
+    keys = [bytes.fromhex(k["scan_key"])] + [rng.randrange(1, N).to_bytes(32, "little") for _ in range(2)]
+    spend = _le(_mul(7))
+    for scan in keys:
+        tw = b"".join(_le(_mul(rng.randrange(1, N))) for _ in range(4))
+        _, t_ref, _ = _values(emu, scan, spend, [], tw)
+        for stride in (1, 64):
+            t = (ctypes.c_uint32 * (8 * 4))()
+            assert emu.emu_shared_secret_lds_y(scan, tw, 4, stride, t) == 0
+            assert (np.frombuffer(t, dtype=np.uint32).reshape(4, 8) == t_ref).all()
+
+
 def test_exceptional_labels(emu):
     """Label == F doubles, label == -F is infinity (reference Python oracle
     semantics, scripts/compute_bip352_expected.py:42-46)."""
