@@ -545,7 +545,6 @@ struct MultiTick {
 // start and end (it is its SIMD's oldest wave and runs until the drain).
 __device__ uint64_t g_multi_clock[4];
 
-
 template <int FBB, bool PIPE>
 __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_multi(const MultiBatch* __restrict__ bd, uint32_t nb,
                                                                    uint32_t total_wr, const int8_t* __restrict__ naf,

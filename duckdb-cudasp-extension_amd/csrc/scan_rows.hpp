@@ -158,8 +158,9 @@ CUDASP_HD int8_t uniform_digit(const int8_t* p, int i) {
 
 // Where the odd-multiple table's y coordinates live (row_shared_secret_point_t).
 // ScrY: all in scratch.  LdsY<N>: entries 0 .. N-1 in the workgroup's LDS
-// (word w of this thread at p[w * stride], stride = the block's threads, so a
-// wave's accesses are conflict-free), the rest in scratch: y is read by every
+// (word w of this thread at p[w * stride], stride = the threads sharing the
+// array -- the block's, or the wave's 64 -- so a wave's accesses are
+// conflict-free), the rest in scratch: y is read by every
 // addition (x only by its half's), so an LDS word of y saves the most
 // scratch traffic, which costs clock under the power cap.
 struct ScrY {
