@@ -138,6 +138,8 @@ __device__ __forceinline__ void store_t(uint32_t* __restrict__ t_out, uint32_t n
 #ifndef CUDASP_STREAM_LDS_Y
 #define CUDASP_STREAM_LDS_Y 5
 #endif
+static_assert(CUDASP_WAVES_A * CUDASP_MULTI_LDS_Y * FW * BLOCK * 4 <= 160 * 1024,
+              "k_scan_multi's LDS y table must leave CUDASP_WAVES_A blocks per CU");
 
 // Stage A: thread `slot` takes the rows g, g + G, ... (G = ceil(n / R)) of
 // each of its groups g, so every row access stays coalesced.  R = ROWS_A rows
