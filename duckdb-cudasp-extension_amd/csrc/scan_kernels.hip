@@ -1695,20 +1695,25 @@ __global__ __launch_bounds__(BLOCK, CUDASP_WAVES_A) void k_scan_stream(StreamCtr
 }
 
 // The fixed-base table of `windows` windows of `entries` odd multiples each
-// (the width's FbWidth), built in runs: a thread takes FB_RUN
-// consecutive odd multiples (2j+1) Q, j = j0 .. j0 + FB_RUN - 1, of one
+// (the width's FbWidth), built in runs: a thread takes run_len (FB_RUN, or
+// the window's entries if fewer) consecutive odd multiples (2j+1) Q,
+// j = j0 .. j0 + run_len - 1, of one
 // window's base Q -- the first by double-and-add, each next one by adding
-// D = 2Q -- keeps them Jacobian in its scratch with the running product of
-// their Z, inverts that product once, and walks back writing each entry's
-// normalized affine words (Montgomery's batch inversion).  Per entry: one
-// mixed addition, three multiplications and the affine conversion, against
-// ~25 doublings, ~12 additions and one inversion for an entry computed on its
-// own (fb_build_entry; 0.55 s for the 26-bit table that way) -- and the same
-// words, since an entry is the unique normalized affine point (k_fb_check).  Scratch:
-// FB_RUN x 4 field elements (X, Y, Z, prefix product) of raw limbs per
-// thread, limb-major over the grid's threads (coalesced).
-constexpr uint32_t FB_RUN = 32;
-constexpr uint32_t FB_RUN_WORDS = FB_RUN * 4 * FE_LIMBS;  // scratch words per thread
+// D = 2Q with a co-Z addition (ZADDU, D kept at the running Z) -- keeps them
+// Jacobian in its scratch with the running product of their Z, inverts that
+// product once, and walks back writing each entry's normalized affine words
+// (Montgomery's batch inversion).  Per entry: one co-Z addition, three
+// multiplications and the affine conversion, against ~25 doublings, ~12
+// additions and one inversion for an entry computed on its own
+// (fb_build_entry; 0.55 s for the 26-bit table that way) -- and the same
+// words, since an entry is the unique normalized affine point (k_fb_check).
+// The run's first entry (a double-and-add) and its inversion are shared by
+// the run's 128 entries (32 before round 6's last change).  Scratch: run_len x
+// 4 field elements (X, Y, Z, prefix product) of raw limbs per thread,
+// limb-major over the grid's threads (coalesced).
+constexpr uint32_t FB_RUN = 128;
+constexpr uint32_t fb_run_len(uint32_t entries) { return entries < FB_RUN ? entries : FB_RUN; }
+constexpr uint32_t fb_run_words(uint32_t run_len) { return run_len * 4 * FE_LIMBS; }  // scratch words per thread
 
 __device__ __forceinline__ void fb_run_store(uint32_t* __restrict__ scr, uint32_t G, uint32_t elem, const fe& a) {
 #pragma unroll
@@ -1720,16 +1725,17 @@ __device__ __forceinline__ void fb_run_load(fe& a, const uint32_t* __restrict__ 
 }
 
 __global__ __launch_bounds__(BLOCK) void k_fb_build_runs(const uint32_t* __restrict__ bases2, uint32_t windows,
-                                                         uint32_t entries, uint32_t* __restrict__ table,
+                                                         uint32_t entries, uint32_t run_len,
+                                                         uint32_t* __restrict__ table,
                                                          uint32_t* __restrict__ scratch) {
   const uint32_t G = gridDim.x * blockDim.x;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* scr = scratch + tid;
-  const uint32_t runs_per_window = entries / FB_RUN;
+  const uint32_t runs_per_window = entries / run_len;
   const uint32_t runs = windows * runs_per_window;
   for (uint32_t run = tid; run < runs; run += G) {
     const uint32_t window = run / runs_per_window;
-    const uint32_t j0 = (run % runs_per_window) * FB_RUN;
+    const uint32_t j0 = (run % runs_per_window) * run_len;
     ge Q, D;
     ge_from_words(Q, bases2 + (size_t)window * 32);
     ge_from_words(D, bases2 + (size_t)window * 32 + 16);
@@ -1742,9 +1748,24 @@ __global__ __launch_bounds__(BLOCK) void k_fb_build_runs(const uint32_t* __restr
       gej_double(P, P);
       if ((m >> b) & 1u) gej_add_ge(P, P, Q);
     }
+    // D = 2Q at P's Z, then each next entry by co-Z addition (ZADDU, 5M + 2S
+    // instead of a mixed addition's 8M + 3S), which moves D to the new Z
+    gej Dz;
+    {
+      fe z2, z3;
+      fe_sqr(z2, P.z);
+      fe_mul(z3, z2, P.z);
+      fe_mul(Dz.x, D.x, z2);
+      fe_mul(Dz.y, D.y, z3);
+      Dz.z = P.z;
+    }
     fe acc;
-    for (uint32_t k = 0; k < FB_RUN; k++) {
-      if (k) gej_add_ge(P, P, D);  // (2 (j0 + k) + 1) Q; never +-D or infinity for j < 2^26
+    for (uint32_t k = 0; k < run_len; k++) {
+      if (k) {  // (2 (j0 + k) + 1) Q; never +-D or infinity for j < 2^26
+        gej nxt;
+        gej_zaddu(nxt, Dz, P);
+        P = nxt;
+      }
       fb_run_store(scr, G, 4 * k + 0, P.x);
       fb_run_store(scr, G, 4 * k + 1, P.y);
       fb_run_store(scr, G, 4 * k + 2, P.z);
@@ -1756,7 +1777,7 @@ __global__ __launch_bounds__(BLOCK) void k_fb_build_runs(const uint32_t* __restr
     }
     fe inv;
     fe_inv(inv, acc);  // 1 / (Z_0 ... Z_{R-1})
-    for (int k = (int)FB_RUN - 1; k >= 0; k--) {
+    for (int k = (int)run_len - 1; k >= 0; k--) {
       gej Pk;
       fb_run_load(Pk.x, scr, G, 4 * k + 0);
       fb_run_load(Pk.y, scr, G, 4 * k + 1);
@@ -2133,11 +2154,12 @@ int ensure_device_table(int device, int bits, const uint32_t** out, bool* built 
                      "or choose 22-bit windows (1.5 GiB; CUDASP_FB_BITS=22)",
                      device, table_bytes / 1e9, bits);
   }
-  // k_fb_build_runs: FB_RUN entries per thread in runs, a grid of 2 blocks
-  // per CU (its scratch, FB_RUN_WORDS per thread, is freed after the build)
+  // k_fb_build_runs: run_len entries per thread in runs, a grid of 2 blocks
+  // per CU (its scratch, fb_run_words(run_len) per thread, is freed after the build)
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-  const uint32_t runs = windows * (entries / FB_RUN);
+  const uint32_t run_len = fb_run_len(entries);
+  const uint32_t runs = windows * (entries / run_len);
   uint32_t blocks = (uint32_t)cus * 2;
   if ((uint64_t)blocks * BLOCK > runs) blocks = (runs + BLOCK - 1) / BLOCK;
   uint32_t* d_bases = nullptr;
@@ -2152,14 +2174,15 @@ int ensure_device_table(int device, int bits, const uint32_t** out, bool* built 
   // work on the device is not serialized behind it (no device-wide synchronize).
   BuildStream bst(stream);
   if (hipMalloc(&d_bases, bases2.size() * 4) != hipSuccess ||
-      hipMalloc(&d_scratch, (size_t)FB_RUN_WORDS * blocks * BLOCK * 4) != hipSuccess ||
+      hipMalloc(&d_scratch, (size_t)fb_run_words(run_len) * blocks * BLOCK * 4) != hipSuccess ||
       (st = bst.st) == nullptr ||
       hipMemcpyAsync(d_bases, bases2.data(), bases2.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
     (void)hipGetLastError();
     cleanup(false);
     return set_error(CUDASP_ERR_HIP, "device %d: fixed-base table build: allocation failed", device);
   }
-  hipLaunchKernelGGL(k_fb_build_runs, dim3(blocks), dim3(BLOCK), 0, st, d_bases, windows, entries, d_table, d_scratch);
+  hipLaunchKernelGGL(k_fb_build_runs, dim3(blocks), dim3(BLOCK), 0, st, d_bases, windows, entries, run_len, d_table,
+                     d_scratch);
   const hipError_t e1 = hipGetLastError();
   const hipError_t e2 = e1 == hipSuccess ? hipStreamSynchronize(st) : e1;
   if (e2 != hipSuccess) {
