@@ -34,6 +34,8 @@ SIGNATURES = {
     "cudasp_scanner_set_fixed_base_bits": (_I32, [_P, _I32]),
     "cudasp_fixed_base_prepare": (_I32, [_I32, _I32, ctypes.POINTER(ctypes.c_double)]),
     "cudasp_debug_fb_check": (_I32, [_I32, _I32, _U32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "cudasp_debug_fold_check": (_I32, [_I32, _I32, ctypes.c_char_p, _U32, ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_uint64)]),
     "cudasp_scanner_fixed_base_bits": (_I32, [_P]),
     "cudasp_scanner_set_spend_fold": (_I32, [_P, _I32]),
     "cudasp_scanner_spend_folded": (_I32, [_P]),

@@ -335,6 +335,12 @@ int cudasp_fixed_base_prepare(int device, int bits, double* build_seconds);
  * double-and-add and an inversion per entry) and compared with the built
  * one; *checked entries, *mismatched of them differ.  Synchronous. */
 int cudasp_debug_fb_check(int device, int bits, uint32_t stride, uint64_t* checked, uint64_t* mismatched);
+/* Test hook: the spend-key fold table of `spend_public_key` (64 bytes, an
+ * on-curve key) at 22 or 26 bits, built as a scanner builds it, and every
+ * stride-th entry (its + B and - B halves) recomputed on its own (one
+ * inversion per entry) and compared.  Synchronous. */
+int cudasp_debug_fold_check(int device, int bits, const uint8_t spend_public_key[64], uint32_t stride,
+                            uint64_t* checked, uint64_t* mismatched);
 
 /* Shader clock of the last k_scan_multi launch on `device` (measurement
  * only): s_memtime ticks over s_memrealtime time of the grid's first wave,

@@ -168,7 +168,7 @@ def test_table_built_in_runs_equals_entries_built_alone(torch, bits, stride):
     """The fixed-base tables are built in runs of consecutive odd multiples
     with one batched inversion per run (k_fb_build_runs); every stride-th
     entry (all of them at 22 and 7 bits; at 26 bits stride 7, which visits
-    every position of a 32-entry run) equals the entry computed on its own
+    every position of a 128-entry run) equals the entry computed on its own
     by double-and-add and its own inversion (k_fb_check)."""
     import ctypes
     from cudasp_amd import _native
@@ -181,3 +181,24 @@ def test_table_built_in_runs_equals_entries_built_alone(torch, bits, stride):
     secs = ctypes.c_double(-1)
     _native.check(lib.cudasp_fixed_base_prepare(0, bits, ctypes.byref(secs)))
     assert secs.value == 0  # already built: nothing to do
+
+
+@pytest.mark.parametrize("bits,stride", [(22, 1), (26, 3)])
+def test_fold_table_built_in_runs_equals_entries_built_alone(torch, bits, stride):
+    """The spend-key fold table (top window + B and - B) is built with one
+    batched inversion per run of 16 entries (k_fb_fold); every stride-th
+    entry's two halves (all of them at 22 bits; at 26 bits stride 3, which
+    visits every position of a run) equal fb_fold_entry's, one inversion per
+    entry (k_fold_check)."""
+    import ctypes
+    from cudasp_amd import _native
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    lib = _native.load()
+    checked, bad = ctypes.c_uint64(), ctypes.c_uint64()
+    _native.check(lib.cudasp_debug_fold_check(0, bits, bench.SPEND_KEY, stride, ctypes.byref(checked),
+                                              ctypes.byref(bad)))
+    top = 1 << (255 - bits * ((256 + bits - 1) // bits - 1))
+    assert checked.value == -(-top // stride)
+    assert bad.value == 0, (bits, bad.value)
