@@ -3254,18 +3254,18 @@ int cudasp_debug_fold_check(int device, int bits, const uint8_t spend_public_key
   SpendWords sw;
   memcpy(sw.w, key.spend, sizeof(sw.w));
   uint32_t* d_bad = nullptr;
-  if (hipMalloc(&d_bad, 4) != hipSuccess) {
-    (void)hipFree(fold);
-    return set_error(CUDASP_ERR_HIP, "allocation failed");
-  }
-  HIP_TRY(hipMemset(d_bad, 0, 4));
-  auto kf = bits == 26 ? k_fold_check<26> : k_fold_check<22>;
-  hipLaunchKernelGGL(kf, dim3(1024), dim3(BLOCK), 0, 0, fb, sw, fold, stride, d_bad);
   uint32_t bad = 0;
-  const hipError_t e = hipGetLastError();
-  const hipError_t e2 = e == hipSuccess ? hipMemcpy(&bad, d_bad, 4, hipMemcpyDeviceToHost) : e;
-  (void)hipFree(d_bad);
-  (void)hipFree(fold);
+  hipError_t e2 = hipMalloc(&d_bad, 4);
+  if (e2 == hipSuccess) e2 = hipMemset(d_bad, 0, 4);
+  if (e2 == hipSuccess) {
+    auto kf = bits == 26 ? k_fold_check<26> : k_fold_check<22>;
+    hipLaunchKernelGGL(kf, dim3(1024), dim3(BLOCK), 0, 0, fb, sw, fold, stride, d_bad);
+    e2 = hipGetLastError();
+  }
+  if (e2 == hipSuccess) e2 = hipMemcpy(&bad, d_bad, 4, hipMemcpyDeviceToHost);
+  (void)hipGetLastError();
+  if (d_bad) (void)hipFree(d_bad);
+  (void)hipFree(fold);  // every path frees both
   if (e2 != hipSuccess) return set_error(CUDASP_ERR_HIP, "fold check failed: %s", hipGetErrorString(e2));
   const uint64_t top = bits == 26 ? FbWidth<26>::TOP_ENTRIES : FbWidth<22>::TOP_ENTRIES;
   *checked = (top + stride - 1) / stride;
